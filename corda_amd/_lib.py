@@ -1,0 +1,112 @@
+"""ctypes binding of libcordahip.so (include/cordahip.h).
+
+The product path has no CPU fallback: if the in-tree HIP library is missing
+or fails to load, every entry point raises `EngineUnavailable` loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcordahip.so")
+
+# lane statuses (CORDAHIP_STATUS_*)
+OK, BAD_SIG, MALFORMED_SIG, BAD_KEY, UNSUPPORTED, EMPTY = 0, 1, 2, 3, 4, 5
+STATUS_NAMES = {OK: "OK", BAD_SIG: "BAD_SIG", MALFORMED_SIG: "MALFORMED_SIG", BAD_KEY: "BAD_KEY",
+                UNSUPPORTED: "UNSUPPORTED", EMPTY: "EMPTY"}
+
+# schemes = Corda SignatureScheme.schemeNumberID (Crypto.kt:77-167)
+RSA_SHA256, ECDSA_SECP256K1_SHA256, ECDSA_SECP256R1_SHA256, EDDSA_ED25519_SHA512, SPHINCS256_SHA256 = 1, 2, 3, 4, 5
+
+SUCCESS = 0
+ERR_NOT_IMPLEMENTED = -7
+
+# every symbol include/cordahip.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "cordahip_abi_version", "cordahip_strerror", "cordahip_init", "cordahip_shutdown",
+    "cordahip_device_count", "cordahip_alloc_pinned", "cordahip_free_pinned", "cordahip_sig_submit",
+    "cordahip_wait", "cordahip_poll", "cordahip_sig_verify", "cordahip_ed25519_verify_device",
+    "cordahip_ed25519_verify_host", "cordahip_ed25519_sign_device", "cordahip_last_kernel_ms",
+]
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__("%s failed: %s (%d)" % (what, strerror(code), code))
+        self.code = code
+
+
+class SigBatch(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("scheme", ctypes.c_void_p),
+        ("key", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
+        ("sig", ctypes.c_void_p), ("sig_off", ctypes.c_void_p),
+        ("msg", ctypes.c_void_p), ("msg_off", ctypes.c_void_p),
+        ("status", ctypes.c_void_p),
+        ("verdict", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineUnavailable("%s not built (run __graft_entry__.build())" % LIB_PATH)
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7
+    # (same SONAME as /opt/rocm's). Loading torch first makes the dynamic linker
+    # bind libcordahip.so to that already-loaded runtime, so torch tensors,
+    # streams and RCCL share one HIP/HSA instance with our kernels.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    try:
+        l = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        raise EngineUnavailable("cannot load %s: %s" % (LIB_PATH, e))
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "cordahip_abi_version": (u32, []),
+        "cordahip_strerror": (ctypes.c_char_p, [i32]),
+        "cordahip_init": (i32, [u32, ctypes.POINTER(vp)]),
+        "cordahip_shutdown": (None, [vp]),
+        "cordahip_device_count": (i32, [vp]),
+        "cordahip_alloc_pinned": (i32, [vp, ctypes.c_size_t, ctypes.POINTER(vp)]),
+        "cordahip_free_pinned": (i32, [vp, vp]),
+        "cordahip_sig_submit": (i32, [vp, ctypes.POINTER(SigBatch), ctypes.POINTER(u64)]),
+        "cordahip_wait": (i32, [vp, u64, ctypes.c_int64]),
+        "cordahip_poll": (i32, [vp, u64]),
+        "cordahip_sig_verify": (i32, [vp, ctypes.POINTER(SigBatch)]),
+        "cordahip_ed25519_verify_device": (i32, [vp, i32, vp, vp, vp, u32, u64, vp, vp, vp]),
+        "cordahip_ed25519_verify_host": (i32, [vp, vp, vp, vp, u32, u64, vp, vp]),
+        "cordahip_ed25519_sign_device": (i32, [vp, i32, vp, vp, u32, u64, vp, vp, vp]),
+        "cordahip_last_kernel_ms": (ctypes.c_double, [vp, i32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(l, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = l
+    return l
+
+
+def strerror(code: int) -> str:
+    try:
+        return lib().cordahip_strerror(code).decode()
+    except EngineUnavailable:
+        return "engine unavailable"
+
+
+def check(code: int, what: str) -> None:
+    if code != SUCCESS:
+        raise EngineError(code, what)

@@ -1,0 +1,383 @@
+// libcordahip.so host runtime: contexts, devices, streams, pinned memory,
+// batch partitioning and the C-ABI of include/cordahip.h.
+//
+// MI355X-first shape: one context drives the devices named by its mask; a
+// dense batch is split into contiguous 64-aligned shards, one per device, and
+// each shard streams through two HIP streams in fixed chunks (H2D of chunk
+// k+1 overlaps the kernel of chunk k). Device buffers are grow-only per
+// device and reused across calls; the Ed25519 base-point table is built once
+// per device at init by a kernel. There is no CPU verification fallback:
+// a HIP failure is returned to the caller as CORDAHIP_ERR_HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <future>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/cordahip.h"
+#include "status.hpp"
+
+namespace cordahip {
+hipError_t launch_ed25519_btable(uint32_t* tab, hipStream_t s);
+size_t ed25519_btable_bytes();
+hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
+                                 uint64_t n, const uint32_t* btab, const uint8_t* pre_status, uint8_t* status,
+                                 unsigned long long* verdict, hipStream_t s);
+hipError_t launch_ed25519_sign(const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len, uint64_t n,
+                               const uint32_t* btab, uint8_t* pubs, uint8_t* sigs, hipStream_t s);
+}  // namespace cordahip
+
+using namespace cordahip;
+
+namespace {
+
+constexpr uint64_t kChunk = 1ull << 20;  // lanes per pipelined chunk (128 MiB of Ed25519 input)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+struct Stage {  // one pipeline slot: device buffers + its stream
+  hipStream_t stream = nullptr;
+  DevBuf keys, sigs, msgs, pre, status, verdict;
+};
+
+struct Device {
+  int id = 0;
+  uint32_t* btab = nullptr;
+  hipStream_t stream = nullptr;  // default stream for *_device calls
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_ms = -1.0;
+  std::mutex mu;  // serialises host-path use of the stages
+  Stage stage[2];
+};
+
+int hip_err(hipError_t e) { return e == hipSuccess ? CORDAHIP_SUCCESS : CORDAHIP_ERR_HIP; }
+
+}  // namespace
+
+struct cordahip_ctx {
+  std::vector<std::unique_ptr<Device>> devs;
+  std::mutex mu;
+  uint64_t next_ticket = 1;
+  std::unordered_map<uint64_t, std::shared_future<int>> jobs;
+};
+
+namespace {
+
+// Dense Ed25519 shard on one device: [lo, hi) of the caller's host arrays.
+int verify_shard_host(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
+                      const uint8_t* pre, uint64_t lo, uint64_t hi, uint8_t* status, uint64_t* verdict) {
+  std::lock_guard<std::mutex> g(d.mu);
+  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  const uint64_t chunk = kChunk;
+  for (int s = 0; s < 2; s++) {
+    Stage& st = d.stage[s];
+    if (!st.stream && hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)
+      return CORDAHIP_ERR_HIP;
+    const uint64_t c = std::min<uint64_t>(chunk, hi - lo);
+    if (st.keys.ensure(c * 32) || st.sigs.ensure(c * 64) || st.msgs.ensure(std::max<uint64_t>(c * msg_len, 16)) ||
+        st.pre.ensure(c) || st.status.ensure(c) || st.verdict.ensure(((c + 63) / 64) * 8))
+      return CORDAHIP_ERR_OUT_OF_MEMORY;
+  }
+  int k = 0;
+  std::vector<uint64_t> vtmp;
+  for (uint64_t off = lo; off < hi; off += chunk, k ^= 1) {
+    Stage& st = d.stage[k];
+    const uint64_t c = std::min<uint64_t>(chunk, hi - off);
+    hipStream_t s = st.stream;
+    hipError_t e = hipSuccess;
+    e = e ? e : hipMemcpyAsync(st.keys.p, keys + off * 32, c * 32, hipMemcpyHostToDevice, s);
+    e = e ? e : hipMemcpyAsync(st.sigs.p, sigs + off * 64, c * 64, hipMemcpyHostToDevice, s);
+    if (msg_len) e = e ? e : hipMemcpyAsync(st.msgs.p, msgs + off * msg_len, c * msg_len, hipMemcpyHostToDevice, s);
+    if (pre) e = e ? e : hipMemcpyAsync(st.pre.p, pre + off, c, hipMemcpyHostToDevice, s);
+    const bool aligned = (off % 64) == 0;
+    e = e ? e
+          : launch_ed25519_verify(st.keys.as<uint8_t>(), st.sigs.as<uint8_t>(), st.msgs.as<uint8_t>(), msg_len, c,
+                                  d.btab, pre ? st.pre.as<uint8_t>() : nullptr, st.status.as<uint8_t>(),
+                                  st.verdict.as<unsigned long long>(), s);
+    e = e ? e : hipMemcpyAsync(status + off, st.status.p, c, hipMemcpyDeviceToHost, s);
+    if (verdict && aligned)
+      e = e ? e : hipMemcpyAsync(verdict + off / 64, st.verdict.p, ((c + 63) / 64) * 8, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return CORDAHIP_ERR_HIP;
+    // the other stage may be reused next iteration: make sure it is idle
+    if (hipStreamSynchronize(d.stage[k ^ 1].stream) != hipSuccess) return CORDAHIP_ERR_HIP;
+  }
+  for (int s = 0; s < 2; s++)
+    if (hipStreamSynchronize(d.stage[s].stream) != hipSuccess) return CORDAHIP_ERR_HIP;
+  return CORDAHIP_SUCCESS;
+}
+
+void verdict_from_status(const uint8_t* status, uint64_t n, uint64_t* verdict) {
+  for (uint64_t w = 0; w < (n + 63) / 64; w++) {
+    uint64_t m = 0;
+    for (uint64_t b = 0; b < 64 && w * 64 + b < n; b++)
+      if (status[w * 64 + b] == CORDAHIP_STATUS_OK) m |= 1ull << b;
+    verdict[w] = m;
+  }
+}
+
+int ed25519_dense_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
+                       uint32_t msg_len, const uint8_t* pre, uint64_t n, uint8_t* status, uint64_t* verdict) {
+  if (n == 0) return CORDAHIP_SUCCESS;
+  const uint64_t nd = ctx->devs.size();
+  // contiguous 64-aligned shards: no cross-device dependency
+  const uint64_t per = ((n + nd - 1) / nd + 63) / 64 * 64;
+  std::vector<std::future<int>> fs;
+  for (uint64_t i = 0; i < nd; i++) {
+    const uint64_t lo = std::min(n, i * per), hi = std::min(n, lo + per);
+    if (lo >= hi) break;
+    Device* d = ctx->devs[i].get();
+    fs.push_back(std::async(std::launch::async, [=] {
+      return verify_shard_host(*d, keys, sigs, msgs, msg_len, pre, lo, hi, status, verdict);
+    }));
+  }
+  int rc = CORDAHIP_SUCCESS;
+  for (auto& f : fs) {
+    const int r = f.get();
+    if (r != CORDAHIP_SUCCESS) rc = r;
+  }
+  // chunk boundaries are 64-aligned except possibly a shard tail; recompute
+  // the verdict words from status so every word is exact
+  if (rc == CORDAHIP_SUCCESS && verdict) verdict_from_status(status, n, verdict);
+  return rc;
+}
+
+// Generic CSR batch: host-side scheme partition and length checks (the
+// Crypto.doVerify require() checks), then one dense device launch per
+// (scheme, message length) group.
+int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
+  const uint64_t n = b->n;
+  if (n == 0) return CORDAHIP_SUCCESS;
+  if (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off || !b->msg || !b->msg_off || !b->status)
+    return CORDAHIP_ERR_INVALID_ARG;
+  std::map<uint64_t, std::vector<uint64_t>> ed_groups;  // msg length -> lanes
+  for (uint64_t i = 0; i < n; i++) {
+    const uint8_t sch = b->scheme[i];
+    if (sch == CORDAHIP_SCHEME_ECDSA_SECP256K1_SHA256 || sch == CORDAHIP_SCHEME_ECDSA_SECP256R1_SHA256)
+      return CORDAHIP_ERR_NOT_IMPLEMENTED;  // caller keeps these batches on the JVM path
+    if (sch != CORDAHIP_SCHEME_EDDSA_ED25519_SHA512) {
+      b->status[i] = CORDAHIP_STATUS_UNSUPPORTED;  // Crypto.kt:474 require(isSupportedSignatureScheme)
+      continue;
+    }
+    if (b->key_off[i + 1] - b->key_off[i] != 32) {
+      b->status[i] = CORDAHIP_STATUS_BAD_KEY;  // EdDSAPublicKeySpec: "public-key length is wrong"
+      continue;
+    }
+    ed_groups[b->msg_off[i + 1] - b->msg_off[i]].push_back(i);
+  }
+  for (auto& kv : ed_groups) {
+    const uint64_t mlen = kv.first;
+    const auto& idx = kv.second;
+    const uint64_t m = idx.size();
+    if (mlen > 0xffffffffull) return CORDAHIP_ERR_INVALID_ARG;
+    std::vector<uint8_t> keys(m * 32), sigs(m * 64, 0), msgs(std::max<uint64_t>(m * mlen, 1)), pre(m, 0), st(m);
+    for (uint64_t j = 0; j < m; j++) {
+      const uint64_t i = idx[j];
+      std::memcpy(&keys[j * 32], b->key + b->key_off[i], 32);
+      const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
+      if (sl == 0 || mlen == 0) pre[j] = CORDAHIP_STATUS_EMPTY;          // Crypto.kt:475-476
+      else if (sl != 64) pre[j] = CORDAHIP_STATUS_MALFORMED_SIG;         // EdDSAEngine length check
+      else std::memcpy(&sigs[j * 64], b->sig + b->sig_off[i], 64);
+      if (mlen) std::memcpy(&msgs[j * mlen], b->msg + b->msg_off[i], mlen);
+    }
+    const int rc = ed25519_dense_host(ctx, keys.data(), sigs.data(), msgs.data(), (uint32_t)mlen, pre.data(), m,
+                                      st.data(), nullptr);
+    if (rc != CORDAHIP_SUCCESS) return rc;
+    for (uint64_t j = 0; j < m; j++) b->status[idx[j]] = st[j];
+  }
+  if (b->verdict) verdict_from_status(b->status, n, b->verdict);
+  return CORDAHIP_SUCCESS;
+}
+
+Device* dev_at(cordahip_ctx* ctx, int device) {
+  if (!ctx || device < 0 || device >= (int)ctx->devs.size()) return nullptr;
+  return ctx->devs[device].get();
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t cordahip_abi_version(void) { return CORDAHIP_ABI_VERSION; }
+
+const char* cordahip_strerror(int code) {
+  switch (code) {
+    case CORDAHIP_SUCCESS: return "success";
+    case CORDAHIP_ERR_INVALID_ARG: return "invalid argument";
+    case CORDAHIP_ERR_HIP: return "HIP runtime error";
+    case CORDAHIP_ERR_NO_DEVICE: return "no usable HIP device";
+    case CORDAHIP_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case CORDAHIP_ERR_TIMEOUT: return "timed out";
+    case CORDAHIP_ERR_UNKNOWN_TICKET: return "unknown ticket";
+    case CORDAHIP_ERR_NOT_IMPLEMENTED: return "not implemented on the GPU path";
+    default: return "unknown error";
+  }
+}
+
+int cordahip_init(uint32_t device_mask, cordahip_ctx** out) {
+  if (!out) return CORDAHIP_ERR_INVALID_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return CORDAHIP_ERR_NO_DEVICE;
+  auto ctx = std::make_unique<cordahip_ctx>();
+  for (int d = 0; d < count && d < 32; d++) {
+    if (device_mask && !((device_mask >> d) & 1u)) continue;
+    auto dev = std::make_unique<Device>();
+    dev->id = d;
+    if (hipSetDevice(d) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (hipEventCreate(&dev->ev0) != hipSuccess || hipEventCreate(&dev->ev1) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (hipMalloc(reinterpret_cast<void**>(&dev->btab), ed25519_btable_bytes()) != hipSuccess)
+      return CORDAHIP_ERR_OUT_OF_MEMORY;
+    if (launch_ed25519_btable(dev->btab, dev->stream) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (hipStreamSynchronize(dev->stream) != hipSuccess) return CORDAHIP_ERR_HIP;
+    ctx->devs.push_back(std::move(dev));
+  }
+  if (ctx->devs.empty()) return CORDAHIP_ERR_NO_DEVICE;
+  *out = ctx.release();
+  return CORDAHIP_SUCCESS;
+}
+
+void cordahip_shutdown(cordahip_ctx* ctx) {
+  if (!ctx) return;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    for (auto& kv : ctx->jobs) kv.second.wait();
+    ctx->jobs.clear();
+  }
+  for (auto& d : ctx->devs) {
+    hipSetDevice(d->id);
+    for (auto& st : d->stage) {
+      for (DevBuf* b : {&st.keys, &st.sigs, &st.msgs, &st.pre, &st.status, &st.verdict})
+        if (b->p) hipFree(b->p);
+      if (st.stream) hipStreamDestroy(st.stream);
+    }
+    if (d->btab) hipFree(d->btab);
+    if (d->ev0) hipEventDestroy(d->ev0);
+    if (d->ev1) hipEventDestroy(d->ev1);
+    if (d->stream) hipStreamDestroy(d->stream);
+  }
+  delete ctx;
+}
+
+int cordahip_device_count(const cordahip_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int cordahip_alloc_pinned(cordahip_ctx* ctx, size_t bytes, void** host) {
+  if (!ctx || !host) return CORDAHIP_ERR_INVALID_ARG;
+  return hipHostMalloc(host, bytes, hipHostMallocPortable) == hipSuccess ? CORDAHIP_SUCCESS
+                                                                          : CORDAHIP_ERR_OUT_OF_MEMORY;
+}
+
+int cordahip_free_pinned(cordahip_ctx* ctx, void* host) {
+  if (!ctx) return CORDAHIP_ERR_INVALID_ARG;
+  return hip_err(hipHostFree(host));
+}
+
+int cordahip_sig_verify(cordahip_ctx* ctx, const cordahip_sig_batch* batch) {
+  if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
+  return sig_verify_impl(ctx, batch);
+}
+
+int cordahip_sig_submit(cordahip_ctx* ctx, const cordahip_sig_batch* batch, uint64_t* ticket) {
+  if (!ctx || !batch || !ticket) return CORDAHIP_ERR_INVALID_ARG;
+  const cordahip_sig_batch copy = *batch;  // descriptor by value; buffers stay caller-owned
+  std::shared_future<int> f = std::async(std::launch::async, [ctx, copy] { return sig_verify_impl(ctx, &copy); });
+  std::lock_guard<std::mutex> g(ctx->mu);
+  *ticket = ctx->next_ticket++;
+  ctx->jobs.emplace(*ticket, f);
+  return CORDAHIP_SUCCESS;
+}
+
+int cordahip_wait(cordahip_ctx* ctx, uint64_t ticket, int64_t timeout_ns) {
+  if (!ctx) return CORDAHIP_ERR_INVALID_ARG;
+  std::shared_future<int> f;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    auto it = ctx->jobs.find(ticket);
+    if (it == ctx->jobs.end()) return CORDAHIP_ERR_UNKNOWN_TICKET;
+    f = it->second;
+  }
+  if (timeout_ns >= 0 && f.wait_for(std::chrono::nanoseconds(timeout_ns)) != std::future_status::ready)
+    return CORDAHIP_ERR_TIMEOUT;
+  const int rc = f.get();
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->jobs.erase(ticket);
+  return rc;
+}
+
+int cordahip_poll(cordahip_ctx* ctx, uint64_t ticket) {
+  if (!ctx) return CORDAHIP_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  auto it = ctx->jobs.find(ticket);
+  if (it == ctx->jobs.end()) return CORDAHIP_ERR_UNKNOWN_TICKET;
+  return it->second.wait_for(std::chrono::seconds(0)) == std::future_status::ready ? 1 : 0;
+}
+
+int cordahip_ed25519_verify_device(cordahip_ctx* ctx, int device, const void* d_keys, const void* d_sigs,
+                                   const void* d_msgs, uint32_t msg_len, uint64_t n, void* d_status,
+                                   void* d_verdict, void* hip_stream) {
+  Device* d = dev_at(ctx, device);
+  if (!d || (!d_keys && n) || (!d_sigs && n) || (!d_status && n)) return CORDAHIP_ERR_INVALID_ARG;
+  if ((reinterpret_cast<uintptr_t>(d_keys) | reinterpret_cast<uintptr_t>(d_sigs)) & 15)
+    return CORDAHIP_ERR_INVALID_ARG;
+  if (msg_len == 32 && (reinterpret_cast<uintptr_t>(d_msgs) & 15)) return CORDAHIP_ERR_INVALID_ARG;
+  if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : d->stream;
+  hipError_t e = hipEventRecord(d->ev0, s);
+  e = e ? e
+        : launch_ed25519_verify(static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
+                                static_cast<const uint8_t*>(d_msgs), msg_len, n, d->btab, nullptr,
+                                static_cast<uint8_t*>(d_status), static_cast<unsigned long long*>(d_verdict), s);
+  e = e ? e : hipEventRecord(d->ev1, s);
+  return hip_err(e);
+}
+
+double cordahip_last_kernel_ms(cordahip_ctx* ctx, int device) {
+  Device* d = dev_at(ctx, device);
+  if (!d) return -1.0;
+  if (hipEventSynchronize(d->ev1) != hipSuccess) return -1.0;
+  float ms = -1.f;
+  if (hipEventElapsedTime(&ms, d->ev0, d->ev1) != hipSuccess) return -1.0;
+  return ms;
+}
+
+int cordahip_ed25519_verify_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
+                                 uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict) {
+  if (!ctx || (n && (!keys || !sigs || !status || (msg_len && !msgs)))) return CORDAHIP_ERR_INVALID_ARG;
+  return ed25519_dense_host(ctx, keys, sigs, msgs, msg_len, nullptr, n, status, verdict);
+}
+
+int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_seeds, const void* d_msgs,
+                                 uint32_t msg_len, uint64_t n, void* d_pubs, void* d_sigs, void* hip_stream) {
+  Device* d = dev_at(ctx, device);
+  if (!d || (n && (!d_seeds || !d_pubs || !d_sigs))) return CORDAHIP_ERR_INVALID_ARG;
+  if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : d->stream;
+  return hip_err(launch_ed25519_sign(static_cast<const uint8_t*>(d_seeds), static_cast<const uint8_t*>(d_msgs),
+                                     msg_len, n, d->btab, static_cast<uint8_t*>(d_pubs),
+                                     static_cast<uint8_t*>(d_sigs), s));
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+"""Python handle on a libcordahip context (plumbing for tests and bench.py).
+
+`Engine` owns one `cordahip_ctx`. Host batches go through the C-ABI's
+generic CSR batch (`cordahip_sig_verify`, the `Crypto.isValid` batch
+replacement) or the dense Ed25519 host path; device batches take torch
+tensors that already live in HBM and run on the caller's HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import EngineError, SigBatch, check, lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+class Engine:
+    def __init__(self, device_mask: int = 0):
+        l = lib()
+        self._ctx = ctypes.c_void_p()
+        check(l.cordahip_init(device_mask, ctypes.byref(self._ctx)), "cordahip_init")
+
+    def close(self):
+        if self._ctx:
+            lib().cordahip_shutdown(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    def device_count(self) -> int:
+        return lib().cordahip_device_count(self._ctx)
+
+    # ---- generic batch: Crypto.isValid per lane -------------------------------
+    @staticmethod
+    def _csr(items: Sequence[bytes]):
+        off = np.zeros(len(items) + 1, dtype=np.uint64)
+        if items:
+            off[1:] = np.cumsum([len(x) for x in items], dtype=np.uint64)
+        blob = np.frombuffer(b"".join(items), dtype=np.uint8) if off[-1] else np.zeros(1, np.uint8)
+        return np.ascontiguousarray(blob), off
+
+    def verify_batch(self, schemes: Sequence[int], keys: Sequence[bytes], sigs: Sequence[bytes],
+                     msgs: Sequence[bytes], async_: bool = False):
+        """Per-lane statuses for (scheme, key, sig, msg) tuples; returns (status, verdict)."""
+        n = len(keys)
+        sch = np.ascontiguousarray(np.asarray(schemes, dtype=np.uint8))
+        kb, ko = self._csr(list(keys))
+        sb, so = self._csr(list(sigs))
+        mb, mo = self._csr(list(msgs))
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        verdict = np.zeros(max((n + 63) // 64, 1), dtype=np.uint64)
+        b = SigBatch(n, _ptr(sch), _ptr(kb), _ptr(ko), _ptr(sb), _ptr(so), _ptr(mb), _ptr(mo),
+                     _ptr(status), _ptr(verdict))
+        keep = (sch, kb, ko, sb, so, mb, mo, status, verdict, b)
+        if async_:
+            t = ctypes.c_uint64()
+            check(lib().cordahip_sig_submit(self._ctx, ctypes.byref(b), ctypes.byref(t)), "cordahip_sig_submit")
+            return Ticket(self, t.value, status[:n], verdict, keep)
+        check(lib().cordahip_sig_verify(self._ctx, ctypes.byref(b)), "cordahip_sig_verify")
+        return status[:n], verdict
+
+    # ---- dense Ed25519 host path ---------------------------------------------
+    def ed25519_verify_host(self, keys: np.ndarray, sigs: np.ndarray, msgs: np.ndarray):
+        keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 32)
+        n = keys.shape[0]
+        sigs = np.ascontiguousarray(sigs, dtype=np.uint8).reshape(n, 64)
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8).reshape(n, -1)
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        verdict = np.zeros(max((n + 63) // 64, 1), dtype=np.uint64)
+        check(lib().cordahip_ed25519_verify_host(self._ctx, _ptr(keys), _ptr(sigs), _ptr(msgs), msgs.shape[1], n,
+                                                 _ptr(status), _ptr(verdict)), "cordahip_ed25519_verify_host")
+        return status[:n], verdict
+
+    # ---- device-resident paths (torch tensors in HBM) -------------------------
+    def ed25519_verify_device(self, keys, sigs, msgs, status, verdict=None, device: int = 0, stream=None):
+        n = keys.shape[0]
+        s = stream.cuda_stream if stream is not None else 0
+        check(lib().cordahip_ed25519_verify_device(
+            self._ctx, device, keys.data_ptr(), sigs.data_ptr(), msgs.data_ptr(), msgs.shape[1], n,
+            status.data_ptr(), verdict.data_ptr() if verdict is not None else None, s),
+            "cordahip_ed25519_verify_device")
+
+    def ed25519_sign_device(self, seeds, msgs, pubs, sigs, device: int = 0, stream=None):
+        n = seeds.shape[0]
+        s = stream.cuda_stream if stream is not None else 0
+        check(lib().cordahip_ed25519_sign_device(self._ctx, device, seeds.data_ptr(), msgs.data_ptr(),
+                                                 msgs.shape[1], n, pubs.data_ptr(), sigs.data_ptr(), s),
+              "cordahip_ed25519_sign_device")
+
+    def last_kernel_ms(self, device: int = 0) -> float:
+        return lib().cordahip_last_kernel_ms(self._ctx, device)
+
+
+class Ticket:
+    def __init__(self, eng: Engine, ticket: int, status, verdict, keep):
+        self.eng, self.ticket, self.status, self.verdict, self._keep = eng, ticket, status, verdict, keep
+
+    def poll(self) -> bool:
+        r = lib().cordahip_poll(self.eng.ctx, self.ticket)
+        if r < 0:
+            raise EngineError(r, "cordahip_poll")
+        return r == 1
+
+    def wait(self, timeout_ns: int = -1):
+        check(lib().cordahip_wait(self.eng.ctx, self.ticket, timeout_ns), "cordahip_wait")
+        return self.status, self.verdict

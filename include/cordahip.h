@@ -1,0 +1,136 @@
+/* cordahip.h — C-ABI of libcordahip.so, the MI355X batch signature and
+ * transaction-id verification engine for Corda's hot path.
+ *
+ * Drop-in boundary. Every entry point is plain C: pointers,
+ * sizes, status codes; no C++ types or exceptions cross it, so a JNI shim (see
+ * INTEGRATION.md) or ctypes binds it directly. The entry points replace:
+ *
+ *   cordahip_sig_submit / cordahip_sig_verify
+ *       -> Crypto.isValid(scheme, key, sig, clear)   core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:534-541
+ *          Crypto.doVerify(scheme, key, sig, clear)  Crypto.kt:472-483
+ *          (one call per signature today, through the JCA SPI at Crypto.kt:537-540;
+ *           here: one call per BATCH, per-lane status instead of throw/false)
+ *   cordahip_ed25519_verify_device / _host
+ *       -> the EDDSA_ED25519_SHA512 lane of the above (Crypto.kt:119-132), dense layout
+ *   cordahip_ed25519_sign_device
+ *       -> Crypto.doSign(EDDSA_ED25519_SHA512, ...) (Crypto.kt:380-400) and
+ *          deriveKeyPairFromEntropy (Crypto.kt:733-739): corpus generation only
+ *   cordahip_tx_ids (tx id = Merkle root of component hashes)
+ *       -> WireTransaction.id (WireTransaction.kt:48) = MerkleTree.getMerkleTree(
+ *          availableComponentHashes).hash (MerkleTree.kt:27-66, MerkleTransaction.kt:69)
+ *   cordahip_signed_tx_verify
+ *       -> SignedTransaction.checkSignaturesAreValid (SignedTransaction.kt:95-100)
+ *          + the tx.id recomputation of verifySignatures (:70-85); signer coverage
+ *          (getMissingSignatures :102-108) stays with the caller, see INTEGRATION.md
+ *
+ * Result contract: a return value < 0 means the whole call failed (the caller
+ * falls back to the JVM path for that batch); per-lane outcomes are DATA in
+ * status[] (CORDAHIP_STATUS_*), never return codes.
+ *
+ * Ownership: the caller owns every host buffer and must leave it untouched
+ * until cordahip_wait()/poll() reports the ticket done. Buffers from
+ * cordahip_alloc_pinned() are page-locked (hipHostMalloc) and are the fast
+ * path for host batches. The library owns device memory and HIP streams.
+ * A context is thread-safe: submit/wait/poll from any thread.
+ */
+#ifndef CORDAHIP_H
+#define CORDAHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CORDAHIP_ABI_VERSION 1u
+
+/* ---- per-lane statuses (status[i]) ------------------------------------- */
+#define CORDAHIP_STATUS_OK 0            /* isValid -> true;  doVerify -> true                         */
+#define CORDAHIP_STATUS_BAD_SIG 1       /* isValid -> false; doVerify -> SignatureException            */
+#define CORDAHIP_STATUS_MALFORMED_SIG 2 /* SignatureException from the engine (bad length / DER)       */
+#define CORDAHIP_STATUS_BAD_KEY 3       /* key decode failed (IllegalArgumentException at key build)   */
+#define CORDAHIP_STATUS_UNSUPPORTED 4   /* IllegalArgumentException: unsupported scheme (Crypto.kt:474)*/
+#define CORDAHIP_STATUS_EMPTY 5         /* IllegalArgumentException: empty sig / clear (Crypto.kt:475) */
+
+/* ---- return codes -------------------------------------------------------- */
+#define CORDAHIP_SUCCESS 0
+#define CORDAHIP_ERR_INVALID_ARG (-1)
+#define CORDAHIP_ERR_HIP (-2)
+#define CORDAHIP_ERR_NO_DEVICE (-3)
+#define CORDAHIP_ERR_OUT_OF_MEMORY (-4)
+#define CORDAHIP_ERR_TIMEOUT (-5)
+#define CORDAHIP_ERR_UNKNOWN_TICKET (-6)
+#define CORDAHIP_ERR_NOT_IMPLEMENTED (-7)
+
+/* ---- signature schemes = Corda SignatureScheme.schemeNumberID ------------ */
+#define CORDAHIP_SCHEME_RSA_SHA256 1             /* Crypto.kt:77  (not on GPU -> UNSUPPORTED lane) */
+#define CORDAHIP_SCHEME_ECDSA_SECP256K1_SHA256 2 /* Crypto.kt:92  */
+#define CORDAHIP_SCHEME_ECDSA_SECP256R1_SHA256 3 /* Crypto.kt:106 */
+#define CORDAHIP_SCHEME_EDDSA_ED25519_SHA512 4   /* Crypto.kt:120 */
+#define CORDAHIP_SCHEME_SPHINCS256_SHA256 5      /* Crypto.kt:140 (not on GPU -> UNSUPPORTED lane) */
+
+typedef struct cordahip_ctx cordahip_ctx;
+
+uint32_t cordahip_abi_version(void);
+const char* cordahip_strerror(int code);
+
+/* device_mask: bit d selects visible HIP device d; 0 = all visible devices. */
+int cordahip_init(uint32_t device_mask, cordahip_ctx** out);
+void cordahip_shutdown(cordahip_ctx* ctx);
+int cordahip_device_count(const cordahip_ctx* ctx);
+
+int cordahip_alloc_pinned(cordahip_ctx* ctx, size_t bytes, void** host);
+int cordahip_free_pinned(cordahip_ctx* ctx, void* host);
+
+/* ---- generic signature batch (host memory) ------------------------------ *
+ * Variable-length fields are CSR: item i's key is key[key_off[i] .. key_off[i+1]).
+ * Key encodings: Ed25519 = the 32-byte A (Kryo wire form, Kryo.kt:386); ECDSA =
+ * SEC1 point (the SPKI BIT STRING payload, Crypto.kt:348-355).
+ * verdict (optional): bit (i % 64) of word (i / 64) = (status[i] == OK).     */
+typedef struct {
+  uint64_t n;
+  const uint8_t* scheme; /* [n] CORDAHIP_SCHEME_* */
+  const uint8_t* key;
+  const uint64_t* key_off; /* [n+1] */
+  const uint8_t* sig;
+  const uint64_t* sig_off; /* [n+1] */
+  const uint8_t* msg;
+  const uint64_t* msg_off; /* [n+1] */
+  uint8_t* status;         /* [n] out */
+  uint64_t* verdict;       /* [(n+63)/64] out, may be NULL */
+} cordahip_sig_batch;
+
+int cordahip_sig_submit(cordahip_ctx* ctx, const cordahip_sig_batch* batch, uint64_t* ticket);
+/* timeout_ns < 0: wait forever. Returns the batch's result code. */
+int cordahip_wait(cordahip_ctx* ctx, uint64_t ticket, int64_t timeout_ns);
+/* 1 = done (result retrievable with wait), 0 = pending, < 0 = error */
+int cordahip_poll(cordahip_ctx* ctx, uint64_t ticket);
+/* synchronous submit + wait */
+int cordahip_sig_verify(cordahip_ctx* ctx, const cordahip_sig_batch* batch);
+
+/* ---- dense Ed25519 paths -------------------------------------------------- *
+ * keys n*32 B, sigs n*64 B (R || S), msgs n*msg_len B, all row-major.
+ * _device: pointers are device (HBM) memory on `device`; 16-byte aligned;
+ *          runs on hip_stream (NULL = the context's stream for that device);
+ *          asynchronous w.r.t. the host.
+ * _host:   host pointers (pinned recommended); shards over all context devices,
+ *          pipelines H2D copy / kernel / D2H copy in chunks; synchronous.   */
+int cordahip_ed25519_verify_device(cordahip_ctx* ctx, int device, const void* d_keys, const void* d_sigs,
+                                   const void* d_msgs, uint32_t msg_len, uint64_t n, void* d_status,
+                                   void* d_verdict, void* hip_stream);
+int cordahip_ed25519_verify_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
+                                 uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict);
+
+/* RFC 8032 keygen + sign from 32-byte seeds (device memory): corpus generation. */
+int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_seeds, const void* d_msgs,
+                                 uint32_t msg_len, uint64_t n, void* d_pubs, void* d_sigs, void* hip_stream);
+
+/* Device time of the last kernel launched by the context on `device` (ms), measured
+ * with HIP events on the stream the kernel ran on; -1 if unavailable. */
+double cordahip_last_kernel_ms(cordahip_ctx* ctx, int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CORDAHIP_H */

@@ -1,0 +1,127 @@
+"""Pins the oracle (test infrastructure) before anything is checked against it.
+
+* oracle/c (the fast restatement) == the committed golden statuses, which come
+  from oracle/i2p_ed25519.py and are cross-checked with OpenSSL 3 wherever
+  RFC 8032 and i2p 0.2.0 agree (tests/golden/make_ed25519_vectors.py).
+* The pure-Python restatement reproduces the golden file on a sample.
+* SHA-2 vs hashlib; slide() C vs Python; the reference's structural Merkle
+  tests (PartialMerkleTreeTest.kt:56-81).
+"""
+import ctypes
+import hashlib
+import random
+
+import pytest
+
+import i2p_ed25519 as ed
+
+
+def test_c_oracle_matches_golden(oracle, ed_vectors):
+    for v in ed_vectors:
+        p, s, m = v["pub"], v["sig"], v["msg"]
+        assert oracle.oracle_ed25519_verify(p, len(p), s, len(s), m, len(m)) == v["status"], (v["cat"], v["note"])
+
+
+def test_python_oracle_matches_golden_sample(ed_vectors):
+    rng = random.Random(3)
+    for v in rng.sample(ed_vectors, 60):
+        assert ed.verify_status(v["pub"], v["sig"], v["msg"]) == v["status"], (v["cat"], v["note"])
+
+
+def test_openssl_agreement_recorded(ed_vectors):
+    agree = {"valid", "fixed_key", "r_bitflip", "s_bitflip", "msg_bitflip", "wrong_key", "sig0_increment",
+             "long_msg", "random_sig"}
+    n = 0
+    for v in ed_vectors:
+        if v["cat"] in agree:
+            assert v["openssl"] == (v["status"] == 0)
+            n += 1
+    assert n > 150
+
+
+def test_golden_catalogue_covers_semantics(ed_vectors):
+    cats = {(v["cat"], v["status"]) for v in ed_vectors}
+    # S + kL: accepted without slide overflow, rejected with it (i2p 0.2.0, no S < L check)
+    assert ("s_plus_kL", 0) in cats and ("s_plus_kL", 1) in cats
+    assert ("key_noncanonical_y", 0) in cats  # y >= p accepted, canonical re-encoding hashed
+    assert ("key_mixed_order", 0) in cats and ("key_mixed_order", 1) in cats  # cofactorless
+    assert ("key_identity_signbit", 0) in cats
+    for st in (0, 1, 2, 3, 5):
+        assert any(v["status"] == st for v in ed_vectors)
+
+
+def test_structural_reference_cases(oracle):
+    # CryptoUtilsTest.kt:233-286: round trip, empty -> throw, sig[0]++ -> reject
+    pub, sig = ed.sign(bytes(range(32)), b"x" * 32)
+    assert ed.verify_status(pub, sig, b"x" * 32) == ed.OK
+    assert ed.verify_status(pub, b"", b"x" * 32) == ed.EMPTY
+    assert ed.verify_status(pub, sig, b"") == ed.EMPTY
+    bad = bytearray(sig)
+    bad[0] = (bad[0] + 1) & 0xFF
+    assert ed.verify_status(pub, bytes(bad), b"x" * 32) == ed.BAD_SIG
+    big = b"\x11" * (1 << 20)  # 1 MB clear data (CryptoUtilsTest: large message)
+    pub2, sig2 = ed.sign(bytes(32), big)
+    assert oracle.oracle_ed25519_verify(pub2, 32, sig2, 64, big, len(big)) == 0
+
+
+def test_sha2_vs_hashlib(oracle):
+    rng = random.Random(5)
+    out = ctypes.create_string_buffer(64)
+    for n in list(range(0, 300)) + [1000, 4096, 100000]:
+        m = bytes(rng.getrandbits(8) for _ in range(n))
+        oracle.oracle_sha256(m, n, out)
+        assert out.raw[:32] == hashlib.sha256(m).digest()
+        oracle.oracle_sha512(m, n, out)
+        assert out.raw == hashlib.sha512(m).digest()
+
+
+def test_slide_c_vs_python(oracle):
+    rng = random.Random(11)
+    r = ctypes.create_string_buffer(256)
+    for _ in range(300):
+        a = rng.getrandbits(256)
+        if rng.random() < 0.5:
+            a |= 1 << 255
+        ab = a.to_bytes(32, "little")
+        dropped = oracle.oracle_slide(ab, r)
+        digits = [int.from_bytes(bytes([x]), "little", signed=True) for x in r.raw]
+        assert digits == ed.slide(ab)
+        assert dropped == (ed.slide_value(ab) != a)
+
+
+def _merkle_py(leaves):
+    """MerkleTree.kt:27-66 restated in Python (independent of oracle/c)."""
+    if not leaves:
+        raise ValueError("MerkleTreeException")
+    n = 1
+    while n < len(leaves):
+        n *= 2
+    lvl = list(leaves) + [bytes(32)] * (n - len(leaves))
+    while len(lvl) > 1:
+        lvl = [hashlib.sha256(lvl[i] + lvl[i + 1]).digest() for i in range(0, len(lvl), 2)]
+    return lvl[0]
+
+
+def _kryo_char_leaf(c):
+    # DERIVED (not pinned): "corda\0\0\1" header + Kryo class id of char (5 + 2) + big-endian char
+    return hashlib.sha256(b"corda\x00\x00\x01" + bytes([7]) + ord(c).to_bytes(2, "big")).digest()
+
+
+def test_merkle_reference_structure(oracle):
+    hashed = [_kryo_char_leaf(c) for c in "abcdef"]
+    root = ctypes.create_string_buffer(32)
+    # PartialMerkleTreeTest.kt:56-59: 6 leaves == explicit padding with 2 zero hashes
+    oracle.oracle_merkle_root(b"".join(hashed), 6, root)
+    padded = ctypes.create_string_buffer(32)
+    oracle.oracle_merkle_root(b"".join(hashed) + bytes(64), 8, padded)
+    assert root.raw == padded.raw == _merkle_py(hashed)
+    # :61-64 empty -> MerkleTreeException
+    assert oracle.oracle_merkle_root(b"", 0, root) == -1
+    # :66-71 one leaf -> root == leaf
+    oracle.oracle_merkle_root(hashed[0], 1, root)
+    assert root.raw == hashed[0]
+    # :73-81 three leaves -> h(h(l0,l1), h(l2, zero))
+    h1 = hashlib.sha256(hashed[0] + hashed[1]).digest()
+    h2 = hashlib.sha256(hashed[2] + bytes(32)).digest()
+    oracle.oracle_merkle_root(b"".join(hashed[:3]), 3, root)
+    assert root.raw == hashlib.sha256(h1 + h2).digest()
