@@ -47,7 +47,7 @@ struct DevBuf {
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
     hipError_t e = hipMalloc(&p, bytes);
@@ -66,7 +66,7 @@ struct Stage {  // one pipeline slot: device buffers + its stream
 struct Device {
   int id = 0;
   uint32_t* btab = nullptr;
-  hipStream_t stream = nullptr;  // default stream for *_device calls
+  hipStream_t stream = nullptr;  // context stream (init-time work)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = -1.0;
   std::mutex mu;  // serialises host-path use of the stages
@@ -268,16 +268,16 @@ void cordahip_shutdown(cordahip_ctx* ctx) {
     ctx->jobs.clear();
   }
   for (auto& d : ctx->devs) {
-    hipSetDevice(d->id);
+    (void)hipSetDevice(d->id);
     for (auto& st : d->stage) {
       for (DevBuf* b : {&st.keys, &st.sigs, &st.msgs, &st.pre, &st.status, &st.verdict})
-        if (b->p) hipFree(b->p);
-      if (st.stream) hipStreamDestroy(st.stream);
+        if (b->p) (void)hipFree(b->p);
+      if (st.stream) (void)hipStreamDestroy(st.stream);
     }
-    if (d->btab) hipFree(d->btab);
-    if (d->ev0) hipEventDestroy(d->ev0);
-    if (d->ev1) hipEventDestroy(d->ev1);
-    if (d->stream) hipStreamDestroy(d->stream);
+    if (d->btab) (void)hipFree(d->btab);
+    if (d->ev0) (void)hipEventDestroy(d->ev0);
+    if (d->ev1) (void)hipEventDestroy(d->ev1);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
   }
   delete ctx;
 }
@@ -344,7 +344,7 @@ int cordahip_ed25519_verify_device(cordahip_ctx* ctx, int device, const void* d_
     return CORDAHIP_ERR_INVALID_ARG;
   if (msg_len == 32 && (reinterpret_cast<uintptr_t>(d_msgs) & 15)) return CORDAHIP_ERR_INVALID_ARG;
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
-  hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : d->stream;
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);  // NULL = the device's null stream
   hipError_t e = hipEventRecord(d->ev0, s);
   e = e ? e
         : launch_ed25519_verify(static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
@@ -374,7 +374,7 @@ int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_se
   Device* d = dev_at(ctx, device);
   if (!d || (n && (!d_seeds || !d_pubs || !d_sigs))) return CORDAHIP_ERR_INVALID_ARG;
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
-  hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : d->stream;
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);  // NULL = the device's null stream
   return hip_err(launch_ed25519_sign(static_cast<const uint8_t*>(d_seeds), static_cast<const uint8_t*>(d_msgs),
                                      msg_len, n, d->btab, static_cast<uint8_t*>(d_pubs),
                                      static_cast<uint8_t*>(d_sigs), s));

@@ -112,8 +112,9 @@ int cordahip_sig_verify(cordahip_ctx* ctx, const cordahip_sig_batch* batch);
 /* ---- dense Ed25519 paths -------------------------------------------------- *
  * keys n*32 B, sigs n*64 B (R || S), msgs n*msg_len B, all row-major.
  * _device: pointers are device (HBM) memory on `device`; 16-byte aligned;
- *          runs on hip_stream (NULL = the context's stream for that device);
- *          asynchronous w.r.t. the host.
+ *          enqueued on hip_stream (a hipStream_t; NULL = the device's null
+ *          stream, with HIP's usual null-stream ordering); asynchronous w.r.t.
+ *          the host, ordered after earlier work on that stream.
  * _host:   host pointers (pinned recommended); shards over all context devices,
  *          pipelines H2D copy / kernel / D2H copy in chunks; synchronous.   */
 int cordahip_ed25519_verify_device(cordahip_ctx* ctx, int device, const void* d_keys, const void* d_sigs,
