@@ -28,7 +28,9 @@ EXPORTS = [
     "cordahip_device_count", "cordahip_alloc_pinned", "cordahip_free_pinned", "cordahip_sig_submit",
     "cordahip_wait", "cordahip_poll", "cordahip_sig_verify", "cordahip_ed25519_verify_device",
     "cordahip_ed25519_verify_host", "cordahip_ed25519_sign_device", "cordahip_last_kernel_ms",
+    "cordahip_tx_ids", "cordahip_signed_tx_verify", "cordahip_signed_tx_verify_ed25519_device",
 ]
+TX_NO_LEAVES, TX_NO_SIGNATURES = 6, 7
 
 
 class EngineUnavailable(RuntimeError):
@@ -50,6 +52,25 @@ class SigBatch(ctypes.Structure):
         ("msg", ctypes.c_void_p), ("msg_off", ctypes.c_void_p),
         ("status", ctypes.c_void_p),
         ("verdict", ctypes.c_void_p),
+    ]
+
+
+class TxidBatch(ctypes.Structure):
+    _fields_ = [
+        ("ntx", ctypes.c_uint64),
+        ("leaf_bytes", ctypes.c_void_p), ("leaf_off", ctypes.c_void_p), ("tx_leaf_off", ctypes.c_void_p),
+        ("txid", ctypes.c_void_p), ("tx_status", ctypes.c_void_p),
+    ]
+
+
+class SignedTxBatch(ctypes.Structure):
+    _fields_ = [
+        ("tx", TxidBatch),
+        ("tx_sig_off", ctypes.c_void_p),
+        ("scheme", ctypes.c_void_p),
+        ("key", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
+        ("sig", ctypes.c_void_p), ("sig_off", ctypes.c_void_p),
+        ("sig_status", ctypes.c_void_p), ("first_bad_sig", ctypes.c_void_p),
     ]
 
 
@@ -91,6 +112,10 @@ def lib() -> ctypes.CDLL:
         "cordahip_ed25519_verify_host": (i32, [vp, vp, vp, vp, u32, u64, vp, vp]),
         "cordahip_ed25519_sign_device": (i32, [vp, i32, vp, vp, u32, u64, vp, vp, vp]),
         "cordahip_last_kernel_ms": (ctypes.c_double, [vp, i32]),
+        "cordahip_tx_ids": (i32, [vp, ctypes.POINTER(TxidBatch)]),
+        "cordahip_signed_tx_verify": (i32, [vp, ctypes.POINTER(SignedTxBatch)]),
+        "cordahip_signed_tx_verify_ed25519_device": (i32, [vp, i32, vp, vp, u64, vp, u64, vp, vp, vp, u64, vp, vp,
+                                                           vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(l, name)

@@ -34,6 +34,14 @@ hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const
                                  unsigned long long* verdict, hipStream_t s);
 hipError_t launch_ed25519_sign(const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len, uint64_t n,
                                const uint32_t* btab, uint8_t* pubs, uint8_t* sigs, hipStream_t s);
+hipError_t launch_sha256_leaves(const uint8_t* bytes, const uint64_t* off, uint64_t nleaves, uint32_t* hashes,
+                                hipStream_t s);
+hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uint64_t ntx, uint8_t* txid,
+                              uint8_t* tx_status, hipStream_t s);
+hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
+                              hipStream_t s);
+hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
+                            uint8_t* tx_status, hipStream_t s);
 }  // namespace cordahip
 
 using namespace cordahip;
@@ -63,14 +71,20 @@ struct Stage {  // one pipeline slot: device buffers + its stream
   DevBuf keys, sigs, msgs, pre, status, verdict;
 };
 
+struct TxWork {  // device buffers of the transaction paths (grow-only)
+  DevBuf leaf_bytes, leaf_off, tx_leaf_off, hashes, txid, tx_status, tx_sig_off, msgs;
+};
+
 struct Device {
   int id = 0;
   uint32_t* btab = nullptr;
-  hipStream_t stream = nullptr;  // context stream (init-time work)
+  hipStream_t stream = nullptr;  // context stream (init-time work and host tx paths)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = -1.0;
   std::mutex mu;  // serialises host-path use of the stages
   Stage stage[2];
+  std::mutex tx_mu;  // serialises use of tx
+  TxWork tx;
 };
 
 int hip_err(hipError_t e) { return e == hipSuccess ? CORDAHIP_SUCCESS : CORDAHIP_ERR_HIP; }
@@ -211,6 +225,97 @@ int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
   return CORDAHIP_SUCCESS;
 }
 
+// Transaction ids for txs [t0, t1) on one device (offsets rebased to the shard).
+int tx_ids_shard(Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1) {
+  std::lock_guard<std::mutex> g(d.tx_mu);
+  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  const uint64_t ntx = t1 - t0;
+  const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1];
+  const uint64_t nleaves = l1 - l0;
+  const uint64_t b0 = b->leaf_off[l0], b1 = b->leaf_off[l1];
+  std::vector<uint64_t> loff(nleaves + 1), toff(ntx + 1);
+  for (uint64_t i = 0; i <= nleaves; i++) loff[i] = b->leaf_off[l0 + i] - b0;
+  for (uint64_t i = 0; i <= ntx; i++) toff[i] = b->tx_leaf_off[t0 + i] - l0;
+  TxWork& w = d.tx;
+  if (w.leaf_bytes.ensure(std::max<uint64_t>(b1 - b0, 16)) || w.leaf_off.ensure((nleaves + 1) * 8) ||
+      w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
+      w.txid.ensure(ntx * 32) || w.tx_status.ensure(ntx))
+    return CORDAHIP_ERR_OUT_OF_MEMORY;
+  hipStream_t s = d.stream;
+  hipError_t e = hipSuccess;
+  if (b1 > b0) e = hipMemcpyAsync(w.leaf_bytes.p, b->leaf_bytes + b0, b1 - b0, hipMemcpyHostToDevice, s);
+  e = e ? e : hipMemcpyAsync(w.leaf_off.p, loff.data(), (nleaves + 1) * 8, hipMemcpyHostToDevice, s);
+  e = e ? e : hipMemcpyAsync(w.tx_leaf_off.p, toff.data(), (ntx + 1) * 8, hipMemcpyHostToDevice, s);
+  e = e ? e : launch_sha256_leaves(w.leaf_bytes.as<uint8_t>(), w.leaf_off.as<uint64_t>(), nleaves,
+                                   w.hashes.as<uint32_t>(), s);
+  e = e ? e : launch_merkle_root(w.hashes.as<uint32_t>(), w.tx_leaf_off.as<uint64_t>(), ntx, w.txid.as<uint8_t>(),
+                                 w.tx_status.as<uint8_t>(), s);
+  e = e ? e : hipMemcpyAsync(b->txid + t0 * 32, w.txid.p, ntx * 32, hipMemcpyDeviceToHost, s);
+  e = e ? e : hipMemcpyAsync(b->tx_status + t0, w.tx_status.p, ntx, hipMemcpyDeviceToHost, s);
+  e = e ? e : hipStreamSynchronize(s);
+  return hip_err(e);
+}
+
+int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
+  if (!b->leaf_off || !b->tx_leaf_off || !b->txid || !b->tx_status || (!b->leaf_bytes && b->ntx))
+    return CORDAHIP_ERR_INVALID_ARG;
+  const uint64_t n = b->ntx, nd = ctx->devs.size();
+  if (n == 0) return CORDAHIP_SUCCESS;
+  const uint64_t per = (n + nd - 1) / nd;  // contiguous tx shards, independent trees
+  std::vector<std::future<int>> fs;
+  for (uint64_t i = 0; i < nd; i++) {
+    const uint64_t t0 = std::min(n, i * per), t1 = std::min(n, t0 + per);
+    if (t0 >= t1) break;
+    Device* d = ctx->devs[i].get();
+    fs.push_back(std::async(std::launch::async, [=] { return tx_ids_shard(*d, b, t0, t1); }));
+  }
+  int rc = CORDAHIP_SUCCESS;
+  for (auto& f : fs) {
+    const int r = f.get();
+    if (r != CORDAHIP_SUCCESS) rc = r;
+  }
+  return rc;
+}
+
+int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
+  const uint64_t ntx = b->tx.ntx;
+  if (!b->tx_sig_off || !b->first_bad_sig || !b->sig_status) return CORDAHIP_ERR_INVALID_ARG;
+  int rc = tx_ids_impl(ctx, &b->tx);
+  if (rc != CORDAHIP_SUCCESS) return rc;
+  const uint64_t nsig = ntx ? b->tx_sig_off[ntx] : 0;
+  // each signature signs its transaction's id (SignedTransaction.kt:98)
+  std::vector<uint8_t> msgs(std::max<uint64_t>(nsig, 1) * 32);
+  std::vector<uint64_t> moff(nsig + 1);
+  for (uint64_t t = 0; t < ntx; t++)
+    for (uint64_t s = b->tx_sig_off[t]; s < b->tx_sig_off[t + 1]; s++) std::memcpy(&msgs[s * 32], b->tx.txid + t * 32, 32);
+  for (uint64_t s = 0; s <= nsig; s++) moff[s] = s * 32;
+  if (nsig) {
+    cordahip_sig_batch sb{nsig, b->scheme, b->key, b->key_off, b->sig, b->sig_off, msgs.data(), moff.data(),
+                          b->sig_status, nullptr};
+    rc = sig_verify_impl(ctx, &sb);
+    if (rc != CORDAHIP_SUCCESS) return rc;
+  }
+  for (uint64_t t = 0; t < ntx; t++) {
+    const uint64_t lo = b->tx_sig_off[t], hi = b->tx_sig_off[t + 1];
+    b->first_bad_sig[t] = -1;
+    if (b->tx.tx_status[t] != CORDAHIP_STATUS_OK) {  // tx.id threw before any signature was checked
+      for (uint64_t s = lo; s < hi; s++) b->sig_status[s] = b->tx.tx_status[t];
+      continue;
+    }
+    if (lo == hi) {
+      b->tx.tx_status[t] = CORDAHIP_TX_NO_SIGNATURES;
+      continue;
+    }
+    for (uint64_t s = lo; s < hi; s++)
+      if (b->sig_status[s] != CORDAHIP_STATUS_OK) {
+        b->first_bad_sig[t] = (int64_t)(s - lo);
+        b->tx.tx_status[t] = b->sig_status[s];
+        break;
+      }
+  }
+  return CORDAHIP_SUCCESS;
+}
+
 Device* dev_at(cordahip_ctx* ctx, int device) {
   if (!ctx || device < 0 || device >= (int)ctx->devs.size()) return nullptr;
   return ctx->devs[device].get();
@@ -274,6 +379,9 @@ void cordahip_shutdown(cordahip_ctx* ctx) {
         if (b->p) (void)hipFree(b->p);
       if (st.stream) (void)hipStreamDestroy(st.stream);
     }
+    for (DevBuf* b : {&d->tx.leaf_bytes, &d->tx.leaf_off, &d->tx.tx_leaf_off, &d->tx.hashes, &d->tx.txid,
+                      &d->tx.tx_status, &d->tx.tx_sig_off, &d->tx.msgs})
+      if (b->p) (void)hipFree(b->p);
     if (d->btab) (void)hipFree(d->btab);
     if (d->ev0) (void)hipEventDestroy(d->ev0);
     if (d->ev1) (void)hipEventDestroy(d->ev1);
@@ -378,6 +486,46 @@ int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_se
   return hip_err(launch_ed25519_sign(static_cast<const uint8_t*>(d_seeds), static_cast<const uint8_t*>(d_msgs),
                                      msg_len, n, d->btab, static_cast<uint8_t*>(d_pubs),
                                      static_cast<uint8_t*>(d_sigs), s));
+}
+
+int cordahip_tx_ids(cordahip_ctx* ctx, const cordahip_txid_batch* batch) {
+  if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
+  return tx_ids_impl(ctx, batch);
+}
+
+int cordahip_signed_tx_verify(cordahip_ctx* ctx, const cordahip_signed_tx_batch* batch) {
+  if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
+  return signed_tx_impl(ctx, batch);
+}
+
+int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, const void* d_leaf_bytes,
+                                             const void* d_leaf_off, uint64_t nleaves, const void* d_tx_leaf_off,
+                                             uint64_t ntx, const void* d_tx_sig_off, const void* d_keys,
+                                             const void* d_sigs, uint64_t nsig, void* d_txid, void* d_tx_status,
+                                             void* d_first_bad, void* d_sig_status, void* hip_stream) {
+  Device* d = dev_at(ctx, device);
+  if (!d || (ntx && (!d_leaf_off || !d_tx_leaf_off || !d_tx_sig_off || !d_txid || !d_tx_status || !d_first_bad)) ||
+      (nsig && (!d_keys || !d_sigs || !d_sig_status)))
+    return CORDAHIP_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(d->tx_mu);
+  if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  if (d->tx.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) || d->tx.msgs.ensure(std::max<uint64_t>(nsig, 1) * 32))
+    return CORDAHIP_ERR_OUT_OF_MEMORY;
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  hipError_t e = hipEventRecord(d->ev0, s);
+  e = e ? e : launch_sha256_leaves(static_cast<const uint8_t*>(d_leaf_bytes), static_cast<const uint64_t*>(d_leaf_off),
+                                   nleaves, d->tx.hashes.as<uint32_t>(), s);
+  e = e ? e : launch_merkle_root(d->tx.hashes.as<uint32_t>(), static_cast<const uint64_t*>(d_tx_leaf_off), ntx,
+                                 static_cast<uint8_t*>(d_txid), static_cast<uint8_t*>(d_tx_status), s);
+  e = e ? e : launch_gather_txid(static_cast<const uint8_t*>(d_txid), static_cast<const uint64_t*>(d_tx_sig_off), ntx,
+                                 d->tx.msgs.as<uint8_t>(), s);
+  e = e ? e : launch_ed25519_verify(static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
+                                    d->tx.msgs.as<uint8_t>(), 32, nsig, d->btab, nullptr,
+                                    static_cast<uint8_t*>(d_sig_status), nullptr, s);
+  e = e ? e : launch_tx_reduce(static_cast<const uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off),
+                               ntx, static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);
+  e = e ? e : hipEventRecord(d->ev1, s);
+  return hip_err(e);
 }
 
 }  // extern "C"

@@ -1,0 +1,234 @@
+// Transaction ids and per-transaction signature verdicts for gfx950 —
+// kernels K3 (leaf hashes), K4 (Merkle roots) and K5 (per-tx reduction).
+//
+// Reference path:
+//   WireTransaction.id = MerkleTree.getMerkleTree(availableComponentHashes).hash
+//     WireTransaction.kt:48,120; MerkleTransaction.kt:69
+//   leaf_i = SHA-256(serialised component i)                  MerkleTransaction.kt:16-18,
+//            ("corda\0\0\1" + Kryo bytes, produced by the host)  Kryo.kt:95,101,165-176
+//   padWithZeros to 2^k with SecureHash.zeroHash               MerkleTree.kt:33-41
+//   node = SHA-256(left || right), no domain separation        MerkleTree.kt:57-63, SecureHash.kt:24
+//   empty -> MerkleTreeException; one leaf -> root = leaf      MerkleTree.kt:49-52
+//   SignedTransaction.checkSignaturesAreValid: sigs verified in list order,
+//   the first failure throws                                   SignedTransaction.kt:95-100
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sha2_device.hpp"
+#include "status.hpp"
+
+namespace cordahip {
+
+// tx-level statuses beyond the lane statuses (include/cordahip.h)
+static constexpr uint8_t kTxNoLeaves = 6;      // MerkleTreeException
+static constexpr uint8_t kTxNoSignatures = 7;  // SignedTransaction init: require(sigs.isNotEmpty())
+
+CDEV uint32_t load_be32_bytes(const uint8_t* __restrict__ p, uint64_t len, uint64_t pos, uint64_t total_bits,
+                              uint64_t padded_len) {
+  // big-endian word of the padded message starting at byte pos
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint64_t q = pos + k;
+    uint32_t b;
+    if (q < len) b = p[q];
+    else if (q == len) b = 0x80;
+    else if (q >= padded_len - 8) b = (uint32_t)((total_bits >> (8 * (padded_len - 1 - q))) & 0xff);
+    else b = 0;
+    w = (w << 8) | b;
+  }
+  return w;
+}
+
+// SHA-256 of an arbitrary byte string in global memory (one lane)
+CDEV void sha256_bytes(uint32_t h[8], const uint8_t* __restrict__ p, uint64_t len) {
+  sha256_init(h);
+  const uint64_t padded = ((len + 9 + 63) / 64) * 64;
+  const uint64_t bits = len * 8;
+  uint32_t w[16];
+  for (uint64_t blk = 0; blk < padded; blk += 64) {
+    if (blk + 64 <= len) {
+      // interior block: plain byte loads, no padding logic
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const uint8_t* b = p + blk + 4 * q;
+        w[q] = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; q++) w[q] = load_be32_bytes(p, len, blk + 4 * q, bits, padded);
+    }
+    sha256_block(h, w);
+  }
+}
+
+// SHA-256(a || b) for two 32-byte digests (state words, big-endian): the
+// Merkle node hash. The second block is the constant padding of a 64-byte
+// message.
+CDEV void sha256_node(uint32_t out[8], const uint32_t a[8], const uint32_t b[8]) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    w[i] = a[i];
+    w[8 + i] = b[i];
+  }
+  sha256_init(out);
+  sha256_block(out, w);
+#pragma unroll
+  for (int i = 0; i < 16; i++) w[i] = 0;
+  w[0] = 0x80000000u;
+  w[15] = 512;
+  sha256_block(out, w);
+}
+
+// K3: one lane per leaf
+__global__ void __launch_bounds__(256) sha256_leaves_kernel(const uint8_t* __restrict__ bytes,
+                                                           const uint64_t* __restrict__ off, uint64_t nleaves,
+                                                           uint32_t* __restrict__ hashes /* [nleaves][8] BE words */) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nleaves) return;
+  uint32_t h[8];
+  const uint64_t lo = off[i], hi = off[i + 1];
+  sha256_bytes(h, bytes + lo, hi - lo);
+  uint4* o = reinterpret_cast<uint4*>(hashes + i * 8);
+  o[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  o[1] = make_uint4(h[4], h[5], h[6], h[7]);
+}
+
+// K4: one lane per transaction; reduces the tx's leaf-hash range in place.
+// Level j holds m_j real nodes; positions >= m_j are the padding constant
+// Z_j (Z_0 = zeroHash, Z_{j+1} = H(Z_j, Z_j)), exactly the padded tree of
+// MerkleTree.kt:33-66.
+__global__ void __launch_bounds__(256) merkle_root_kernel(uint32_t* __restrict__ hashes,
+                                                         const uint64_t* __restrict__ tx_leaf_off, uint64_t ntx,
+                                                         uint8_t* __restrict__ txid, uint8_t* __restrict__ tx_status) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;
+  const uint64_t lo = tx_leaf_off[t], hi = tx_leaf_off[t + 1];
+  uint64_t m = hi - lo;
+  if (m == 0) {
+    if (tx_status) tx_status[t] = kTxNoLeaves;
+#pragma unroll
+    for (int i = 0; i < 32; i++) txid[t * 32 + i] = 0;
+    return;
+  }
+  uint32_t* v = hashes + lo * 8;
+  uint32_t z[8];  // Z_zlevel
+#pragma unroll
+  for (int i = 0; i < 8; i++) z[i] = 0;
+  int zlevel = 0;
+  for (int level = 0; m > 1; level++) {
+    const uint64_t half = (m + 1) / 2;
+    if (m & 1) {  // the last real node pairs with the padding constant Z_level
+      for (; zlevel < level; zlevel++) {
+        uint32_t zz[8];
+        sha256_node(zz, z, z);
+#pragma unroll
+        for (int k = 0; k < 8; k++) z[k] = zz[k];
+      }
+    }
+    for (uint64_t i = 0; i < half; i++) {
+      uint32_t a[8], b[8], r[8];
+      const uint4* pa = reinterpret_cast<const uint4*>(v + 16 * i);
+      const uint4 a0 = pa[0], a1 = pa[1];
+      a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
+      if (2 * i + 1 < m) {
+        const uint4 b0 = pa[2], b1 = pa[3];
+        b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) b[k] = z[k];
+      }
+      sha256_node(r, a, b);
+      uint4* po = reinterpret_cast<uint4*>(v + 8 * i);
+      po[0] = make_uint4(r[0], r[1], r[2], r[3]);
+      po[1] = make_uint4(r[4], r[5], r[6], r[7]);
+    }
+    m = half;
+  }
+  // root = v[0]; emit big-endian bytes (SecureHash byte order)
+  uint4* o = reinterpret_cast<uint4*>(txid + t * 32);
+  const uint4* pv = reinterpret_cast<const uint4*>(v);
+  const uint4 r0 = pv[0], r1 = pv[1];
+  o[0] = make_uint4(bswap32(r0.x), bswap32(r0.y), bswap32(r0.z), bswap32(r0.w));
+  o[1] = make_uint4(bswap32(r1.x), bswap32(r1.y), bswap32(r1.z), bswap32(r1.w));
+  if (tx_status) tx_status[t] = kStatusOk;
+}
+
+// gather: msgs[s] = txid[sig_tx[s]] (each signature signs its tx id, SignedTransaction.kt:98)
+__global__ void __launch_bounds__(256) gather_txid_kernel(const uint8_t* __restrict__ txid,
+                                                         const uint64_t* __restrict__ tx_sig_off, uint64_t ntx,
+                                                         uint8_t* __restrict__ msgs) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;
+  const uint4* src = reinterpret_cast<const uint4*>(txid + t * 32);
+  const uint4 a = src[0], b = src[1];
+  for (uint64_t s = tx_sig_off[t]; s < tx_sig_off[t + 1]; s++) {
+    uint4* d = reinterpret_cast<uint4*>(msgs + s * 32);
+    d[0] = a;
+    d[1] = b;
+  }
+}
+
+// K5: checkSignaturesAreValid order — the first non-OK signature (list order)
+// decides the tx outcome; -1 when every signature verified.
+__global__ void __launch_bounds__(256) tx_reduce_kernel(const uint8_t* __restrict__ sig_status,
+                                                       const uint64_t* __restrict__ tx_sig_off, uint64_t ntx,
+                                                       int64_t* __restrict__ first_bad, uint8_t* __restrict__ tx_status) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;
+  if (tx_status[t] != kStatusOk) {  // no leaves: the id itself could not be computed
+    first_bad[t] = -1;
+    return;
+  }
+  const uint64_t lo = tx_sig_off[t], hi = tx_sig_off[t + 1];
+  if (lo == hi) {
+    first_bad[t] = -1;
+    tx_status[t] = kTxNoSignatures;
+    return;
+  }
+  int64_t fb = -1;
+  uint8_t st = kStatusOk;
+  for (uint64_t s = lo; s < hi; s++) {
+    const uint8_t v = sig_status[s];
+    if (v != kStatusOk) {
+      fb = (int64_t)(s - lo);
+      st = v;
+      break;
+    }
+  }
+  first_bad[t] = fb;
+  tx_status[t] = st;
+}
+
+// ---------------------------------------------------------------------------
+hipError_t launch_sha256_leaves(const uint8_t* bytes, const uint64_t* off, uint64_t nleaves, uint32_t* hashes,
+                                hipStream_t s) {
+  if (!nleaves) return hipSuccess;
+  hipLaunchKernelGGL(sha256_leaves_kernel, dim3((uint32_t)((nleaves + 255) / 256)), dim3(256), 0, s, bytes, off,
+                     nleaves, hashes);
+  return hipGetLastError();
+}
+hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uint64_t ntx, uint8_t* txid,
+                              uint8_t* tx_status, hipStream_t s) {
+  if (!ntx) return hipSuccess;
+  hipLaunchKernelGGL(merkle_root_kernel, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, s, hashes, tx_leaf_off,
+                     ntx, txid, tx_status);
+  return hipGetLastError();
+}
+hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
+                              hipStream_t s) {
+  if (!ntx) return hipSuccess;
+  hipLaunchKernelGGL(gather_txid_kernel, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, s, txid, tx_sig_off,
+                     ntx, msgs);
+  return hipGetLastError();
+}
+hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
+                            uint8_t* tx_status, hipStream_t s) {
+  if (!ntx) return hipSuccess;
+  hipLaunchKernelGGL(tx_reduce_kernel, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, s, sig_status,
+                     tx_sig_off, ntx, first_bad, tx_status);
+  return hipGetLastError();
+}
+
+}  // namespace cordahip

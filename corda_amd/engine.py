@@ -13,7 +13,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import EngineError, SigBatch, check, lib
+from ._lib import EngineError, SigBatch, SignedTxBatch, TxidBatch, check, lib
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -100,6 +100,50 @@ class Engine:
         check(lib().cordahip_ed25519_sign_device(self._ctx, device, seeds.data_ptr(), msgs.data_ptr(),
                                                  msgs.shape[1], n, pubs.data_ptr(), sigs.data_ptr(), s),
               "cordahip_ed25519_sign_device")
+
+    # ---- transactions: WireTransaction.id and SignedTransaction verification ---
+    def _tx_arrays(self, txs: Sequence[Sequence[bytes]]):
+        leaves = [leaf for tx in txs for leaf in tx]
+        lb, lo = self._csr(leaves)
+        to = np.zeros(len(txs) + 1, dtype=np.uint64)
+        if txs:
+            to[1:] = np.cumsum([len(tx) for tx in txs], dtype=np.uint64)
+        txid = np.zeros((max(len(txs), 1), 32), dtype=np.uint8)
+        st = np.zeros(max(len(txs), 1), dtype=np.uint8)
+        b = TxidBatch(len(txs), _ptr(lb), _ptr(lo), _ptr(to), _ptr(txid), _ptr(st))
+        return b, (lb, lo, to, txid, st)
+
+    def tx_ids(self, txs: Sequence[Sequence[bytes]]):
+        """txs: per transaction, the serialised components (leaf preimages). Returns (ids[ntx,32], status[ntx])."""
+        b, keep = self._tx_arrays(txs)
+        check(lib().cordahip_tx_ids(self._ctx, ctypes.byref(b)), "cordahip_tx_ids")
+        return keep[3][:len(txs)], keep[4][:len(txs)]
+
+    def signed_tx_verify(self, txs: Sequence[Sequence[bytes]], sigs: Sequence[Sequence[tuple]]):
+        """sigs[t] = [(scheme, key, sig), ...] in list order. Returns (ids, tx_status, first_bad, sig_status)."""
+        b, keep = self._tx_arrays(txs)
+        flat = [x for per in sigs for x in per]
+        so = np.zeros(len(txs) + 1, dtype=np.uint64)
+        if txs:
+            so[1:] = np.cumsum([len(per) for per in sigs], dtype=np.uint64)
+        sch = np.ascontiguousarray(np.asarray([x[0] for x in flat] or [0], dtype=np.uint8))
+        kb, ko = self._csr([x[1] for x in flat])
+        sb, sgo = self._csr([x[2] for x in flat])
+        sst = np.zeros(max(len(flat), 1), dtype=np.uint8)
+        fb = np.zeros(max(len(txs), 1), dtype=np.int64)
+        sbatch = SignedTxBatch(b, _ptr(so), _ptr(sch), _ptr(kb), _ptr(ko), _ptr(sb), _ptr(sgo), _ptr(sst), _ptr(fb))
+        check(lib().cordahip_signed_tx_verify(self._ctx, ctypes.byref(sbatch)), "cordahip_signed_tx_verify")
+        n = len(txs)
+        return keep[3][:n], keep[4][:n], fb[:n], sst[:len(flat)]
+
+    def signed_tx_verify_ed25519_device(self, leaf_bytes, leaf_off, tx_leaf_off, tx_sig_off, keys, sigs,
+                                        txid, tx_status, first_bad, sig_status, device: int = 0, stream=None):
+        s = stream.cuda_stream if stream is not None else 0
+        check(lib().cordahip_signed_tx_verify_ed25519_device(
+            self._ctx, device, leaf_bytes.data_ptr(), leaf_off.data_ptr(), leaf_off.shape[0] - 1,
+            tx_leaf_off.data_ptr(), tx_leaf_off.shape[0] - 1, tx_sig_off.data_ptr(), keys.data_ptr(),
+            sigs.data_ptr(), keys.shape[0], txid.data_ptr(), tx_status.data_ptr(), first_bad.data_ptr(),
+            sig_status.data_ptr(), s), "cordahip_signed_tx_verify_ed25519_device")
 
     def last_kernel_ms(self, device: int = 0) -> float:
         return lib().cordahip_last_kernel_ms(self._ctx, device)

@@ -127,6 +127,51 @@ int cordahip_ed25519_verify_host(cordahip_ctx* ctx, const uint8_t* keys, const u
 int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_seeds, const void* d_msgs,
                                  uint32_t msg_len, uint64_t n, void* d_pubs, void* d_sigs, void* hip_stream);
 
+/* ---- transaction ids and SignedTransaction batches ----------------------- */
+/* tx-level statuses (tx_status[t]) in addition to the lane statuses above */
+#define CORDAHIP_TX_NO_LEAVES 6     /* MerkleTreeException: empty component list (MerkleTree.kt:49-50) */
+#define CORDAHIP_TX_NO_SIGNATURES 7 /* IllegalArgumentException: require(sigs.isNotEmpty()) (SignedTransaction.kt:37-39) */
+
+/* Leaves are the serialised components of each WireTransaction, in
+ * availableComponents order (MerkleTransaction.kt:51-62), each including the
+ * "corda\0\0\1" Kryo header (Kryo.kt:101); the host serialises, the GPU hashes. */
+typedef struct {
+  uint64_t ntx;
+  const uint8_t* leaf_bytes;
+  const uint64_t* leaf_off;    /* [nleaves+1] into leaf_bytes */
+  const uint64_t* tx_leaf_off; /* [ntx+1] leaves of tx t: [tx_leaf_off[t], tx_leaf_off[t+1]) */
+  uint8_t* txid;               /* [ntx*32] out: WireTransaction.id (SecureHash bytes) */
+  uint8_t* tx_status;          /* [ntx] out: OK, NO_LEAVES (ids) / first failing lane status (signed tx) */
+} cordahip_txid_batch;
+int cordahip_tx_ids(cordahip_ctx* ctx, const cordahip_txid_batch* batch);
+
+/* SignedTransaction.checkSignaturesAreValid over many transactions: every
+ * signature is verified over its transaction's recomputed id; first_bad_sig[t]
+ * is the index (within tx t, list order) of the signature whose exception the
+ * reference would throw first, -1 if none. Signer coverage
+ * (getMissingSignatures, CompositeKey.isFulfilledBy) stays with the caller. */
+typedef struct {
+  cordahip_txid_batch tx;
+  const uint64_t* tx_sig_off; /* [ntx+1] signatures of tx t */
+  const uint8_t* scheme;      /* [nsig] per signature, CSR key/sig as in cordahip_sig_batch */
+  const uint8_t* key;
+  const uint64_t* key_off;
+  const uint8_t* sig;
+  const uint64_t* sig_off;
+  uint8_t* sig_status;    /* [nsig] out */
+  int64_t* first_bad_sig; /* [ntx] out */
+} cordahip_signed_tx_batch;
+int cordahip_signed_tx_verify(cordahip_ctx* ctx, const cordahip_signed_tx_batch* batch);
+
+/* Device-resident dense variant (all Ed25519, 32-byte keys, 64-byte sigs;
+ * every array in HBM on `device`): K3 leaf hashes -> K4 Merkle roots ->
+ * txid gather -> K1 verify -> K5 per-tx reduce, all on hip_stream. */
+int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, const void* d_leaf_bytes,
+                                             const void* d_leaf_off, uint64_t nleaves, const void* d_tx_leaf_off,
+                                             uint64_t ntx, const void* d_tx_sig_off, const void* d_keys,
+                                             const void* d_sigs, uint64_t nsig, void* d_txid, void* d_tx_status,
+                                             void* d_first_bad, void* d_sig_status, void* hip_stream);
+
 /* Device time of the last kernel launched by the context on `device` (ms), measured
  * with HIP events on the stream the kernel ran on; -1 if unavailable. */
 double cordahip_last_kernel_ms(cordahip_ctx* ctx, int device);

@@ -23,3 +23,16 @@ int oracle_merkle_root(const uint8_t* leaves, size_t n, uint8_t root[32]) {
   free(lvl);
   return 0;
 }
+
+/* WireTransaction.id (WireTransaction.kt:48,120): leaves are SHA-256 of the
+ * serialised components (MerkleTransaction.kt:16-18,69), root per MerkleTree.kt.
+ * leaf_off has nleaves+1 entries into leaf_bytes. Returns -1 for no leaves. */
+int oracle_tx_id(const uint8_t* leaf_bytes, const uint64_t* leaf_off, size_t nleaves, uint8_t id[32]) {
+  if (nleaves == 0) return -1;
+  uint8_t* h = (uint8_t*)malloc(nleaves * 32);
+  for (size_t i = 0; i < nleaves; i++)
+    oracle_sha256(leaf_bytes + leaf_off[i], (size_t)(leaf_off[i + 1] - leaf_off[i]), h + 32 * i);
+  int rc = oracle_merkle_root(h, nleaves, id);
+  free(h);
+  return rc;
+}

@@ -53,6 +53,9 @@ void oracle_ed25519_sign(const uint8_t seed[32], const uint8_t* msg, size_t msgl
  * (MerkleTreeException, MerkleTree.kt:49-50). */
 int oracle_merkle_root(const uint8_t* leaves, size_t nleaves, uint8_t root[32]);
 
+/* WireTransaction.id from the serialised components (leaf preimages, CSR). */
+int oracle_tx_id(const uint8_t* leaf_bytes, const uint64_t* leaf_off, size_t nleaves, uint8_t id[32]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,6 +37,7 @@ def load_oracle():
     lib.oracle_sha512.argtypes = [cp, sz, ctypes.c_char_p]
     lib.oracle_merkle_root.argtypes = [cp, sz, ctypes.c_char_p]
     lib.oracle_slide.argtypes = [cp, ctypes.c_char_p]
+    lib.oracle_tx_id.argtypes = [ctypes.c_void_p, ctypes.c_void_p, sz, ctypes.c_char_p]
     return lib
 
 

@@ -1,0 +1,112 @@
+"""K3/K4/K5 parity on the GPU: transaction ids (WireTransaction.id) and
+SignedTransaction.checkSignaturesAreValid semantics, through the C-ABI."""
+import ctypes
+import hashlib
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ED = 4
+
+
+def _golden_txs():
+    path = os.path.join(os.path.dirname(__file__), "golden", "merkle_vectors.json")
+    return json.load(open(path))["txs"]
+
+
+def test_tx_ids_golden(engine):
+    txs = _golden_txs()
+    ids, st = engine.tx_ids([[bytes.fromhex(x) for x in t["leaves"]] for t in txs])
+    for t, i, s in zip(txs, ids, st):
+        if t["id"] is None:
+            assert s == 6, t["name"]  # MerkleTreeException
+        else:
+            assert s == 0 and i.tobytes().hex() == t["id"], t["name"]
+
+
+def test_tx_ids_random_vs_oracle(engine, oracle):
+    rng = random.Random(9)
+    txs = []
+    for _ in range(3000):
+        n = rng.choice([1, 2, 3, 5, 5, 5, 8, 9, 16, 17, 40])
+        txs.append([bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 200))) for _ in range(n)])
+    ids, st = engine.tx_ids(txs)
+    out = ctypes.create_string_buffer(32)
+    for tx, i in zip(txs, ids):
+        blob = np.frombuffer(b"".join(tx) or b"\0", np.uint8).copy()
+        off = np.zeros(len(tx) + 1, np.uint64)
+        off[1:] = np.cumsum([len(x) for x in tx])
+        assert oracle.oracle_tx_id(blob.ctypes.data, off.ctypes.data, len(tx), out) == 0
+        assert out.raw == i.tobytes()
+    assert (st == 0).all()
+
+
+def _sign(oracle, seed, msg):
+    pub, sig = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+    oracle.oracle_ed25519_sign(seed, msg, len(msg), pub, sig)
+    return pub.raw, sig.raw
+
+
+def test_signed_tx_semantics(engine, oracle):
+    """TransactionSerializationTests.kt:61-97 / TransactionTests.kt:27-94 shapes."""
+    rng = random.Random(4)
+    txs = [[bytes(rng.getrandbits(8) for _ in range(n)) for n in (450, 150, 140, 43, 55)] for _ in range(6)]
+    ids, _ = engine.tx_ids(txs)
+    seeds = [hashlib.sha256(b"signer%d" % i).digest() for i in range(3)]
+    good = [[(ED,) + _sign(oracle, sd, ids[t].tobytes()) for sd in seeds] for t in range(len(txs))]
+    sigs = [list(g) for g in good]
+    # tx1: second signature corrupted -> first_bad = 1, BAD_SIG
+    s1 = bytearray(sigs[1][1][2]); s1[0] ^= 1
+    sigs[1][1] = (ED, sigs[1][1][1], bytes(s1))
+    # tx2: signatures swapped between transactions -> BAD_SIG at index 0
+    sigs[2][0] = good[3][0]
+    # tx3: one component byte changed -> the recomputed id no longer matches every signature
+    txs[3][2] = bytes([txs[3][2][0] ^ 1]) + txs[3][2][1:]
+    # tx4: no signatures; tx5: no components
+    sigs[4] = []
+    txs[5] = []
+    got_ids, tx_st, first_bad, sig_st = engine.signed_tx_verify(txs, sigs)
+    assert list(tx_st) == [0, 1, 1, 1, 7, 6]
+    assert list(first_bad) == [-1, 1, 0, 0, -1, -1]
+    assert got_ids[0].tobytes() == ids[0].tobytes()
+    flat = [x for per in sigs for x in per]
+    assert len(sig_st) == len(flat)
+
+
+def test_signed_tx_device_path(engine, oracle):
+    torch = pytest.importorskip("torch")
+    rng = random.Random(12)
+    ntx = 700
+    txs = [[bytes(rng.getrandbits(8) for _ in range(n)) for n in (450, 150, 140, 43, 55)] for _ in range(ntx)]
+    ids, _ = engine.tx_ids(txs)
+    nsig = [rng.choice([1, 2, 3]) for _ in range(ntx)]
+    keys, sgs = [], []
+    for t in range(ntx):
+        for k in range(nsig[t]):
+            p, s = _sign(oracle, hashlib.sha256(b"k%d" % ((t * 7 + k) % 50)).digest(), ids[t].tobytes())
+            if t % 10 == 3 and k == nsig[t] - 1:
+                s = s[:40] + bytes([s[40] ^ 4]) + s[41:]
+            keys.append(p)
+            sgs.append(s)
+    dev = torch.device("cuda:0")
+    leaves = [x for tx in txs for x in tx]
+    lb = torch.tensor(np.frombuffer(b"".join(leaves), np.uint8), device=dev)
+    lo = torch.tensor(np.concatenate([[0], np.cumsum([len(x) for x in leaves])]).astype(np.int64), device=dev)
+    tlo = torch.tensor(np.arange(0, 5 * ntx + 1, 5, dtype=np.int64), device=dev)
+    tso = torch.tensor(np.concatenate([[0], np.cumsum(nsig)]).astype(np.int64), device=dev)
+    k = torch.tensor(np.frombuffer(b"".join(keys), np.uint8).reshape(-1, 32), device=dev)
+    s = torch.tensor(np.frombuffer(b"".join(sgs), np.uint8).reshape(-1, 64), device=dev)
+    txid = torch.empty((ntx, 32), dtype=torch.uint8, device=dev)
+    tst = torch.empty(ntx, dtype=torch.uint8, device=dev)
+    fb = torch.empty(ntx, dtype=torch.int64, device=dev)
+    sst = torch.empty(len(keys), dtype=torch.uint8, device=dev)
+    engine.signed_tx_verify_ed25519_device(lb, lo, tlo, tso, k, s, txid, tst, fb, sst)
+    torch.cuda.synchronize()
+    assert np.array_equal(txid.cpu().numpy(), ids)
+    want_bad = [(nsig[t] - 1 if t % 10 == 3 else -1) for t in range(ntx)]
+    assert list(fb.cpu().numpy()) == want_bad
+    assert list(tst.cpu().numpy()) == [1 if t % 10 == 3 else 0 for t in range(ntx)]

@@ -125,3 +125,21 @@ def test_merkle_reference_structure(oracle):
     h2 = hashlib.sha256(hashed[2] + bytes(32)).digest()
     oracle.oracle_merkle_root(b"".join(hashed[:3]), 3, root)
     assert root.raw == hashlib.sha256(h1 + h2).digest()
+
+
+def test_tx_id_oracle_matches_golden(oracle):
+    import json
+    import os
+    import numpy as np
+    path = os.path.join(os.path.dirname(__file__), "golden", "merkle_vectors.json")
+    for tx in json.load(open(path))["txs"]:
+        leaves = [bytes.fromhex(x) for x in tx["leaves"]]
+        blob = np.frombuffer(b"".join(leaves) or b"\0", np.uint8).copy()
+        off = np.zeros(len(leaves) + 1, np.uint64)
+        off[1:] = np.cumsum([len(x) for x in leaves])
+        out = ctypes.create_string_buffer(32)
+        rc = oracle.oracle_tx_id(blob.ctypes.data, off.ctypes.data, len(leaves), out)
+        if tx["id"] is None:
+            assert rc == -1
+        else:
+            assert rc == 0 and out.raw.hex() == tx["id"], tx["name"]
