@@ -53,6 +53,14 @@ void oracle_ed25519_sign(const uint8_t seed[32], const uint8_t* msg, size_t msgl
  * (MerkleTreeException, MerkleTree.kt:49-50). */
 int oracle_merkle_root(const uint8_t* leaves, size_t nleaves, uint8_t root[32]);
 
+/* Per-lane status of Crypto.isValid(ECDSA_SECP256K1_SHA256 (2) | ECDSA_SECP256R1_SHA256 (3),
+ * SEC1 key, DER sig, msg) with BouncyCastle 1.57 semantics (oracle/bc_ecdsa.py). */
+int oracle_ecdsa_verify(int scheme, const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
+                        const uint8_t* msg, size_t msglen);
+void oracle_ecdsa_verify_batch(size_t n, const uint8_t* scheme, const uint8_t* key, const uint64_t* key_off,
+                               const uint8_t* sig, const uint64_t* sig_off, const uint8_t* msg,
+                               const uint64_t* msg_off, uint8_t* status, int nthreads);
+
 /* WireTransaction.id from the serialised components (leaf preimages, CSR). */
 int oracle_tx_id(const uint8_t* leaf_bytes, const uint64_t* leaf_off, size_t nleaves, uint8_t id[32]);
 

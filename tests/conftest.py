@@ -37,6 +37,8 @@ def load_oracle():
     lib.oracle_sha512.argtypes = [cp, sz, ctypes.c_char_p]
     lib.oracle_merkle_root.argtypes = [cp, sz, ctypes.c_char_p]
     lib.oracle_slide.argtypes = [cp, ctypes.c_char_p]
+    lib.oracle_ecdsa_verify.argtypes = [ctypes.c_int, cp, sz, cp, sz, cp, sz]
+    lib.oracle_ecdsa_verify_batch.argtypes = [sz] + [ctypes.c_void_p] * 8 + [ctypes.c_void_p, ctypes.c_int]
     lib.oracle_tx_id.argtypes = [ctypes.c_void_p, ctypes.c_void_p, sz, ctypes.c_char_p]
     return lib
 
@@ -49,6 +51,14 @@ def oracle():
 @pytest.fixture(scope="session")
 def ed_vectors():
     with open(os.path.join(ROOT, "tests", "golden", "ed25519_vectors.json")) as f:
+        vs = json.load(f)["vectors"]
+    return [dict(v, pub=bytes.fromhex(v["pub"]), sig=bytes.fromhex(v["sig"]), msg=bytes.fromhex(v["msg"]))
+            for v in vs]
+
+
+@pytest.fixture(scope="session")
+def ec_vectors():
+    with open(os.path.join(ROOT, "tests", "golden", "ecdsa_vectors.json")) as f:
         vs = json.load(f)["vectors"]
     return [dict(v, pub=bytes.fromhex(v["pub"]), sig=bytes.fromhex(v["sig"]), msg=bytes.fromhex(v["msg"]))
             for v in vs]

@@ -143,3 +143,28 @@ def test_tx_id_oracle_matches_golden(oracle):
             assert rc == -1
         else:
             assert rc == 0 and out.raw.hex() == tx["id"], tx["name"]
+
+
+def test_ecdsa_c_oracle_matches_golden(oracle, ec_vectors):
+    for v in ec_vectors:
+        p, s, m = v["pub"], v["sig"], v["msg"]
+        got = oracle.oracle_ecdsa_verify(v["scheme"], p, len(p), s, len(s), m, len(m))
+        assert got == v["status"], (v["cat"], v["scheme"], v["note"], got, v["status"])
+
+
+def test_ecdsa_python_oracle_sample(ec_vectors):
+    import bc_ecdsa as ec
+    rng = random.Random(8)
+    for v in rng.sample(ec_vectors, 40):
+        assert ec.verify_status(v["scheme"], v["pub"], v["sig"], v["msg"]) == v["status"], v["cat"]
+
+
+def test_ecdsa_golden_covers_catalogue(ec_vectors):
+    cats = {(v["cat"], v["status"]) for v in ec_vectors}
+    for c in ("valid", "valid_compressed", "high_s", "x_ge_n"):
+        assert (c, 0) in cats
+    for c in ("der_long_len", "der_trailing", "der_nonminimal_int", "der_wrong_tag", "der_indefinite"):
+        assert (c, 2) in cats
+    for c in ("r_zero", "s_ge_n", "r_negative"):
+        assert (c, 1) in cats
+    assert ("key_off_curve", 3) in cats and ("key_x_ge_p", 3) in cats
