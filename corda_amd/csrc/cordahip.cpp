@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/cordahip.h"
+#include "der.hpp"
 #include "status.hpp"
 
 namespace cordahip {
@@ -42,6 +43,14 @@ hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, u
                               hipStream_t s);
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
                             uint8_t* tx_status, hipStream_t s);
+size_t ecdsa_gtable_bytes();
+hipError_t launch_ecdsa_gtables(uint32_t* k1, uint32_t* r1, hipStream_t s);
+hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
+                               const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs,
+                               const uint64_t* msg_off, uint32_t msg_len, uint64_t n, const uint32_t* gk1,
+                               const uint32_t* gr1, const uint8_t* pre_status, uint8_t* status,
+                               unsigned long long* verdict, unsigned int* counters6, unsigned int* perm,
+                               hipStream_t s);
 }  // namespace cordahip
 
 using namespace cordahip;
@@ -75,9 +84,17 @@ struct TxWork {  // device buffers of the transaction paths (grow-only)
   DevBuf leaf_bytes, leaf_off, tx_leaf_off, hashes, txid, tx_status, tx_sig_off, msgs;
 };
 
+struct EcWork {  // device buffers of the ECDSA paths (grow-only)
+  DevBuf scheme, keys, key_len, sigs, sig_len, msgs, msg_off, pre, status, counters, perm;
+};
+
 struct Device {
   int id = 0;
   uint32_t* btab = nullptr;
+  uint32_t* gtab_k1 = nullptr;  // [k]G tables, k = 0..128, secp256k1 / P-256
+  uint32_t* gtab_r1 = nullptr;
+  std::mutex ec_mu;
+  EcWork ec;
   hipStream_t stream = nullptr;  // context stream (init-time work and host tx paths)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = -1.0;
@@ -178,6 +195,68 @@ int ed25519_dense_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* si
   return rc;
 }
 
+// ECDSA lanes of a generic batch: pack into the kernel's slot layout (65-byte
+// keys, 72-byte DER slots, CSR messages) and run K2 on one device. Signatures
+// longer than 72 bytes cannot hold r, s < n (some INTEGER needs > 33 bytes):
+// the host decides them with the same DER rules (der.hpp), the kernel still
+// decodes the key first so key errors keep precedence.
+int ecdsa_host_lanes(cordahip_ctx* ctx, const cordahip_sig_batch* b, const std::vector<uint64_t>& lanes) {
+  const uint64_t m = lanes.size();
+  std::vector<uint8_t> sch(m), keys(m * 65, 0), klen(m), sigs(m * 72, 0), slen(m), pre(m, 0), st(m);
+  std::vector<uint64_t> moff(m + 1, 0);
+  for (uint64_t j = 0; j < m; j++) moff[j + 1] = moff[j] + (b->msg_off[lanes[j] + 1] - b->msg_off[lanes[j]]);
+  std::vector<uint8_t> msgs(std::max<uint64_t>(moff[m], 1));
+  for (uint64_t j = 0; j < m; j++) {
+    const uint64_t i = lanes[j];
+    sch[j] = b->scheme[i];
+    const uint64_t kl = b->key_off[i + 1] - b->key_off[i];
+    std::memcpy(&keys[j * 65], b->key + b->key_off[i], kl);
+    klen[j] = (uint8_t)kl;
+    const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
+    const uint64_t ml = b->msg_off[i + 1] - b->msg_off[i];
+    if (sl <= 72) {
+      std::memcpy(&sigs[j * 72], b->sig + b->sig_off[i], sl);
+      slen[j] = (uint8_t)sl;
+    } else {
+      DerInt r, s;
+      pre[j] = ml == 0 ? CORDAHIP_STATUS_EMPTY
+                       : der_decode_sig(b->sig + b->sig_off[i], (uint32_t)std::min<uint64_t>(sl, 0xffffffffu), r, s)
+                             ? CORDAHIP_STATUS_BAD_SIG
+                             : CORDAHIP_STATUS_MALFORMED_SIG;
+      slen[j] = 72;
+    }
+    std::memcpy(&msgs[moff[j]], b->msg + b->msg_off[i], ml);
+  }
+  Device& d = *ctx->devs[0];
+  std::lock_guard<std::mutex> g(d.ec_mu);
+  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  EcWork& w = d.ec;
+  if (w.scheme.ensure(m) || w.keys.ensure(m * 65) || w.key_len.ensure(m) || w.sigs.ensure(m * 72) ||
+      w.sig_len.ensure(m) || w.msgs.ensure(msgs.size()) || w.msg_off.ensure((m + 1) * 8) || w.pre.ensure(m) ||
+      w.status.ensure(m) || w.counters.ensure(64) || w.perm.ensure(m * 4))
+    return CORDAHIP_ERR_OUT_OF_MEMORY;
+  hipStream_t s = d.stream;
+  hipError_t e = hipMemcpyAsync(w.scheme.p, sch.data(), m, hipMemcpyHostToDevice, s);
+  e = e ? e : hipMemcpyAsync(w.keys.p, keys.data(), m * 65, hipMemcpyHostToDevice, s);
+  e = e ? e : hipMemcpyAsync(w.key_len.p, klen.data(), m, hipMemcpyHostToDevice, s);
+  e = e ? e : hipMemcpyAsync(w.sigs.p, sigs.data(), m * 72, hipMemcpyHostToDevice, s);
+  e = e ? e : hipMemcpyAsync(w.sig_len.p, slen.data(), m, hipMemcpyHostToDevice, s);
+  e = e ? e : hipMemcpyAsync(w.msgs.p, msgs.data(), msgs.size(), hipMemcpyHostToDevice, s);
+  e = e ? e : hipMemcpyAsync(w.msg_off.p, moff.data(), (m + 1) * 8, hipMemcpyHostToDevice, s);
+  e = e ? e : hipMemcpyAsync(w.pre.p, pre.data(), m, hipMemcpyHostToDevice, s);
+  e = e ? e
+        : launch_ecdsa_verify(w.scheme.as<uint8_t>(), w.keys.as<uint8_t>(), w.key_len.as<uint8_t>(),
+                              w.sigs.as<uint8_t>(), w.sig_len.as<uint8_t>(), w.msgs.as<uint8_t>(),
+                              w.msg_off.as<uint64_t>(), 0, m, d.gtab_k1, d.gtab_r1, w.pre.as<uint8_t>(),
+                              w.status.as<uint8_t>(), nullptr, w.counters.as<unsigned int>(),
+                              w.perm.as<unsigned int>(), s);
+  e = e ? e : hipMemcpyAsync(st.data(), w.status.p, m, hipMemcpyDeviceToHost, s);
+  e = e ? e : hipStreamSynchronize(s);
+  if (e != hipSuccess) return CORDAHIP_ERR_HIP;
+  for (uint64_t j = 0; j < m; j++) b->status[lanes[j]] = st[j];
+  return CORDAHIP_SUCCESS;
+}
+
 // Generic CSR batch: host-side scheme partition and length checks (the
 // Crypto.doVerify require() checks), then one dense device launch per
 // (scheme, message length) group.
@@ -187,10 +266,18 @@ int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
   if (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off || !b->msg || !b->msg_off || !b->status)
     return CORDAHIP_ERR_INVALID_ARG;
   std::map<uint64_t, std::vector<uint64_t>> ed_groups;  // msg length -> lanes
+  std::vector<uint64_t> ec_lanes;
   for (uint64_t i = 0; i < n; i++) {
     const uint8_t sch = b->scheme[i];
-    if (sch == CORDAHIP_SCHEME_ECDSA_SECP256K1_SHA256 || sch == CORDAHIP_SCHEME_ECDSA_SECP256R1_SHA256)
-      return CORDAHIP_ERR_NOT_IMPLEMENTED;  // caller keeps these batches on the JVM path
+    if (sch == CORDAHIP_SCHEME_ECDSA_SECP256K1_SHA256 || sch == CORDAHIP_SCHEME_ECDSA_SECP256R1_SHA256) {
+      const uint64_t kl = b->key_off[i + 1] - b->key_off[i];
+      if (kl != 33 && kl != 65) {
+        b->status[i] = CORDAHIP_STATUS_BAD_KEY;  // ECCurve.decodePoint: invalid point encoding
+        continue;
+      }
+      ec_lanes.push_back(i);
+      continue;
+    }
     if (sch != CORDAHIP_SCHEME_EDDSA_ED25519_SHA512) {
       b->status[i] = CORDAHIP_STATUS_UNSUPPORTED;  // Crypto.kt:474 require(isSupportedSignatureScheme)
       continue;
@@ -220,6 +307,10 @@ int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
                                       st.data(), nullptr);
     if (rc != CORDAHIP_SUCCESS) return rc;
     for (uint64_t j = 0; j < m; j++) b->status[idx[j]] = st[j];
+  }
+  if (!ec_lanes.empty()) {
+    const int rc = ecdsa_host_lanes(ctx, b, ec_lanes);
+    if (rc != CORDAHIP_SUCCESS) return rc;
   }
   if (b->verdict) verdict_from_status(b->status, n, b->verdict);
   return CORDAHIP_SUCCESS;
@@ -357,6 +448,10 @@ int cordahip_init(uint32_t device_mask, cordahip_ctx** out) {
     if (hipMalloc(reinterpret_cast<void**>(&dev->btab), ed25519_btable_bytes()) != hipSuccess)
       return CORDAHIP_ERR_OUT_OF_MEMORY;
     if (launch_ed25519_btable(dev->btab, dev->stream) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (hipMalloc(reinterpret_cast<void**>(&dev->gtab_k1), ecdsa_gtable_bytes()) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dev->gtab_r1), ecdsa_gtable_bytes()) != hipSuccess)
+      return CORDAHIP_ERR_OUT_OF_MEMORY;
+    if (launch_ecdsa_gtables(dev->gtab_k1, dev->gtab_r1, dev->stream) != hipSuccess) return CORDAHIP_ERR_HIP;
     if (hipStreamSynchronize(dev->stream) != hipSuccess) return CORDAHIP_ERR_HIP;
     ctx->devs.push_back(std::move(dev));
   }
@@ -382,6 +477,11 @@ void cordahip_shutdown(cordahip_ctx* ctx) {
     for (DevBuf* b : {&d->tx.leaf_bytes, &d->tx.leaf_off, &d->tx.tx_leaf_off, &d->tx.hashes, &d->tx.txid,
                       &d->tx.tx_status, &d->tx.tx_sig_off, &d->tx.msgs})
       if (b->p) (void)hipFree(b->p);
+    for (DevBuf* b : {&d->ec.scheme, &d->ec.keys, &d->ec.key_len, &d->ec.sigs, &d->ec.sig_len, &d->ec.msgs,
+                      &d->ec.msg_off, &d->ec.pre, &d->ec.status, &d->ec.counters, &d->ec.perm})
+      if (b->p) (void)hipFree(b->p);
+    if (d->gtab_k1) (void)hipFree(d->gtab_k1);
+    if (d->gtab_r1) (void)hipFree(d->gtab_r1);
     if (d->btab) (void)hipFree(d->btab);
     if (d->ev0) (void)hipEventDestroy(d->ev0);
     if (d->ev1) (void)hipEventDestroy(d->ev1);
@@ -458,6 +558,28 @@ int cordahip_ed25519_verify_device(cordahip_ctx* ctx, int device, const void* d_
         : launch_ed25519_verify(static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
                                 static_cast<const uint8_t*>(d_msgs), msg_len, n, d->btab, nullptr,
                                 static_cast<uint8_t*>(d_status), static_cast<unsigned long long*>(d_verdict), s);
+  e = e ? e : hipEventRecord(d->ev1, s);
+  return hip_err(e);
+}
+
+int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_scheme, const void* d_keys,
+                                 const void* d_key_len, const void* d_sigs, const void* d_sig_len, const void* d_msgs,
+                                 uint32_t msg_len, uint64_t n, void* d_status, void* d_verdict, void* hip_stream) {
+  Device* d = dev_at(ctx, device);
+  if (!d || (n && (!d_scheme || !d_keys || !d_key_len || !d_sigs || !d_sig_len || !d_status || (msg_len && !d_msgs))))
+    return CORDAHIP_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(d->ec_mu);
+  if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  if (d->ec.counters.ensure(64) || d->ec.perm.ensure(std::max<uint64_t>(n, 1) * 4)) return CORDAHIP_ERR_OUT_OF_MEMORY;
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  hipError_t e = hipEventRecord(d->ev0, s);
+  e = e ? e
+        : launch_ecdsa_verify(static_cast<const uint8_t*>(d_scheme), static_cast<const uint8_t*>(d_keys),
+                              static_cast<const uint8_t*>(d_key_len), static_cast<const uint8_t*>(d_sigs),
+                              static_cast<const uint8_t*>(d_sig_len), static_cast<const uint8_t*>(d_msgs), nullptr,
+                              msg_len, n, d->gtab_k1, d->gtab_r1, nullptr, static_cast<uint8_t*>(d_status),
+                              static_cast<unsigned long long*>(d_verdict), d->ec.counters.as<unsigned int>(),
+                              d->ec.perm.as<unsigned int>(), s);
   e = e ? e : hipEventRecord(d->ev1, s);
   return hip_err(e);
 }

@@ -1,0 +1,592 @@
+// ECDSA (ECDSA_SECP256K1_SHA256 = 2, ECDSA_SECP256R1_SHA256 = 3) batch
+// verification for gfx950 — kernel K2.
+//
+// Replaces, per lane, Crypto.isValid for the two ECDSA schemes
+// (core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:91-116, :534-541)
+// -> JCA "SHA256withECDSA" -> BouncyCastle 1.57 DSABase.engineVerify /
+// ECDSASigner.verifySignature (semantics: SURVEY App. A.2, restated in
+// oracle/bc_ecdsa.py and oracle/c/ecdsa.c):
+//   key: SEC1 point, coordinates < p, on the curve (else BAD_KEY);
+//   sig: strict DER (der.hpp) else MALFORMED_SIG; r, s in [1, n-1] else BAD_SIG;
+//   e = SHA-256(msg); w = s^-1; P = (e w) G + (r w) Q; accept iff P != O and
+//   x(P) mod n == r, checked inversion-free as X == r Z^2 or (r + n) Z^2.
+// One lane per signature; lanes are permuted so each wave holds one curve
+// (device-side partition kernels below), so the two curves' code never
+// diverges inside a wave except at the single boundary wave.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "der.hpp"
+#include "mp256.hpp"
+#include "sc25519.hpp"
+#include "sha2_device.hpp"
+#include "status.hpp"
+
+namespace cordahip {
+
+#define CH_LIMBS(name, a0, a1, a2, a3, a4, a5, a6, a7)                                              \
+  CDEV static constexpr uint32_t name(int i) {                                                      \
+    return i == 0 ? a0 : i == 1 ? a1 : i == 2 ? a2 : i == 3 ? a3 : i == 4 ? a4 : i == 5 ? a5 : i == 6 ? a6 : a7; \
+  }
+
+struct K1P {
+  CH_LIMBS(limb, 0xfffffc2fu, 0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu)
+  CH_LIMBS(r2, 0x000e90a1u, 0x000007a2u, 0x00000001u, 0u, 0u, 0u, 0u, 0u)
+  static constexpr uint32_t kMinv = 0xd2253531u;
+};
+struct K1N {
+  CH_LIMBS(limb, 0xd0364141u, 0xbfd25e8cu, 0xaf48a03bu, 0xbaaedce6u, 0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu)
+  CH_LIMBS(r2, 0x67d7d140u, 0x896cf214u, 0x0e7cf878u, 0x741496c2u, 0x5bcd07c6u, 0xe697f5e4u, 0x81c69bc5u, 0x9d671cd5u)
+  static constexpr uint32_t kMinv = 0x5588b13fu;
+};
+struct R1P {
+  CH_LIMBS(limb, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u, 0x00000001u, 0xffffffffu)
+  CH_LIMBS(r2, 0x00000003u, 0u, 0xffffffffu, 0xfffffffbu, 0xfffffffeu, 0xffffffffu, 0xfffffffdu, 0x00000004u)
+  static constexpr uint32_t kMinv = 0x00000001u;
+};
+struct R1N {
+  CH_LIMBS(limb, 0xfc632551u, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu, 0xffffffffu, 0xffffffffu, 0u, 0xffffffffu)
+  CH_LIMBS(r2, 0xbe79eea2u, 0x83244c95u, 0x49bd6fa6u, 0x4699799cu, 0x2b6bec59u, 0x2845b239u, 0xf3d95620u, 0x66e12d94u)
+  static constexpr uint32_t kMinv = 0xee00bc4fu;
+};
+// exponents: (p+1)/4 (square root, p = 3 mod 4), p-2 and n-2 (Fermat inversion)
+struct K1Sqrt { CH_LIMBS(limb, 0xbfffff0cu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x3fffffffu) };
+struct K1Pm2 { CH_LIMBS(limb, 0xfffffc2du, 0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu) };
+struct K1Nm2 { CH_LIMBS(limb, 0xd036413fu, 0xbfd25e8cu, 0xaf48a03bu, 0xbaaedce6u, 0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu) };
+struct R1Sqrt { CH_LIMBS(limb, 0u, 0u, 0x40000000u, 0u, 0u, 0x40000000u, 0xc0000000u, 0x3fffffffu) };
+struct R1Pm2 { CH_LIMBS(limb, 0xfffffffdu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u, 0x00000001u, 0xffffffffu) };
+struct R1Nm2 { CH_LIMBS(limb, 0xfc63254fu, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu, 0xffffffffu, 0xffffffffu, 0u, 0xffffffffu) };
+
+struct K1B { CH_LIMBS(limb, 0x00001ab7u, 0x00000007u, 0u, 0u, 0u, 0u, 0u, 0u) };
+struct K1PmN { CH_LIMBS(limb, 0x22fc9baeu, 0x402da172u, 0x50b75fc4u, 0x45512319u, 0x00000001u, 0u, 0u, 0u) };
+struct K1Gx { CH_LIMBS(limb, 0x487e2097u, 0xd7362e5au, 0x29bc66dbu, 0x231e2953u, 0x33fd129cu, 0x979f48c0u, 0xe9089f48u, 0x9981e643u) };
+struct K1Gy { CH_LIMBS(limb, 0xd3dbabe2u, 0xb15ea6d2u, 0x1f1dc64du, 0x8dfc5d5du, 0xac19c136u, 0x70b6b59au, 0xd4a582d6u, 0xcf3f851fu) };
+struct R1B { CH_LIMBS(limb, 0x29c4bddfu, 0xd89cdf62u, 0x78843090u, 0xacf005cdu, 0xf7212ed6u, 0xe5a220abu, 0x04874834u, 0xdc30061du) };
+struct R1PmN { CH_LIMBS(limb, 0x039cdaaeu, 0x0c46353du, 0x58e8617bu, 0x43190553u, 0u, 0u, 0u, 0u) };
+struct R1Gx { CH_LIMBS(limb, 0x18a9143cu, 0x79e730d4u, 0x5fedb601u, 0x75ba95fcu, 0x77622510u, 0x79fb732bu, 0xa53755c6u, 0x18905f76u) };
+struct R1Gy { CH_LIMBS(limb, 0xce95560au, 0xddf25357u, 0xba19e45cu, 0x8b4ab8e4u, 0xdd21f325u, 0xd2e88688u, 0x25885d85u, 0x8571ff18u) };
+
+template <int SCHEME>
+struct Curve;
+template <>
+struct Curve<2> {  // secp256k1: y^2 = x^3 + 7
+  using P = K1P;
+  using N = K1N;
+  using Sqrt = K1Sqrt;
+  using Pm2 = K1Pm2;
+  using Nm2 = K1Nm2;
+  static constexpr bool kAm3 = false;
+  using B = K1B;
+  using PmN = K1PmN;
+  using Gx = K1Gx;
+  using Gy = K1Gy;
+};
+template <>
+struct Curve<3> {  // secp256r1 / P-256: y^2 = x^3 - 3x + b
+  using P = R1P;
+  using N = R1N;
+  using Sqrt = R1Sqrt;
+  using Pm2 = R1Pm2;
+  using Nm2 = R1Nm2;
+  static constexpr bool kAm3 = true;
+  using B = R1B;
+  using PmN = R1PmN;
+  using Gx = R1Gx;
+  using Gy = R1Gy;
+};
+
+template <class F>
+CDEV u256 limbs_of() {
+  u256 r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = F::limb(i);
+  return r;
+}
+
+template <class M>
+CDEV void to_mont(u256& r, const u256& a) {
+  u256 r2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r2.v[i] = M::r2(i);
+  mont_mul<M>(r, a, r2);
+}
+template <class M>
+CDEV void from_mont(u256& r, const u256& a) {
+  u256 one;
+#pragma unroll
+  for (int i = 0; i < 8; i++) one.v[i] = i == 0;
+  mont_mul<M>(r, a, one);
+}
+
+// ---- Jacobian points (Montgomery-form coordinates) --------------------------
+struct jpt {
+  u256 X, Y, Z;
+  bool inf;
+};
+
+// 2P. a = -3: dbl-2001-b (3M + 5S); a = 0: dbl-2009-l (2M + 5S). Prime-order
+// curves have no 2-torsion, so only the point at infinity is exceptional.
+template <class C>
+CDEV void jdbl(jpt& r, const jpt& p) {
+  using P = typename C::P;
+  if (p.inf) {
+    r.inf = true;
+    return;
+  }
+  u256 x3, y3, z3;
+  if (C::kAm3) {
+    u256 delta, gamma, beta, alpha, t, u;
+    mont_sqr<P>(delta, p.Z);
+    mont_sqr<P>(gamma, p.Y);
+    mont_mul<P>(beta, p.X, gamma);
+    mod_sub<P>(t, p.X, delta);
+    mod_add<P>(u, p.X, delta);
+    mont_mul<P>(alpha, t, u);
+    mod_add<P>(t, alpha, alpha);
+    mod_add<P>(alpha, alpha, t);  // 3 (X - delta)(X + delta)
+    mont_sqr<P>(x3, alpha);
+    mod_add<P>(t, beta, beta);
+    mod_add<P>(t, t, t);          // 4 beta
+    mod_add<P>(u, t, t);          // 8 beta
+    mod_sub<P>(x3, x3, u);
+    mod_add<P>(z3, p.Y, p.Z);
+    mont_sqr<P>(z3, z3);
+    mod_sub<P>(z3, z3, gamma);
+    mod_sub<P>(z3, z3, delta);
+    mod_sub<P>(u, t, x3);
+    mont_mul<P>(y3, alpha, u);
+    mont_sqr<P>(u, gamma);
+    mod_add<P>(u, u, u);
+    mod_add<P>(u, u, u);
+    mod_add<P>(u, u, u);          // 8 gamma^2
+    mod_sub<P>(y3, y3, u);
+  } else {
+    u256 A, B, Cc, D, E, F, t;
+    mont_sqr<P>(A, p.X);
+    mont_sqr<P>(B, p.Y);
+    mont_sqr<P>(Cc, B);
+    mod_add<P>(t, p.X, B);
+    mont_sqr<P>(t, t);
+    mod_sub<P>(t, t, A);
+    mod_sub<P>(t, t, Cc);
+    mod_add<P>(D, t, t);
+    mod_add<P>(E, A, A);
+    mod_add<P>(E, E, A);
+    mont_sqr<P>(F, E);
+    mod_add<P>(t, D, D);
+    mod_sub<P>(x3, F, t);
+    mod_sub<P>(t, D, x3);
+    mont_mul<P>(y3, E, t);
+    mod_add<P>(t, Cc, Cc);
+    mod_add<P>(t, t, t);
+    mod_add<P>(t, t, t);          // 8 C
+    mod_sub<P>(y3, y3, t);
+    mont_mul<P>(z3, p.Y, p.Z);
+    mod_add<P>(z3, z3, z3);
+  }
+  r.X = x3;
+  r.Y = y3;
+  r.Z = z3;
+  r.inf = false;
+}
+
+// P + Q, both Jacobian (add-2007-bl, 11M + 5S), with the exceptional cases
+template <class C>
+CDEV void jadd(jpt& r, const jpt& p, const jpt& q) {
+  using P = typename C::P;
+  if (p.inf) {
+    r = q;
+    return;
+  }
+  if (q.inf) {
+    r = p;
+    return;
+  }
+  u256 z1z1, z2z2, u1, u2, s1, s2, h, rr, t;
+  mont_sqr<P>(z1z1, p.Z);
+  mont_sqr<P>(z2z2, q.Z);
+  mont_mul<P>(u1, p.X, z2z2);
+  mont_mul<P>(u2, q.X, z1z1);
+  mont_mul<P>(t, p.Y, q.Z);
+  mont_mul<P>(s1, t, z2z2);
+  mont_mul<P>(t, q.Y, p.Z);
+  mont_mul<P>(s2, t, z1z1);
+  mod_sub<P>(h, u2, u1);
+  mod_sub<P>(rr, s2, s1);
+  if (u256_iszero(h)) {
+    if (u256_iszero(rr)) {
+      jdbl<C>(r, p);
+    } else {
+      r.inf = true;
+    }
+    return;
+  }
+  u256 i, j, v, x3, y3, z3;
+  mod_add<P>(t, h, h);
+  mont_sqr<P>(i, t);
+  mont_mul<P>(j, h, i);
+  mod_add<P>(rr, rr, rr);
+  mont_mul<P>(v, u1, i);
+  mont_sqr<P>(x3, rr);
+  mod_sub<P>(x3, x3, j);
+  mod_sub<P>(x3, x3, v);
+  mod_sub<P>(x3, x3, v);
+  mod_sub<P>(t, v, x3);
+  mont_mul<P>(y3, rr, t);
+  mont_mul<P>(t, s1, j);
+  mod_add<P>(t, t, t);
+  mod_sub<P>(y3, y3, t);
+  mod_add<P>(t, p.Z, q.Z);
+  mont_sqr<P>(t, t);
+  mod_sub<P>(t, t, z1z1);
+  mod_sub<P>(t, t, z2z2);
+  mont_mul<P>(z3, t, h);
+  r.X = x3;
+  r.Y = y3;
+  r.Z = z3;
+  r.inf = false;
+}
+
+// P + (x2, y2) affine (madd-2007-bl, 7M + 4S)
+template <class C>
+CDEV void jmadd(jpt& r, const jpt& p, const u256& x2, const u256& y2) {
+  using P = typename C::P;
+  if (p.inf) {
+    r.X = x2;
+    r.Y = y2;
+    u256 one;  // Z = 1, i.e. 2^256 mod p in Montgomery form
+#pragma unroll
+    for (int i = 0; i < 8; i++) one.v[i] = i == 0;
+    to_mont<P>(r.Z, one);
+    r.inf = false;
+    return;
+  }
+  u256 z1z1, u2, s2, h, hh, i, j, rr, v, t, x3, y3, z3;
+  mont_sqr<P>(z1z1, p.Z);
+  mont_mul<P>(u2, x2, z1z1);
+  mont_mul<P>(t, y2, p.Z);
+  mont_mul<P>(s2, t, z1z1);
+  mod_sub<P>(h, u2, p.X);
+  mod_sub<P>(rr, s2, p.Y);
+  if (u256_iszero(h)) {
+    if (u256_iszero(rr)) {
+      jdbl<C>(r, p);
+    } else {
+      r.inf = true;
+    }
+    return;
+  }
+  mont_sqr<P>(hh, h);
+  mod_add<P>(i, hh, hh);
+  mod_add<P>(i, i, i);
+  mont_mul<P>(j, h, i);
+  mod_add<P>(rr, rr, rr);
+  mont_mul<P>(v, p.X, i);
+  mont_sqr<P>(x3, rr);
+  mod_sub<P>(x3, x3, j);
+  mod_sub<P>(x3, x3, v);
+  mod_sub<P>(x3, x3, v);
+  mod_sub<P>(t, v, x3);
+  mont_mul<P>(y3, rr, t);
+  mont_mul<P>(t, p.Y, j);
+  mod_add<P>(t, t, t);
+  mod_sub<P>(y3, y3, t);
+  mod_add<P>(t, p.Z, h);
+  mont_sqr<P>(t, t);
+  mod_sub<P>(t, t, z1z1);
+  mod_sub<P>(z3, t, hh);
+  r.X = x3;
+  r.Y = y3;
+  r.Z = z3;
+  r.inf = false;
+}
+
+// ---- G tables: entry k (1..128) = [k]G affine (Montgomery x, y), 16 u32 ------
+static constexpr int kGEntries = 129;
+static constexpr int kGEntryWords = 16;
+
+template <class C>
+__global__ void __launch_bounds__(64) ecdsa_gtable_kernel(uint32_t* __restrict__ tab) {
+  using P = typename C::P;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= kGEntries) return;
+  uint32_t* o = tab + k * kGEntryWords;
+  if (k == 0) {
+    for (int i = 0; i < kGEntryWords; i++) o[i] = 0;
+    return;
+  }
+  jpt G, R;
+  G.X = limbs_of<typename C::Gx>();
+  G.Y = limbs_of<typename C::Gy>();
+  u256 one;
+#pragma unroll
+  for (int i = 0; i < 8; i++) one.v[i] = i == 0;
+  to_mont<P>(G.Z, one);
+  G.inf = false;
+  R.inf = true;
+  for (int bit = 7; bit >= 0; bit--) {
+    jdbl<C>(R, R);
+    if ((k >> bit) & 1) jadd<C>(R, R, G);
+  }
+  u256 zi, zi2, x, y;
+  mont_pow_const<P, typename C::Pm2>(zi, R.Z);
+  mont_sqr<P>(zi2, zi);
+  mont_mul<P>(x, R.X, zi2);
+  mont_mul<P>(zi2, zi2, zi);
+  mont_mul<P>(y, R.Y, zi2);
+  for (int i = 0; i < 8; i++) {
+    o[i] = x.v[i];
+    o[8 + i] = y.v[i];
+  }
+}
+
+CDEV void load_g(u256& x, u256& y, const uint32_t* __restrict__ tab, int idx) {
+  const uint4* e = reinterpret_cast<const uint4*>(tab + idx * kGEntryWords);
+  const uint4 a = e[0], b = e[1], c = e[2], d = e[3];
+  x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
+  x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+  y.v[0] = c.x; y.v[1] = c.y; y.v[2] = c.z; y.v[3] = c.w;
+  y.v[4] = d.x; y.v[5] = d.y; y.v[6] = d.z; y.v[7] = d.w;
+}
+
+// SEC1 point decode + validation (BC ECCurve.decodePoint); Montgomery form
+template <class C>
+CDEV bool decode_key(jpt& Q, const uint8_t* __restrict__ key, uint32_t len) {
+  using P = typename C::P;
+  const u256 pm = mod_m<P>();
+  u256 x, y, xm, ym, rhs, t;
+  const bool unc = (len == 65 && key[0] == 4);
+  const bool cmp = (len == 33 && (key[0] == 2 || key[0] == 3));
+  if (!unc && !cmp) return false;
+  u256_from_be_bytes(x, key + 1);
+  if (u256_geq(x, pm)) return false;
+  to_mont<P>(xm, x);
+  // rhs = x^3 + a x + b
+  mont_sqr<P>(rhs, xm);
+  mont_mul<P>(rhs, rhs, xm);
+  if (C::kAm3) {
+    mod_sub<P>(rhs, rhs, xm);
+    mod_sub<P>(rhs, rhs, xm);
+    mod_sub<P>(rhs, rhs, xm);
+  }
+  mod_add<P>(rhs, rhs, limbs_of<typename C::B>());
+  if (unc) {
+    u256_from_be_bytes(y, key + 33);
+    if (u256_geq(y, pm)) return false;
+    to_mont<P>(ym, y);
+  } else {
+    mont_pow_const<P, typename C::Sqrt>(ym, rhs);
+    u256 yp;
+    from_mont<P>(yp, ym);
+    if ((yp.v[0] & 1) != (uint32_t)(key[0] & 1)) mod_neg<P>(ym, ym);
+  }
+  mont_sqr<P>(t, ym);
+  if (!u256_eq(t, rhs)) return false;
+  Q.X = xm;
+  Q.Y = ym;
+  u256 one;
+#pragma unroll
+  for (int i = 0; i < 8; i++) one.v[i] = i == 0;
+  to_mont<P>(Q.Z, one);
+  Q.inf = false;
+  return true;
+}
+
+// scalar k < n -> (k' < 2^255, neg) with [k]X = neg ? -[k']X : [k']X
+template <class N>
+CDEV void split_sign(u256& out, bool& neg, const u256& k) {
+  neg = (k.v[7] >> 31) != 0;
+  u256 t;
+  u256_sub(t, mod_m<N>(), k);
+#pragma unroll
+  for (int i = 0; i < 8; i++) out.v[i] = neg ? t.v[i] : k.v[i];
+}
+
+template <class C>
+CDEV uint8_t ecdsa_verify_lane(const uint8_t* __restrict__ key, uint32_t key_len, const uint8_t* __restrict__ sig,
+                               uint32_t sig_len, const uint8_t* __restrict__ msg, uint64_t msg_len,
+                               const uint32_t* __restrict__ gtab, uint8_t pre_status) {
+  using P = typename C::P;
+  using N = typename C::N;
+  jpt Q;
+  if (!decode_key<C>(Q, key, key_len)) return kStatusBadKey;  // key built before verify
+  if (pre_status != kStatusOk) return pre_status;
+  if (sig_len == 0 || msg_len == 0) return kStatusEmpty;      // Crypto.kt:475-476
+  DerInt dr, ds;
+  if (!der_decode_sig(sig, sig_len, dr, ds)) return kStatusMalformedSig;
+  u256 r, s;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.v[i] = dr.v[i];
+    s.v[i] = ds.v[i];
+  }
+  const u256 nm = mod_m<N>();
+  if (dr.neg || dr.big || ds.neg || ds.big || u256_iszero(r) || u256_iszero(s) || u256_geq(r, nm) ||
+      u256_geq(s, nm))
+    return kStatusBadSig;
+  // e = SHA-256(msg) as a big-endian integer, reduced below n
+  uint32_t hw[8];
+  sha256_bytes(hw, msg, msg_len);
+  u256 e;
+#pragma unroll
+  for (int i = 0; i < 8; i++) e.v[i] = hw[7 - i];
+  {
+    u256 t;
+    if (!u256_sub(t, e, nm)) e = t;
+  }
+  // w = s^-1 (Montgomery), u1 = e w, u2 = r w (plain: one Montgomery factor cancels)
+  u256 sm, w, u1, u2;
+  to_mont<N>(sm, s);
+  mont_pow_const<N, typename C::Nm2>(w, sm);
+  mont_mul<N>(u1, e, w);
+  mont_mul<N>(u2, r, w);
+  bool neg1, neg2;
+  split_sign<N>(u1, neg1, u1);
+  split_sign<N>(u2, neg2, u2);
+  // per-lane table: [k]Q, k = 1..8
+  jpt qt[8];
+  qt[0] = Q;
+  jdbl<C>(qt[1], Q);
+  for (int k = 2; k < 8; k++) jadd<C>(qt[k], qt[k - 1], Q);
+  jpt acc;
+  acc.inf = true;
+  for (int j = 63; j >= 0; j--) {
+    if (j != 63) {
+      jdbl<C>(acc, acc);
+      jdbl<C>(acc, acc);
+      jdbl<C>(acc, acc);
+      jdbl<C>(acc, acc);
+    }
+    const int dq = booth_digit<4>(u2.v, j);
+    if (dq != 0) {
+      jpt T = qt[(dq < 0 ? -dq : dq) - 1];
+      if ((dq < 0) != neg2) mod_neg<P>(T.Y, T.Y);
+      jadd<C>(acc, acc, T);
+    }
+    if ((j & 1) == 0) {
+      const int dg = booth_digit<8>(u1.v, j >> 1);
+      if (dg != 0) {
+        u256 gx, gy;
+        load_g(gx, gy, gtab, dg < 0 ? -dg : dg);
+        if ((dg < 0) != neg1) mod_neg<P>(gy, gy);
+        jmadd<C>(acc, acc, gx, gy);
+      }
+    }
+  }
+  if (acc.inf) return kStatusBadSig;
+  // x(P) mod n == r  <=>  X == r Z^2  or (r < p - n and X == (r + n) Z^2)
+  u256 z2, rm, t;
+  mont_sqr<P>(z2, acc.Z);
+  to_mont<P>(rm, r);
+  mont_mul<P>(t, rm, z2);
+  if (u256_eq(t, acc.X)) return kStatusOk;
+  if (!u256_geq(r, limbs_of<typename C::PmN>())) {
+    u256 rn;
+    u256_add(rn, r, nm);
+    to_mont<P>(rm, rn);
+    mont_mul<P>(t, rm, z2);
+    if (u256_eq(t, acc.X)) return kStatusOk;
+  }
+  return kStatusBadSig;
+}
+
+// ---- device-side scheme partition (wave-aggregated atomics) -----------------
+CDEV int scheme_class(uint8_t s) { return s == 2 ? 0 : s == 3 ? 1 : 2; }
+
+__global__ void __launch_bounds__(256) ecdsa_count_kernel(const uint8_t* __restrict__ scheme, uint64_t n,
+                                                         unsigned int* __restrict__ counts) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = i < n ? scheme_class(scheme[i]) : -1;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const unsigned long long m = __ballot(c == k);
+    if (lane == 0 && m) atomicAdd(&counts[k], (unsigned int)__popcll(m));
+  }
+}
+
+__global__ void __launch_bounds__(256) ecdsa_scatter_kernel(const uint8_t* __restrict__ scheme, uint64_t n,
+                                                           const unsigned int* __restrict__ counts,
+                                                           unsigned int* __restrict__ cursors,
+                                                           unsigned int* __restrict__ perm) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = i < n ? scheme_class(scheme[i]) : -1;
+  const int lane = threadIdx.x & 63;
+  const unsigned int base[3] = {0u, counts[0], counts[0] + counts[1]};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const unsigned long long m = __ballot(c == k);
+    if (!m) continue;
+    unsigned int start = 0;
+    if (lane == __ffsll((long long)m) - 1) start = atomicAdd(&cursors[k], (unsigned int)__popcll(m));
+    start = __shfl(start, __ffsll((long long)m) - 1);
+    if (c == k) {
+      const unsigned int rank = __popcll(m & ((1ull << lane) - 1));
+      perm[base[k] + start + rank] = (unsigned int)i;
+    }
+  }
+}
+
+// keys: 65-byte slots + key_len; sigs: 72-byte slots + sig_len; msgs: CSR
+// (msg_off) or fixed stride msg_len. perm may be null (identity).
+__global__ void __launch_bounds__(256) ecdsa_verify_kernel(
+    const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, const uint8_t* __restrict__ keys,
+    const uint8_t* __restrict__ key_len, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ sig_len,
+    const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ msg_off, uint32_t msg_len, uint64_t n,
+    const uint32_t* __restrict__ gtab_k1, const uint32_t* __restrict__ gtab_r1, const uint8_t* __restrict__ pre_status,
+    uint8_t* __restrict__ status) {
+  const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= n) return;
+  const uint64_t i = perm ? perm[slot] : slot;
+  const uint8_t sch = scheme[i];
+  const uint8_t* key = keys + i * 65;
+  const uint8_t* sig = sigs + i * 72;
+  const uint8_t* msg = msg_off ? msgs + msg_off[i] : msgs + i * (uint64_t)msg_len;
+  const uint64_t ml = msg_off ? msg_off[i + 1] - msg_off[i] : msg_len;
+  const uint8_t pre = pre_status ? pre_status[i] : kStatusOk;
+  uint8_t st;
+  if (sch == 2)
+    st = ecdsa_verify_lane<Curve<2>>(key, key_len[i], sig, sig_len[i], msg, ml, gtab_k1, pre);
+  else if (sch == 3)
+    st = ecdsa_verify_lane<Curve<3>>(key, key_len[i], sig, sig_len[i], msg, ml, gtab_r1, pre);
+  else
+    st = kStatusUnsupported;
+  status[i] = st;
+}
+
+__global__ void __launch_bounds__(256) verdict_kernel(const uint8_t* __restrict__ status, uint64_t n,
+                                                     unsigned long long* __restrict__ verdict) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long m = __ballot(i < n && status[i] == kStatusOk);
+  if ((threadIdx.x & 63) == 0 && i < n) verdict[i >> 6] = m;
+}
+
+// ---------------------------------------------------------------------------
+size_t ecdsa_gtable_bytes() { return (size_t)kGEntries * kGEntryWords * sizeof(uint32_t); }
+
+hipError_t launch_ecdsa_gtables(uint32_t* k1, uint32_t* r1, hipStream_t s) {
+  hipLaunchKernelGGL(ecdsa_gtable_kernel<Curve<2>>, dim3((kGEntries + 63) / 64), dim3(64), 0, s, k1);
+  hipLaunchKernelGGL(ecdsa_gtable_kernel<Curve<3>>, dim3((kGEntries + 63) / 64), dim3(64), 0, s, r1);
+  return hipGetLastError();
+}
+
+// partition + verify + verdict; work: counts[3] + cursors[3] (zeroed here) and perm[n]
+hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
+                               const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs,
+                               const uint64_t* msg_off, uint32_t msg_len, uint64_t n, const uint32_t* gk1,
+                               const uint32_t* gr1, const uint8_t* pre_status, uint8_t* status,
+                               unsigned long long* verdict, unsigned int* counters6, unsigned int* perm,
+                               hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const dim3 grid((uint32_t)((n + 255) / 256));
+  hipError_t e = hipMemsetAsync(counters6, 0, 6 * sizeof(unsigned int), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ecdsa_count_kernel, grid, dim3(256), 0, s, scheme, n, counters6);
+  hipLaunchKernelGGL(ecdsa_scatter_kernel, grid, dim3(256), 0, s, scheme, n, counters6, counters6 + 3, perm);
+  hipLaunchKernelGGL(ecdsa_verify_kernel, grid, dim3(256), 0, s, perm, scheme, keys, key_len, sigs, sig_len, msgs,
+                     msg_off, msg_len, n, gk1, gr1, pre_status, status);
+  if (verdict) hipLaunchKernelGGL(verdict_kernel, grid, dim3(256), 0, s, status, n, verdict);
+  return hipGetLastError();
+}
+
+}  // namespace cordahip

@@ -104,4 +104,42 @@ CDEV void sha256_block(uint32_t h[8], uint32_t w[16]) {
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
 
+// big-endian word at byte pos of the SHA-256-padded message p[0..len)
+CDEV uint32_t sha256_padded_word(const uint8_t* __restrict__ p, uint64_t len, uint64_t pos, uint64_t total_bits,
+                                 uint64_t padded_len) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint64_t q = pos + k;
+    uint32_t b;
+    if (q < len) b = p[q];
+    else if (q == len) b = 0x80;
+    else if (q >= padded_len - 8) b = (uint32_t)((total_bits >> (8 * (padded_len - 1 - q))) & 0xff);
+    else b = 0;
+    w = (w << 8) | b;
+  }
+  return w;
+}
+
+// SHA-256 of an arbitrary byte string in global memory (one lane)
+CDEV void sha256_bytes(uint32_t h[8], const uint8_t* __restrict__ p, uint64_t len) {
+  sha256_init(h);
+  const uint64_t padded = ((len + 9 + 63) / 64) * 64;
+  const uint64_t bits = len * 8;
+  uint32_t w[16];
+  for (uint64_t blk = 0; blk < padded; blk += 64) {
+    if (blk + 64 <= len) {  // interior block: plain byte loads
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const uint8_t* b = p + blk + 4 * q;
+        w[q] = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; q++) w[q] = sha256_padded_word(p, len, blk + 4 * q, bits, padded);
+    }
+    sha256_block(h, w);
+  }
+}
+
 }  // namespace cordahip

@@ -145,6 +145,15 @@ class Engine:
             sigs.data_ptr(), keys.shape[0], txid.data_ptr(), tx_status.data_ptr(), first_bad.data_ptr(),
             sig_status.data_ptr(), s), "cordahip_signed_tx_verify_ed25519_device")
 
+    def ecdsa_verify_device(self, scheme, keys, key_len, sigs, sig_len, msgs, status, verdict=None, device: int = 0,
+                            stream=None):
+        """Dense mixed secp256k1/P-256 batch in HBM: keys [n,65] + key_len, DER sigs [n,72] + sig_len."""
+        s = stream.cuda_stream if stream is not None else 0
+        check(lib().cordahip_ecdsa_verify_device(
+            self._ctx, device, scheme.data_ptr(), keys.data_ptr(), key_len.data_ptr(), sigs.data_ptr(),
+            sig_len.data_ptr(), msgs.data_ptr(), msgs.shape[1], scheme.shape[0], status.data_ptr(),
+            verdict.data_ptr() if verdict is not None else None, s), "cordahip_ecdsa_verify_device")
+
     def last_kernel_ms(self, device: int = 0) -> float:
         return lib().cordahip_last_kernel_ms(self._ctx, device)
 

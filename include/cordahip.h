@@ -123,6 +123,15 @@ int cordahip_ed25519_verify_device(cordahip_ctx* ctx, int device, const void* d_
 int cordahip_ed25519_verify_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                                  uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict);
 
+/* ---- dense ECDSA path (secp256k1 = 2 and P-256 = 3 mixed) ------------------ *
+ * scheme[n]; keys in 65-byte slots (SEC1 04||X||Y or 02/03||X) + key_len[n];
+ * DER signatures in 72-byte slots + sig_len[n] (72 = the longest DER encoding of
+ * r, s < 2^256); msgs n*msg_len. Device memory; lanes are partitioned by curve on
+ * the device (one curve per wavefront), status and verdict come back in input order. */
+int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_scheme, const void* d_keys,
+                                 const void* d_key_len, const void* d_sigs, const void* d_sig_len, const void* d_msgs,
+                                 uint32_t msg_len, uint64_t n, void* d_status, void* d_verdict, void* hip_stream);
+
 /* RFC 8032 keygen + sign from 32-byte seeds (device memory): corpus generation. */
 int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_seeds, const void* d_msgs,
                                  uint32_t msg_len, uint64_t n, void* d_pubs, void* d_sigs, void* hip_stream);

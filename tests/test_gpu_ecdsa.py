@@ -1,0 +1,88 @@
+"""K2 parity on the GPU: secp256k1 / P-256 lanes vs the BouncyCastle-1.57 oracle,
+through the C-ABI (generic CSR batch and the dense device path)."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_golden_vectors(engine, ec_vectors):
+    st, verdict = engine.verify_batch([v["scheme"] for v in ec_vectors], [v["pub"] for v in ec_vectors],
+                                      [v["sig"] for v in ec_vectors], [v["msg"] for v in ec_vectors])
+    bad = [(v["cat"], v["scheme"], v["note"], int(s), v["status"]) for v, s in zip(ec_vectors, st)
+           if s != v["status"]]
+    assert not bad, bad[:20]
+
+
+def test_mixed_with_ed25519_and_unsupported(engine, ec_vectors, ed_vectors):
+    vs = ec_vectors[:200] + ed_vectors[:200]
+    schemes = [v.get("scheme", 4) for v in vs] + [1, 5]
+    keys = [v["pub"] for v in vs] + [b"k", b"k"]
+    sigs = [v["sig"] for v in vs] + [b"s", b"s"]
+    msgs = [v["msg"] for v in vs] + [b"m", b"m"]
+    st, _ = engine.verify_batch(schemes, keys, sigs, msgs)
+    assert [int(x) for x in st] == [v["status"] for v in vs] + [4, 4]
+
+
+def _corpus(n, seed):
+    import bc_ecdsa as ec
+    rng = random.Random(seed)
+    rows = []
+    for i in range(n):
+        scheme = 2 if i % 2 == 0 else 3
+        c = ec.CURVES[scheme]
+        d = rng.randrange(1, c.n)
+        pub = ec.keypair(scheme, d)
+        if i % 7 == 0:
+            pub = ec.compress(pub)
+        m = hashlib.sha256(b"tx%d-%d" % (seed, i)).digest()
+        r, s = ec.sign(scheme, d, m, rng.randrange(1, c.n))
+        if i % 3 == 0:
+            s = c.n - s  # high-S: still valid
+        sig = ec.der_encode(r, s)
+        if i % 11 == 0:
+            b = bytearray(sig)
+            b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+            sig = bytes(b)
+        rows.append((scheme, pub, sig, m))
+    return rows
+
+
+def test_random_vs_c_oracle(engine, oracle):
+    rows = _corpus(600, 5)
+    st, _ = engine.verify_batch(*zip(*rows))
+    for (scheme, pub, sig, m), got in zip(rows, st):
+        assert got == oracle.oracle_ecdsa_verify(scheme, pub, len(pub), sig, len(sig), m, len(m))
+    assert (st == 0).sum() > 450
+
+
+def test_device_path(engine, oracle):
+    torch = pytest.importorskip("torch")
+    rows = _corpus(512, 6)
+    n = len(rows)
+    keys = np.zeros((n, 65), np.uint8)
+    sigs = np.zeros((n, 72), np.uint8)
+    kl = np.zeros(n, np.uint8)
+    sl = np.zeros(n, np.uint8)
+    for i, (_, p, s, _) in enumerate(rows):
+        keys[i, :len(p)] = np.frombuffer(p, np.uint8)
+        kl[i] = len(p)
+        sigs[i, :len(s)] = np.frombuffer(s, np.uint8)
+        sl[i] = len(s)
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    sch = t(np.array([r[0] for r in rows], np.uint8))
+    msgs = t(np.frombuffer(b"".join(r[3] for r in rows), np.uint8).reshape(n, 32))
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    verdict = torch.empty(n // 64, dtype=torch.int64, device=dev)
+    engine.ecdsa_verify_device(sch, t(keys), t(kl), t(sigs), t(sl), msgs, status, verdict)
+    torch.cuda.synchronize()
+    got = status.cpu().numpy()
+    want = [oracle.oracle_ecdsa_verify(r[0], r[1], len(r[1]), r[2], len(r[2]), r[3], 32) for r in rows]
+    assert list(got) == want
+    v = verdict.cpu().numpy().view(np.uint64)
+    for i in range(n):
+        assert ((int(v[i // 64]) >> (i % 64)) & 1) == (want[i] == 0)
