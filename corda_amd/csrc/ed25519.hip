@@ -14,6 +14,7 @@
 // once per context), finally encode(R') == R byte-for-byte.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "fe25519.hpp"
 #include "ge25519.hpp"
@@ -45,11 +46,31 @@ CDEV void ge_base(ge_p3& b) {
   fe_set(b.Z, 1);
 }
 
+// B' = [2^128]B (second fixed base of the half-size-scalar ladder)
+CDEV void ge_base128(ge_p3& b) {
+  const uint32_t bx[10] = {0xb7e824, 0x11eb98, 0x7cbf90, 0x4e1739, 0x2639a17,
+                           0x14e29a0, 0x29cc270, 0x6592a5, 0x3f3c45f, 0x1309ebf};
+  const uint32_t by[10] = {0x3f5a66b, 0xaf4452, 0x93cb77, 0xf28d26, 0x24342f8,
+                           0xc29c3a, 0x8f5b13, 0x10fb2be, 0x26526dc, 0x17cb267};
+  const uint32_t bt[10] = {0x2f1338a, 0x1cc7251, 0x1b53d3c, 0x13331d, 0x51e192,
+                           0x1924b6a, 0xab0003, 0x5fa9c, 0x3d0bf46, 0x168593};
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    b.X.v[i] = bx[i];
+    b.Y.v[i] = by[i];
+    b.T.v[i] = bt[i];
+  }
+  fe_set(b.Z, 1);
+}
+
+// tab: entries [0, 129) = [k]B, entries [129, 258) = [k]B'
 __global__ void __launch_bounds__(64) ed25519_btable_kernel(uint32_t* __restrict__ tab) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= kBTableEntries) return;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 2 * kBTableEntries) return;
+  const int k = g % kBTableEntries;
   ge_p3 B, P;
-  ge_base(B);
+  if (g < kBTableEntries) ge_base(B);
+  else ge_base128(B);
   ge_cached bc;
   ge_to_cached(bc, B);
   ge_identity(P);
@@ -68,7 +89,7 @@ __global__ void __launch_bounds__(64) ed25519_btable_kernel(uint32_t* __restrict
   fe_sub(n.ymx, y, x);
   fe_mul(t, x, y);
   fe_mul(n.xy2d, t, d2);
-  uint32_t* o = tab + k * kBEntryWords;
+  uint32_t* o = tab + g * kBEntryWords;
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     o[i] = n.ypx.v[i];
@@ -263,31 +284,336 @@ CDEV uint8_t ed25519_verify_lane(const uint32_t key[8], const uint32_t sig[16], 
   return diff == 0 ? kStatusOk : kStatusBadSig;
 }
 
+// ---------------------------------------------------------------------------
+// Half-size scalars (the default path). With R decoded strictly,
+//   encode([S]B - [h]A) == R_bytes  <=>  P := [S]B - [h]A - R == O.
+// For any (c0, c1) with c0 == c1*h (mod 8L) and c1 odd, c1 != 0 (mod L):
+//   [c1]P == [c1*S mod L]B - [c0]A - [c1]R,   and   [c1]P == O <=> P == O
+// (A, R may carry torsion: every point's order divides 8L, so the mod-8L
+// congruence makes [c0]A == [c1 h]A exact; c1 odd kills no 2-power torsion;
+// c1 != 0 mod L keeps the prime-order part). Extended Euclid on (8L, h),
+// stopped below sqrt(8L), gives |c0|, |c1| ~ 2^128: the ladder needs ~128
+// doublings instead of ~252 (idea: T. Pornin, ePrint 2020/454). The
+// equivalence is checked on the golden catalogue in tools/proto/half_scalar.py.
+CDEV bool mp8_ge(const uint32_t a[8], const uint32_t b[8]) {
+  bool gt = false, eq = true;
+#pragma unroll
+  for (int i = 7; i >= 0; i--) {
+    gt = gt || (eq && a[i] > b[i]);
+    eq = eq && (a[i] == b[i]);
+  }
+  return gt || eq;
+}
+CDEV void mp8_sub(uint32_t a[8], const uint32_t b[8]) {
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t d = (uint64_t)a[i] - b[i] - br;
+    a[i] = (uint32_t)d;
+    br = (d >> 63) & 1;
+  }
+}
+CDEV void mp8_add(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c += (uint64_t)a[i] + b[i];
+    r[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+CDEV uint32_t mp8_shl1(uint32_t r[8], const uint32_t a[8]) {
+  const uint32_t out = a[7] >> 31;
+#pragma unroll
+  for (int i = 7; i > 0; i--) r[i] = (a[i] << 1) | (a[i - 1] >> 31);
+  r[0] = a[0] << 1;
+  return out;
+}
+CDEV void mp8_shr1(uint32_t a[8], bool arith) {
+  const uint32_t top = arith ? (a[7] & 0x80000000u) : 0u;
+#pragma unroll
+  for (int i = 0; i < 7; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 31);
+  a[7] = (a[7] >> 1) | top;
+}
+CDEV void mp8_neg(uint32_t a[8]) {
+  uint64_t c = 1;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c += (uint64_t)(~a[i]);
+    a[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+CDEV int mp8_bitlen(const uint32_t a[8]) {
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) n = a[i] ? 32 * i + 32 - __builtin_clz(a[i]) : n;
+  return n;
+}
+CDEV void mp8_copy(uint32_t d[8], const uint32_t s[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = s[i];
+}
+// |a| of a two's-complement value and its sign
+CDEV int mp8_absbits(const uint32_t a[8]) {
+  uint32_t t[8];
+  mp8_copy(t, a);
+  if (a[7] >> 31) mp8_neg(t);
+  return mp8_bitlen(t);
+}
+
+// rp <- rp mod rc,  tp <- tp - (rp div rc) * tc   (bit-serial long division;
+// Euclid's partial quotients are small: ~1.7 quotient bits per step)
+CDEV void euclid_divstep(uint32_t rp[8], const uint32_t rc[8], uint32_t tp[8], const uint32_t tc[8]) {
+  uint32_t T[8], Tt[8];
+  mp8_copy(T, rc);
+  mp8_copy(Tt, tc);
+  int k = 0;
+  while (true) {
+    uint32_t T2[8];
+    const uint32_t c = mp8_shl1(T2, T);
+    if (c || !mp8_ge(rp, T2)) break;
+    mp8_copy(T, T2);
+    mp8_shl1(Tt, Tt);
+    k++;
+  }
+  for (; k >= 0; k--) {
+    if (mp8_ge(rp, T)) {
+      mp8_sub(rp, T);
+      mp8_sub(tp, Tt);
+    }
+    mp8_shr1(T, false);
+    mp8_shr1(Tt, true);
+  }
+}
+
+// (c0, c1): c0 == c1*h (mod 8L), c1 odd and positive; returns |c0| and its sign
+CDEV void half_scalars(uint32_t c0abs[8], bool& c0neg, uint32_t c1[8], const uint32_t h[8]) {
+  const uint32_t kM[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0u, 0u, 0u, 0x80000000u};  // 8L
+  const uint32_t kS[8] = {0x754abea0u, 0x597d89b3u, 0xf9de6484u, 0xb504f333u, 0u, 0u, 0u, 0u};        // isqrt(8L)+1
+  uint32_t rp[8], rc[8], tp[8], tc[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    rp[i] = kM[i];
+    rc[i] = h[i];
+    tp[i] = 0;
+    tc[i] = i == 0;
+  }
+  while (mp8_ge(rc, kS)) {
+    euclid_divstep(rp, rc, tp, tc);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t a = rp[i], b = tp[i];
+      rp[i] = rc[i];
+      rc[i] = a;
+      tp[i] = tc[i];
+      tc[i] = b;
+    }
+  }
+  uint32_t a0[8], a1[8];  // chosen (c0, c1), two's complement
+  mp8_copy(a0, rc);
+  mp8_copy(a1, tc);
+  if (!(tc[0] & 1)) {
+    // v1 = (rc, tc) has even c1; v3 = next Euclid vector has odd c1, and so do v1 +- v3
+    uint32_t r3[8], t3[8];
+    mp8_copy(r3, rp);
+    mp8_copy(t3, tp);
+    euclid_divstep(r3, rc, t3, tc);
+    uint32_t p0[8], p1[8], m0[8], m1[8], nr3[8], nt3[8];
+    mp8_add(p0, rc, r3);
+    mp8_add(p1, tc, t3);
+    mp8_copy(nr3, r3);
+    mp8_neg(nr3);
+    mp8_copy(nt3, t3);
+    mp8_neg(nt3);
+    mp8_add(m0, rc, nr3);
+    mp8_add(m1, tc, nt3);
+    int best = max(mp8_absbits(r3), mp8_absbits(t3));
+    mp8_copy(a0, r3);
+    mp8_copy(a1, t3);
+    const int bp = max(mp8_absbits(p0), mp8_absbits(p1));
+    if (bp < best) {
+      best = bp;
+      mp8_copy(a0, p0);
+      mp8_copy(a1, p1);
+    }
+    const int bm = max(mp8_absbits(m0), mp8_absbits(m1));
+    if (bm < best) {
+      mp8_copy(a0, m0);
+      mp8_copy(a1, m1);
+    }
+  }
+  if (a1[7] >> 31) {  // make c1 positive: (c0, c1) -> (-c0, -c1)
+    mp8_neg(a0);
+    mp8_neg(a1);
+  }
+  c0neg = (a0[7] >> 31) != 0;
+  if (c0neg) mp8_neg(a0);
+  mp8_copy(c0abs, a0);
+  mp8_copy(c1, a1);
+}
+
+// Strict R decode: the reference never decodes R, it compares encode(R')
+// with the 32 bytes; those equal only when the bytes are the canonical
+// encoding of a curve point: y < p, on the curve, not (x == 0 with bit 255).
+CDEV bool ge_frombytes_strict(ge_p3& R, const uint32_t w[8]) {
+  bool all_ones = (w[7] & 0x7fffffffu) == 0x7fffffffu;
+#pragma unroll
+  for (int i = 1; i < 7; i++) all_ones = all_ones && (w[i] == 0xffffffffu);
+  if (all_ones && w[0] >= 0xffffffedu) return false;  // y >= p
+  if (!ge_frombytes_i2p(R, w)) return false;
+  if ((w[7] >> 31) && fe_iszero(R.X)) return false;
+  return true;
+}
+
+CDEV void cached_table9(ge_cached tab[9], const ge_p3& base) {
+  fe_set(tab[0].YpX, 1);
+  fe_set(tab[0].YmX, 1);
+  fe_set(tab[0].Z, 1);
+  fe_set(tab[0].T2d, 0);
+  ge_to_cached(tab[1], base);
+  ge_p3 Q;
+  ge_dbl<true>(Q, base);
+  ge_to_cached(tab[2], Q);
+  for (int k = 3; k <= 8; k++) {
+    ge_add<true>(Q, Q, tab[1]);
+    ge_to_cached(tab[k], Q);
+  }
+}
+
+CDEV void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8], const uint32_t c[8]);
+
+// [ka]Abase + [kr]Rbase + [e]B, ka, kr < 2^(4W-1), e < L; W wave-uniform
+CDEV void straus_half(ge_p3& P, const ge_p3& Abase, const ge_p3& Rbase, const uint32_t ka[8], const uint32_t kr[8],
+                      const uint32_t e[8], int W, const uint32_t* __restrict__ btab) {
+  ge_cached ta[9], tr[9];
+  cached_table9(ta, Abase);
+  cached_table9(tr, Rbase);
+  const uint32_t* btab128 = btab + kBTableEntries * kBEntryWords;
+  ge_identity(P);
+  for (int j = W - 1; j >= 0; j--) {
+    if (j != W - 1) {
+      ge_dbl<false>(P, P);
+      ge_dbl<false>(P, P);
+      ge_dbl<false>(P, P);
+      ge_dbl<true>(P, P);
+    }
+    const int da = booth_digit<4>(ka, j);
+    ge_cached ca = ta[da < 0 ? -da : da];
+    cached_cneg(ca, da < 0);
+    ge_add<true>(P, P, ca);
+    const int dr = booth_digit<4>(kr, j);
+    ge_cached cr = tr[dr < 0 ? -dr : dr];
+    cached_cneg(cr, dr < 0);
+    if ((j & 1) == 0 && j < 32) {
+      ge_add<true>(P, P, cr);
+      const int d0 = booth_digit<8>(e, j >> 1), d1 = booth_digit<8>(e, (j >> 1) + 16);
+      ge_niels nb;
+      load_niels(nb, btab, d0 < 0 ? -d0 : d0);
+      niels_cneg(nb, d0 < 0);
+      ge_madd<true>(P, P, nb);
+      load_niels(nb, btab128, d1 < 0 ? -d1 : d1);
+      niels_cneg(nb, d1 < 0);
+      ge_madd<false>(P, P, nb);
+    } else {
+      ge_add<false>(P, P, cr);
+    }
+  }
+}
+
+CDEV int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+CDEV uint8_t ed25519_verify_lane_half(const uint32_t key[8], const uint32_t sig[16], const uint8_t* __restrict__ msg,
+                                      uint32_t msg_len, const uint32_t* __restrict__ btab, uint8_t pre_status,
+                                      bool active) {
+  // every lane of the wave reaches the wave-uniform ladder; inactive or
+  // already-decided lanes run it on dummy scalars and keep their status
+  uint8_t st = kStatusOk;
+  ge_p3 A, R;
+  if (!active) st = kStatusBadSig;
+  else if (!ge_frombytes_i2p(A, key)) st = kStatusBadKey;
+  else if (pre_status != kStatusOk) st = pre_status;
+  else if (msg_len == 0) st = kStatusEmpty;
+  uint32_t Rw[8], S[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    Rw[i] = sig[i];
+    S[i] = sig[8 + i];
+  }
+  if (st == kStatusOk && !ge_frombytes_strict(R, Rw)) st = kStatusBadSig;
+  uint32_t ka[8], kr[8], e[8];
+  bool c0neg = false;
+  if (st == kStatusOk) {
+    uint32_t abyte[8];
+    fe_tobytes(abyte, A.Y);
+    abyte[7] |= fe_isnegative(A.X) << 31;
+    uint32_t hd[16], h[8], se[8], zero[8];
+    sha512_segments(hd, Rw, abyte, true, msg, msg_len);
+    sc_reduce512(h, hd);
+    const bool dropped = slide_drops_carry(S);
+    sc_effective_S(se, S, dropped);
+    half_scalars(ka, c0neg, kr, h);
+#pragma unroll
+    for (int i = 0; i < 8; i++) zero[i] = 0;
+    sc_muladd(e, kr, se, zero);  // e = c1 S_eff mod L
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++) ka[i] = kr[i] = e[i] = 0;
+    ge_identity(A);
+    ge_identity(R);
+  }
+  const int bits = max(mp8_bitlen(ka), mp8_bitlen(kr));
+  const int W = wave_max((bits + 1 + 3) / 4);
+  // [e]B + [c0](-A) + [c1](-R): -A when c0 > 0, A when c0 < 0; always -R
+  ge_p3 Ab = A, Rb = R;
+  if (!c0neg) {
+    fe_neg(Ab.X, A.X);
+    fe_neg(Ab.T, A.T);
+  }
+  fe_neg(Rb.X, R.X);
+  fe_neg(Rb.T, R.T);
+  ge_p3 P;
+  straus_half(P, Ab, Rb, ka, kr, e, W > 0 ? W : 1, btab);
+  if (st != kStatusOk) return st;
+  fe d;
+  fe_sub(d, P.Y, P.Z);
+  return (fe_iszero(P.X) && fe_iszero(d)) ? kStatusOk : kStatusBadSig;
+}
+
 // keys n*32 B, sigs n*64 B, msgs n*msg_len B (16-B aligned rows when msg_len == 32)
+template <bool HALF>
 __global__ void __launch_bounds__(256) ed25519_verify_kernel(
     const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
     uint32_t msg_len, uint64_t n, const uint32_t* __restrict__ btab, const uint8_t* __restrict__ pre_status,
     uint8_t* __restrict__ status, unsigned long long* __restrict__ verdict) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t st = kStatusBadSig;
-  if (i < n) {
-    const uint4* k4 = reinterpret_cast<const uint4*>(keys + i * 32);
-    const uint4* s4 = reinterpret_cast<const uint4*>(sigs + i * 64);
-    const uint4 ka = k4[0], kb = k4[1];
-    const uint32_t key[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
-    uint32_t sig[16];
+  const bool active = i < n;
+  const uint64_t ii = active ? i : 0;  // inactive lanes read lane 0's row (n > 0), discard it
+  const uint4* k4 = reinterpret_cast<const uint4*>(keys + ii * 32);
+  const uint4* s4 = reinterpret_cast<const uint4*>(sigs + ii * 64);
+  const uint4 ka = k4[0], kb = k4[1];
+  const uint32_t key[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+  uint32_t sig[16];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const uint4 v = s4[q];
-      sig[4 * q] = v.x;
-      sig[4 * q + 1] = v.y;
-      sig[4 * q + 2] = v.z;
-      sig[4 * q + 3] = v.w;
-    }
-    st = ed25519_verify_lane(key, sig, msgs + i * (uint64_t)msg_len, msg_len, btab,
-                             pre_status ? pre_status[i] : kStatusOk);
-    status[i] = st;
+  for (int q = 0; q < 4; q++) {
+    const uint4 v = s4[q];
+    sig[4 * q] = v.x;
+    sig[4 * q + 1] = v.y;
+    sig[4 * q + 2] = v.z;
+    sig[4 * q + 3] = v.w;
   }
+  const uint8_t pre = (pre_status && active) ? pre_status[ii] : kStatusOk;
+  if (HALF) {
+    st = ed25519_verify_lane_half(key, sig, msgs + ii * (uint64_t)msg_len, msg_len, btab, pre, active);
+  } else if (active) {
+    st = ed25519_verify_lane(key, sig, msgs + ii * (uint64_t)msg_len, msg_len, btab, pre);
+  }
+  if (active) status[i] = st;
   const unsigned long long ok = __ballot(i < n && st == kStatusOk);
   if ((threadIdx.x & 63) == 0 && i < n && verdict) verdict[i >> 6] = ok;
 }
@@ -401,18 +727,32 @@ __global__ void __launch_bounds__(256) ed25519_sign_kernel(const uint8_t* __rest
 // host-side launchers (called by cordahip.cpp)
 namespace cordahip {
 hipError_t launch_ed25519_btable(uint32_t* tab, hipStream_t s) {
-  hipLaunchKernelGGL(ed25519_btable_kernel, dim3((kBTableEntries + 63) / 64), dim3(64), 0, s, tab);
+  hipLaunchKernelGGL(ed25519_btable_kernel, dim3((2 * kBTableEntries + 63) / 64), dim3(64), 0, s, tab);
   return hipGetLastError();
 }
-size_t ed25519_btable_bytes() { return (size_t)kBTableEntries * kBEntryWords * sizeof(uint32_t); }
+size_t ed25519_btable_bytes() { return 2 * (size_t)kBTableEntries * kBEntryWords * sizeof(uint32_t); }
+
+// CORDAHIP_ED25519_LADDER=full selects the full-length (252-doubling) ladder
+// instead of the half-size-scalar one; both are bit-exact, kept for A/B runs.
+static bool use_half_ladder() {
+  static const bool half = [] {
+    const char* v = getenv("CORDAHIP_ED25519_LADDER");
+    return !(v && v[0] == 'f');
+  }();
+  return half;
+}
 
 hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
                                  uint64_t n, const uint32_t* btab, const uint8_t* pre_status, uint8_t* status,
                                  unsigned long long* verdict, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint64_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(ed25519_verify_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, keys, sigs, msgs, msg_len, n,
-                     btab, pre_status, status, verdict);
+  if (use_half_ladder())
+    hipLaunchKernelGGL(ed25519_verify_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0, s, keys, sigs, msgs,
+                       msg_len, n, btab, pre_status, status, verdict);
+  else
+    hipLaunchKernelGGL(ed25519_verify_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, s, keys, sigs, msgs,
+                       msg_len, n, btab, pre_status, status, verdict);
   return hipGetLastError();
 }
 
