@@ -1,15 +1,21 @@
 #!/usr/bin/env python3
 """bench.py — headline benchmark of the MI355X Corda verification engine.
 
-Workload (BASELINE.json configs[1], "C2"): one step = one pass of the hot path
-(`Crypto.isValid(EDDSA_ED25519_SHA512, ...)` over a batch, kernel K1) over a
-batch of 2^24 Ed25519 (key, sig, 32-byte txId) tuples resident in HBM, 1% of
-them corrupted / non-canonical with SURVEY.md §8(d)'s fixed catalogue, plus
-the RCCL all-gather of the per-GPU verdict bitmasks when N > 1.
+Default workload (BASELINE.json configs[1], "C2"): one step = one pass of the
+hot path (`Crypto.isValid(EDDSA_ED25519_SHA512, ...)` over a batch, kernel K1)
+over 2^24 Ed25519 (key, sig, 32-byte txId) tuples resident in HBM, 1% of them
+corrupted / non-canonical with SURVEY.md §8(d)'s fixed catalogue, plus the
+RCCL all-gather of the per-GPU verdict bitmasks when N > 1.
+
+Other workloads (`--workload`), same contract, used for profiling the other rows:
+  c3  mixed secp256k1 / P-256 ECDSA, 2^24 per GPU, 1% corrupted (kernel K2)
+  c4  SignedTransaction.verifySignatures over synthetic cash-issue transactions
+      (5 leaves, 1-3 Ed25519 signers): leaf SHA-256 + Merkle id + signatures
+      + per-tx reduce (K3/K4/K1/K5); 10^7 / 8 txs per GPU by default.
 
 Contract: `python bench.py --gpus N --steps K --warmup W` (N > 1 under
 torch.distributed.run, one rank per GPU); rank 0 prints ONE JSON line.
-Weak scaling: every rank verifies its own 2^24 batch; value = all ranks'
+Weak scaling: every rank verifies its own batch; value = all ranks'
 verifications / max-over-ranks wall time of the K timed steps.
 """
 from __future__ import annotations
@@ -24,39 +30,251 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "signature verifications/sec (whole node, 1/2/4/8 GPU) + % integer-ALU peak"
-# algorithmic work per Ed25519 verification, in limb-MACs
+# algorithmic work per verification, in limb-MACs
 # (32x32->64 multiply-accumulates of schoolbook radix-2^32: 64 per field mul).
-LIMB_MACS_PER_ED25519 = 198_000
+LIMB_MACS = {"ed25519": 198_000, "p256": 211_000, "secp256k1": 192_000}
 # Integer-ALU peak: 256 CUs x 64 v_mad_u64_u32 lane-ops per CU-cycle x 2.4 GHz
 # (per-CU rate measured: profiles/r01_int_rates.jsonl, 59-62 lane-ops/CU-cycle).
 INT_MAC_PEAK_T = 256 * 64 * 2.4e9 / 1e12
+C4_LEAF_LENS = (450, 150, 140, 43, 55)  # SURVEY §8(d) C4 synthetic cash-issue component lengths
 
 
-def cpu_baseline(pubs, sigs, msgs, sample: int):
-    """Oracle (oracle/c, a C port of the i2p 0.2.0 path) on the box's host cores."""
-    import ctypes
-    import numpy as np
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from conftest import load_oracle  # oracle loader lives with the tests (checker only)
+    return load_oracle()
 
-    orc = load_oracle()
-    k = pubs[:sample].cpu().numpy().copy()
-    s = sigs[:sample].cpu().numpy().copy()
-    m = msgs[:sample].cpu().numpy().copy()
-    out = np.zeros(sample, np.uint8)
-    cores = max(1, min(16, os.cpu_count() or 1))
-    t0 = time.perf_counter()
-    orc.oracle_ed25519_verify_batch(sample, k.ctypes.data, s.ctypes.data, m.ctypes.data, 32, out.ctypes.data, cores)
-    dt = time.perf_counter() - t0
-    one = min(sample, 4096)
-    out1 = np.zeros(one, np.uint8)
-    t1 = time.perf_counter()
-    orc.oracle_ed25519_verify_batch(one, k.ctypes.data, s.ctypes.data, m.ctypes.data, 32, out1.ctypes.data, 1)
-    dt1 = time.perf_counter() - t1
-    return {"value": sample / dt, "unit": "verifications/s", "cores": cores, "kind": "port",
-            "sample": "first %d tuples of the rank-0 C2 batch (same corpus, 1%% corrupted), %d threads; "
-                      "single-thread rate on %d tuples: %.0f/s" % (sample, cores, one, one / dt1),
-            "single_thread_value": one / dt1, "wall_s": dt}, out
+
+def _cores():
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+# ---- C2: Ed25519 ---------------------------------------------------------------
+class C2:
+    kernel = "ed25519_verify_kernel"
+    pmc = "r01_pmc_ed25519_verify.json"
+
+    def __init__(self, eng, device, stream, rank, args):
+        import torch
+        from corda_amd.corpus import make_c2_corpus
+        self.torch, self.eng, self.device, self.stream = torch, eng, device, stream
+        self.n = n = 1 << args.batch_log2
+        self.pubs, self.sigs, self.msgs, self.expected, _ = make_c2_corpus(eng, n, 0xC0DA0002 + rank, device,
+                                                                           stream=stream)
+        self.status = torch.empty(n, dtype=torch.uint8, device=device)
+        self.verdict = torch.empty((n + 63) // 64, dtype=torch.int64, device=device)
+        self.units = n
+        self.macs = LIMB_MACS["ed25519"]
+        self.workload = ("C2: Ed25519 batch of 2^%d sigs per GPU, 32-byte txIds, 1%% corrupted/non-canonical"
+                         % args.batch_log2)
+        self.data = ("synthetic: seeded RFC 8032 tuples signed on the GPU (cordahip_ed25519_sign_device), "
+                     "1% corrupted per SURVEY §8(d) C2")
+        self.config = {"batch_per_gpu": n, "msg_len": 32, "corrupt_frac": 0.01}
+
+    def step(self):
+        self.eng.ed25519_verify_device(self.pubs, self.sigs, self.msgs, self.status, self.verdict, device=0,
+                                       stream=self.stream)
+
+    def check(self):
+        # vs the corpus construction (slide-dependent lanes excluded; full bit-exact
+        # parity vs the oracle is tests/test_gpu_ed25519.py's job and the sample below)
+        known = self.expected >= 0
+        return {"mismatches_vs_construction": int((self.status[known].to(self.torch.int16)
+                                                   != self.expected[known]).sum()),
+                "accepted": int((self.status == 0).sum()), "corrupted": int((self.expected != 0).sum())}
+
+    def cpu_baseline(self, sample):
+        import numpy as np
+        orc = _oracle()
+        k = self.pubs[:sample].cpu().numpy().copy()
+        s = self.sigs[:sample].cpu().numpy().copy()
+        m = self.msgs[:sample].cpu().numpy().copy()
+        out = np.zeros(sample, np.uint8)
+        cores = _cores()
+        t0 = time.perf_counter()
+        orc.oracle_ed25519_verify_batch(sample, k.ctypes.data, s.ctypes.data, m.ctypes.data, 32, out.ctypes.data,
+                                        cores)
+        dt = time.perf_counter() - t0
+        one = min(sample, 4096)
+        out1 = np.zeros(one, np.uint8)
+        t1 = time.perf_counter()
+        orc.oracle_ed25519_verify_batch(one, k.ctypes.data, s.ctypes.data, m.ctypes.data, 32, out1.ctypes.data, 1)
+        dt1 = time.perf_counter() - t1
+        mism = int((out != self.status[:sample].cpu().numpy()).sum())
+        return {"value": sample / dt, "unit": "verifications/s", "cores": cores, "kind": "port",
+                "sample": "first %d tuples of the rank-0 C2 batch (same corpus, 1%% corrupted), %d threads; "
+                          "single-thread rate on %d tuples: %.0f/s" % (sample, cores, one, one / dt1),
+                "single_thread_value": one / dt1, "wall_s": dt, "gpu_vs_port_mismatches_on_sample": mism}
+
+
+# ---- C3: mixed secp256k1 / P-256 ECDSA ----------------------------------------
+class C3:
+    kernel = "ecdsa_verify_kernel"
+    pmc = "r01_pmc_ecdsa_verify.json"
+
+    def __init__(self, eng, device, stream, rank, args):
+        import torch
+        from corda_amd.corpus import make_c3_corpus
+        self.torch, self.eng, self.device, self.stream = torch, eng, device, stream
+        self.n = n = 1 << args.batch_log2
+        (self.scheme, self.keys, self.key_len, self.sigs, self.sig_len, self.msgs, self.expected,
+         self.cats) = make_c3_corpus(eng, n, 0xC0DA0003 + rank, device, stream=stream)
+        self.status = torch.empty(n, dtype=torch.uint8, device=device)
+        self.verdict = torch.empty((n + 63) // 64, dtype=torch.int64, device=device)
+        self.units = n
+        self.macs = (LIMB_MACS["p256"] + LIMB_MACS["secp256k1"]) // 2
+        self.workload = ("C3: mixed ECDSA_SECP256K1_SHA256 / ECDSA_SECP256R1_SHA256 (interleaved 50/50) batch of "
+                         "2^%d sigs per GPU, 32-byte txIds, 1%% corrupted, ~10%% compressed keys, ~50%% high-S"
+                         % args.batch_log2)
+        self.data = ("synthetic: seeded keys/sigs made on the GPU (cordahip_ecdsa_sign_device), 1% corrupted per "
+                     "SURVEY §8(d) C3 (DER malformations, r/s = 0, r/s >= n, bit flips, off-curve keys)")
+        self.config = {"batch_per_gpu": n, "msg_len": 32, "corrupt_frac": 0.01}
+
+    def step(self):
+        self.eng.ecdsa_verify_device(self.scheme, self.keys, self.key_len, self.sigs, self.sig_len, self.msgs,
+                                     self.status, self.verdict, device=0, stream=self.stream)
+
+    def check(self):
+        from corda_amd.corpus import REJECT_ANY
+        st = self.status.to(self.torch.int16)
+        exact = self.expected >= 0
+        anyrej = self.expected == REJECT_ANY
+        return {"mismatches_vs_construction": int((st[exact] != self.expected[exact]).sum())
+                + int((st[anyrej] == 0).sum()),
+                "accepted": int((self.status == 0).sum()), "corrupted": int((self.expected != 0).sum()),
+                "compressed_valid": int(self.cats["compressed_valid"].numel())}
+
+    def cpu_baseline(self, sample):
+        import numpy as np
+        orc = _oracle()
+        sc = self.scheme[:sample].cpu().numpy().copy()
+        kl = self.key_len[:sample].cpu().numpy().astype(np.uint64)
+        sl = self.sig_len[:sample].cpu().numpy().astype(np.uint64)
+        # CSR views over the fixed slots: offsets point at each slot, lengths from key_len / sig_len
+        K = self.keys[:sample].cpu().numpy().copy()
+        S = self.sigs[:sample].cpu().numpy().copy()
+        M = self.msgs[:sample].cpu().numpy().copy()
+        kb = np.ascontiguousarray(np.concatenate([K[i, :kl[i]] for i in range(sample)]))
+        sb = np.ascontiguousarray(np.concatenate([S[i, :sl[i]] for i in range(sample)]))
+        ko = np.zeros(sample + 1, np.uint64)
+        so = np.zeros(sample + 1, np.uint64)
+        ko[1:] = np.cumsum(kl)
+        so[1:] = np.cumsum(sl)
+        mo = (np.arange(sample + 1, dtype=np.uint64) * 32)
+        out = np.zeros(sample, np.uint8)
+        cores = _cores()
+        t0 = time.perf_counter()
+        orc.oracle_ecdsa_verify_batch(sample, sc.ctypes.data, kb.ctypes.data, ko.ctypes.data, sb.ctypes.data,
+                                      so.ctypes.data, M.ctypes.data, mo.ctypes.data, out.ctypes.data, cores)
+        dt = time.perf_counter() - t0
+        mism = int((out != self.status[:sample].cpu().numpy()).sum())
+        return {"value": sample / dt, "unit": "verifications/s", "cores": cores, "kind": "port",
+                "sample": "first %d tuples of the rank-0 C3 batch (BouncyCastle-1.57 restatement in C, "
+                          "%d threads)" % (sample, cores),
+                "wall_s": dt, "gpu_vs_port_mismatches_on_sample": mism}
+
+
+# ---- C4: SignedTransaction.verifySignatures on cash-issue transactions --------
+class C4:
+    kernel = "ed25519_verify_kernel"
+    pmc = "r01_pmc_ed25519_verify.json"
+
+    def __init__(self, eng, device, stream, rank, args):
+        import torch
+        self.torch, self.eng, self.device, self.stream = torch, eng, device, stream
+        ntx = args.c4_txs
+        g = torch.Generator(device=device)
+        g.manual_seed(0xC0DA0004 + rank)
+        nl = len(C4_LEAF_LENS)
+        per_tx = sum(C4_LEAF_LENS)
+        self.leaf_bytes = torch.randint(0, 256, (ntx * per_tx,), dtype=torch.uint8, device=device, generator=g)
+        lens = torch.tensor(C4_LEAF_LENS, dtype=torch.int64, device=device).repeat(ntx)
+        self.leaf_off = torch.zeros(ntx * nl + 1, dtype=torch.int64, device=device)
+        self.leaf_off[1:] = torch.cumsum(lens, 0)
+        self.tx_leaf_off = torch.arange(ntx + 1, dtype=torch.int64, device=device) * nl
+        nsig = torch.randint(1, 4, (ntx,), dtype=torch.int64, device=device, generator=g)
+        self.tx_sig_off = torch.zeros(ntx + 1, dtype=torch.int64, device=device)
+        self.tx_sig_off[1:] = torch.cumsum(nsig, 0)
+        ns = int(self.tx_sig_off[-1])
+        self.keys = torch.zeros((ns, 32), dtype=torch.uint8, device=device)
+        self.sigs = torch.zeros((ns, 64), dtype=torch.uint8, device=device)
+        self.txid = torch.empty((ntx, 32), dtype=torch.uint8, device=device)
+        self.tx_status = torch.empty(ntx, dtype=torch.uint8, device=device)
+        self.first_bad = torch.empty(ntx, dtype=torch.int64, device=device)
+        self.sig_status = torch.empty(ns, dtype=torch.uint8, device=device)
+        self.step()  # computes the ids (signatures still blank)
+        torch.cuda.synchronize(device)
+        tx_of_sig = torch.repeat_interleave(torch.arange(ntx, device=device), nsig)
+        seeds = torch.randint(0, 256, (ns, 32), dtype=torch.uint8, device=device, generator=g)
+        msgs = self.txid[tx_of_sig].contiguous()
+        eng.ed25519_sign_device(seeds, msgs, self.keys, self.sigs, stream=stream)
+        torch.cuda.synchronize(device)
+        del seeds, msgs
+        # 0.5% of signatures: one bit of R flipped; 0.5% of transactions: one leaf byte flipped
+        self.exp_status = torch.zeros(ntx, dtype=torch.uint8, device=device)
+        self.exp_bad = torch.full((ntx,), -1, dtype=torch.int64, device=device)
+        bad_sig = torch.randperm(ns, device=device, generator=g)[:max(1, ns // 200)]
+        bit = torch.randint(0, 256, (bad_sig.numel(),), device=device, generator=g)
+        self.sigs[bad_sig, bit // 8] ^= (1 << (bit % 8)).to(torch.uint8)
+        t_bad = tx_of_sig[bad_sig]
+        idx_in_tx = bad_sig - self.tx_sig_off[t_bad]
+        self.exp_status[t_bad] = 1
+        self.exp_bad.scatter_reduce_(0, t_bad, idx_in_tx, reduce="amin", include_self=False)
+        bad_tx = torch.randperm(ntx, device=device, generator=g)[:max(1, ntx // 200)]
+        pos = self.leaf_off[bad_tx * nl] + torch.randint(0, C4_LEAF_LENS[0], (bad_tx.numel(),), device=device,
+                                                         generator=g)
+        self.leaf_bytes[pos] ^= 1
+        self.exp_status[bad_tx] = 1
+        self.exp_bad[bad_tx] = 0
+        self.ntx, self.ns = ntx, ns
+        self.units = ns
+        self.macs = LIMB_MACS["ed25519"]
+        self.workload = ("C4: SignedTransaction.verifySignatures on %d synthetic cash-issue txs per GPU "
+                         "(5 leaves of %s B, 1-3 Ed25519 signers; leaf SHA-256 + Merkle id + sigs + per-tx reduce)"
+                         % (ntx, list(C4_LEAF_LENS)))
+        self.data = ("synthetic: seeded random leaf bytes (real Kryo bytes not producible here), signatures made "
+                     "on the GPU over the GPU-computed ids; 0.5% sigs and 0.5% txs corrupted")
+        self.config = {"txs_per_gpu": ntx, "sigs_per_gpu": ns, "leaf_lens": list(C4_LEAF_LENS)}
+
+    def step(self):
+        self.eng.signed_tx_verify_ed25519_device(self.leaf_bytes, self.leaf_off, self.tx_leaf_off, self.tx_sig_off,
+                                                 self.keys, self.sigs, self.txid, self.tx_status, self.first_bad,
+                                                 self.sig_status, device=0, stream=self.stream)
+
+    def check(self):
+        return {"mismatches_vs_construction": int((self.tx_status != self.exp_status).sum())
+                + int((self.first_bad != self.exp_bad).sum()),
+                "accepted_txs": int((self.tx_status == 0).sum()), "txs": self.ntx, "sigs": self.ns}
+
+    def cpu_baseline(self, sample):
+        import ctypes
+        import numpy as np
+        orc = _oracle()
+        ntx = max(1, min(self.ntx, sample // 2))
+        lb = self.leaf_bytes[:int(self.leaf_off[ntx * len(C4_LEAF_LENS)])].cpu().numpy().copy()
+        lo = self.leaf_off[:ntx * len(C4_LEAF_LENS) + 1].cpu().numpy().astype(np.uint64)
+        so = self.tx_sig_off[:ntx + 1].cpu().numpy()
+        ns = int(so[-1])
+        K = self.keys[:ns].cpu().numpy().copy()
+        S = self.sigs[:ns].cpu().numpy().copy()
+        ids = np.zeros((ntx, 32), np.uint8)
+        out = np.zeros(ns, np.uint8)
+        cores = _cores()
+        nl = len(C4_LEAF_LENS)
+        t0 = time.perf_counter()
+        for t in range(ntx):
+            orc.oracle_tx_id(lb.ctypes.data, lo[t * nl:].ctypes.data, nl, ctypes.cast(ids[t].ctypes.data, ctypes.c_char_p))
+        M = ids[np.repeat(np.arange(ntx), np.diff(so))]
+        orc.oracle_ed25519_verify_batch(ns, K.ctypes.data, S.ctypes.data, M.ctypes.data, 32, out.ctypes.data, cores)
+        dt = time.perf_counter() - t0
+        mism = int((out != self.sig_status[:ns].cpu().numpy()).sum())
+        return {"value": ns / dt, "unit": "verifications/s", "cores": cores, "kind": "port",
+                "sample": "first %d txs (%d sigs) of the rank-0 C4 batch: tx ids single-threaded, signatures on %d "
+                          "threads" % (ntx, ns, cores),
+                "wall_s": dt, "txs_per_s": ntx / dt, "gpu_vs_port_mismatches_on_sample": mism}
+
+
+WORKLOADS = {"c2": C2, "c3": C3, "c4": C4}
 
 
 def main():
@@ -64,49 +282,47 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--batch-log2", type=int, default=24)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 17)
+    ap.add_argument("--c4-txs", type=int, default=10_000_000 // 8)
+    ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
+    from corda_amd.dist import gather_verdicts, max_over_ranks
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+        dist.init_process_group("nccl", device_id=device)
 
-    from corda_amd.corpus import make_c2_corpus
     from corda_amd.engine import Engine
 
     eng = Engine(1 << local_rank)
-    # one explicit stream carries corpus generation, the kernel and the timing
+    # one explicit stream carries corpus generation, the kernels and the timing
     # events, so the events bracket exactly the launches they time
     stream = torch.cuda.Stream(device)
     torch.cuda.set_stream(stream)
-    n = 1 << args.batch_log2
     t_gen = time.perf_counter()
-    pubs, sigs, msgs, expected, cats = make_c2_corpus(eng, n, 0xC0DA0002 + rank, device, stream=stream)
+    wl = WORKLOADS[args.workload](eng, device, stream, rank, args)
+    torch.cuda.synchronize(device)
     t_gen = time.perf_counter() - t_gen
-    status = torch.empty(n, dtype=torch.uint8, device=device)
-    verdict = torch.empty(n // 64, dtype=torch.int64, device=device)
-    gathered = torch.empty(world * (n // 64), dtype=torch.int64, device=device) if world > 1 else None
+    verdict = getattr(wl, "verdict", None)
 
     def step(ev_s=None, ev_e=None):
         if ev_s is not None:
             ev_s.record(stream)
-        eng.ed25519_verify_device(pubs, sigs, msgs, status, verdict, device=0, stream=stream)
+        wl.step()
         if ev_e is not None:
             ev_e.record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, verdict)
+        if world > 1 and verdict is not None:
+            gather_verdicts(verdict, world)  # the only data-path collective (RCCL all-gather)
 
     for _ in range(args.warmup):
         step()
@@ -124,24 +340,15 @@ def main():
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-
-    # verdict sanity against the corpus construction (slide-dependent lanes excluded;
-    # full bit-exact parity vs the oracle is tests/test_gpu_ed25519.py's job)
-    known = expected >= 0
-    mismatches = int((status[known].to(torch.int16) != expected[known]).sum())
-    accepted = int((status == 0).sum())
-
-    if world > 1:
-        t = torch.tensor([elapsed, float(mismatches)], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
-        mismatches = int(t[1])
+    chk = wl.check()
+    elapsed = max_over_ranks(elapsed, device)
+    chk["mismatches_vs_construction"] = int(max_over_ranks(float(chk["mismatches_vs_construction"]), device))
 
     if rank == 0:
-        value = world * n * args.steps / elapsed
-        achieved = LIMB_MACS_PER_ED25519 * n / (kernel_ms * 1e-3) / 1e12
+        value = world * wl.units * args.steps / elapsed
+        achieved = wl.macs * wl.units / (kernel_ms * 1e-3) / 1e12
         traffic = None
-        pmc_file = os.path.join(ROOT, "profiles", "r01_pmc_ed25519_verify.json")
+        pmc_file = os.path.join(ROOT, "profiles", wl.pmc)
         if os.path.exists(pmc_file):
             with open(pmc_file) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
@@ -157,26 +364,21 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic: seeded RFC 8032 tuples signed on the GPU (cordahip_ed25519_sign_device), "
-                    "1% corrupted per SURVEY §8(d) C2",
-            "config": {"workload": "C2: Ed25519 batch of 2^%d sigs per GPU, 32-byte txIds, 1%% corrupted/non-canonical"
-                                   % args.batch_log2,
-                       "batch_per_gpu": n, "msg_len": 32, "corrupt_frac": 0.01,
-                       "parallelism": "dp%d (independent shards, RCCL all-gather of verdict masks)" % world},
+            "data": wl.data,
+            "config": dict({"workload": wl.workload,
+                            "parallelism": "dp%d (independent shards, RCCL all-gather of verdict masks)" % world},
+                           **wl.config),
             "roofline": {"bound": "valu", "achieved": achieved, "peak": INT_MAC_PEAK_T,
                          "unit": "Tlimb-MAC/s", "frac": achieved / INT_MAC_PEAK_T, "traffic": traffic,
-                         "kernel": "ed25519_verify_kernel", "kernel_ms": kernel_ms,
-                         "work_per_unit": "%d limb-MACs per verification (SURVEY §8d)" % LIMB_MACS_PER_ED25519},
+                         "kernel": wl.kernel, "kernel_ms": kernel_ms,
+                         "work_per_unit": "%d limb-MACs per verification (SURVEY §8d)" % wl.macs},
             "int_alu_peak_frac": achieved / INT_MAC_PEAK_T,
-            "verdict_check": {"mismatches_vs_construction": mismatches, "accepted": accepted,
-                              "corrupted": int((expected != 0).sum())},
+            "verdict_check": chk,
             "corpus_gen_s": t_gen,
         }
         if world == 1 and not args.no_cpu_baseline:
-            cb, cpu_status = cpu_baseline(pubs, sigs, msgs, min(args.cpu_sample, n))
-            cpu_mism = int((torch.from_numpy(cpu_status).to(device) != status[:len(cpu_status)]).sum())
-            cb["gpu_vs_port_mismatches_on_sample"] = cpu_mism
-            out["cpu_baseline"] = cb
+            sample = args.cpu_sample or {"c2": 1 << 17, "c3": 1 << 16, "c4": 1 << 16}[args.workload]
+            out["cpu_baseline"] = wl.cpu_baseline(min(sample, wl.units))
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

@@ -27,7 +27,7 @@ EXPORTS = [
     "cordahip_abi_version", "cordahip_strerror", "cordahip_init", "cordahip_shutdown",
     "cordahip_device_count", "cordahip_alloc_pinned", "cordahip_free_pinned", "cordahip_sig_submit",
     "cordahip_wait", "cordahip_poll", "cordahip_sig_verify", "cordahip_ed25519_verify_device",
-    "cordahip_ed25519_verify_host", "cordahip_ed25519_sign_device", "cordahip_last_kernel_ms",
+    "cordahip_ed25519_verify_host", "cordahip_ed25519_sign_device", "cordahip_ecdsa_sign_device", "cordahip_last_kernel_ms",
     "cordahip_tx_ids", "cordahip_signed_tx_verify", "cordahip_signed_tx_verify_ed25519_device",
     "cordahip_ecdsa_verify_device",
 ]
@@ -118,6 +118,7 @@ def lib() -> ctypes.CDLL:
         "cordahip_signed_tx_verify_ed25519_device": (i32, [vp, i32, vp, vp, u64, vp, u64, vp, vp, vp, u64, vp, vp,
                                                            vp, vp, vp]),
         "cordahip_ecdsa_verify_device": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, u32, u64, vp, vp, vp]),
+        "cordahip_ecdsa_sign_device": (i32, [vp, i32, vp, vp, vp, u32, u64, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(l, name)

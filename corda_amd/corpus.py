@@ -124,3 +124,151 @@ def corrupt_c2(pubs, sigs, msgs, seed: int, g, corrupt_frac: float = 0.01):
         e = C2_EXPECTED[name]
         expected[idx] = -1 if e is None else e
     return expected, cats
+
+
+# ---- C3: mixed secp256k1 / P-256 ECDSA --------------------------------------
+N_K1 = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+N_R1 = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+CURVE_N = {2: N_K1, 3: N_R1}
+REJECT_ANY = -2  # expected "some rejection status" (exact status decided by the oracle in tests)
+
+# C3 mix (fractions of the corrupted lanes), SURVEY §8(d)
+C3_MIX = [("sig_bitflip", 0.30), ("msg_bitflip", 0.10), ("wrong_key", 0.10), ("key_off_curve", 0.10),
+          ("r_zero", 0.05), ("s_zero", 0.05), ("r_ge_n", 0.05), ("s_ge_n", 0.05), ("der_trailing", 0.05),
+          ("der_wrong_tag", 0.05), ("der_nonminimal", 0.05), ("der_long_len", 0.05)]
+C3_EXPECTED = {"sig_bitflip": REJECT_ANY, "msg_bitflip": 1, "wrong_key": 1, "key_off_curve": 3, "r_zero": 1,
+               "s_zero": 1, "r_ge_n": 1, "s_ge_n": 1, "der_trailing": 2, "der_wrong_tag": 2, "der_nonminimal": 2,
+               "der_long_len": 2}
+C3_COMPRESSED_FRAC = 0.10  # valid lanes re-encoded as 33-byte compressed keys (must still accept)
+
+
+def der_ints(sig: bytes):
+    """(r, s) of a minimal DER SEQUENCE{INTEGER r, INTEGER s} as written by the device signer."""
+    lr = sig[3]
+    r = int.from_bytes(sig[4:4 + lr], "big")
+    ls = sig[5 + lr]
+    return r, int.from_bytes(sig[6 + lr:6 + lr + ls], "big")
+
+
+def _der_int(v: int, extra_zero: bool = False) -> bytes:
+    b = v.to_bytes(max(1, (v.bit_length() + 7) // 8), "big")
+    if b[0] & 0x80:
+        b = b"\x00" + b
+    if extra_zero:
+        b = b"\x00" + b
+    return b"\x02" + bytes([len(b)]) + b
+
+
+def der_sig(r: int, s: int, nonminimal_r: bool = False, long_len: bool = False) -> bytes:
+    body = _der_int(r, nonminimal_r) + _der_int(s)
+    return b"\x30" + (b"\x81" if long_len else b"") + bytes([len(body)]) + body
+
+
+def make_c3_corpus(engine, n: int, seed: int, device, corrupt_frac: float = 0.01, stream=None, dev_index: int = 0):
+    """Returns (scheme[n], keys[n,65], key_len[n], sigs[n,72], sig_len[n], msgs[n,32], expected[n] int16, cats).
+    Schemes alternate secp256k1 / P-256 lane by lane; keys and sigs are made by the device signer."""
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    scheme = (2 + (torch.arange(n, device=device) & 1)).to(torch.uint8)
+    seeds = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device=device, generator=g)
+    msgs = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device=device, generator=g)
+    keys = torch.zeros((n, 65), dtype=torch.uint8, device=device)
+    key_len = torch.zeros(n, dtype=torch.uint8, device=device)
+    sigs = torch.zeros((n, 72), dtype=torch.uint8, device=device)
+    sig_len = torch.zeros(n, dtype=torch.uint8, device=device)
+    engine.ecdsa_sign_device(scheme, seeds, msgs, keys, key_len, sigs, sig_len, device=dev_index, stream=stream)
+    torch.cuda.synchronize(device)
+    del seeds
+    expected, cats = corrupt_c3(scheme, keys, key_len, sigs, sig_len, msgs, seed, g, corrupt_frac)
+    torch.cuda.synchronize(device)
+    return scheme, keys, key_len, sigs, sig_len, msgs, expected, cats
+
+
+def corrupt_c3(scheme, keys, key_len, sigs, sig_len, msgs, seed: int, g, corrupt_frac: float = 0.01):
+    """Apply the C3 catalogue in place (CPU or GPU tensors); then compress a share of the untouched keys."""
+    import torch
+
+    n, device = keys.shape[0], keys.device
+    expected = torch.zeros(n, dtype=torch.int16, device=device)
+    ncor = int(n * corrupt_frac)
+    perm = torch.randperm(n, device=device, generator=g)
+    cor = perm[:ncor]
+    cats: Dict[str, torch.Tensor] = {}
+    start = 0
+    for i, (name, frac) in enumerate(C3_MIX):
+        cnt = ncor - start if i == len(C3_MIX) - 1 else int(round(ncor * frac))
+        cats[name] = cor[start:start + cnt]
+        start += cnt
+    orig_keys = keys.clone()
+
+    idx = cats["sig_bitflip"]
+    if idx.numel():
+        ln = sig_len[idx].to(torch.int64)
+        bit = (torch.rand(idx.numel(), device=device, generator=g) * (ln * 8).to(torch.float32)).to(torch.int64)
+        bit = torch.minimum(bit, ln * 8 - 1)
+        sigs[idx, bit // 8] ^= (1 << (bit % 8)).to(torch.uint8)
+    idx = cats["msg_bitflip"]
+    if idx.numel():
+        bit = torch.randint(0, 256, (idx.numel(),), device=device, generator=g)
+        msgs[idx, bit // 8] ^= (1 << (bit % 8)).to(torch.uint8)
+    idx = cats["wrong_key"]  # lane +- 2 has the same curve (schemes alternate)
+    keys[idx] = orig_keys[(idx + 2) % n if n > 2 else idx]
+    idx = cats["key_off_curve"]
+    if idx.numel():
+        bit = torch.randint(0, 256, (idx.numel(),), device=device, generator=g)
+        keys[idx, 33 + bit // 8] ^= (1 << (bit % 8)).to(torch.uint8)
+
+    # DER / range edits: re-encoded on the host (a few hundred lanes per 2^24)
+    edit = [nm for nm in ("r_zero", "s_zero", "r_ge_n", "s_ge_n", "der_trailing", "der_wrong_tag",
+                          "der_nonminimal", "der_long_len") if cats[nm].numel()]
+    if edit:
+        all_idx = torch.cat([cats[nm] for nm in edit])
+        S = sigs[all_idx].cpu().numpy()
+        SL = sig_len[all_idx].cpu().numpy()
+        SC = scheme[all_idx].cpu().numpy()
+        outS, outL, pos = S.copy(), SL.copy(), 0
+        for nm in edit:
+            for _ in range(cats[nm].numel()):
+                sig = S[pos, :SL[pos]].tobytes()
+                r, s = der_ints(sig)
+                nn = CURVE_N[int(SC[pos])]
+                if nm == "r_zero":
+                    new = der_sig(0, s)
+                elif nm == "s_zero":
+                    new = der_sig(r, 0)
+                elif nm == "r_ge_n":
+                    new = der_sig(r + nn if r + nn < 2**256 else nn, s)
+                elif nm == "s_ge_n":
+                    new = der_sig(r, s + nn if s + nn < 2**256 else nn)
+                elif nm == "der_trailing":
+                    new = sig + b"\x00" if len(sig) < 72 else b"\x31" + sig[1:]
+                elif nm == "der_wrong_tag":
+                    new = b"\x31" + sig[1:]
+                elif nm == "der_nonminimal":
+                    new = der_sig(r, s, nonminimal_r=True)
+                    if len(new) > 72:
+                        new = b"\x30" + sig[1:2] + b"\x03" + sig[3:]  # INTEGER tag -> BIT STRING
+                else:  # der_long_len: sequence length in long form (BER, not DER)
+                    new = der_sig(r, s, long_len=True)
+                    if len(new) > 72:
+                        new = b"\x30\x81" + sig[1:-1]  # long form, body truncated by one byte
+                outS[pos] = 0
+                outS[pos, :len(new)] = np.frombuffer(new, np.uint8)
+                outL[pos] = len(new)
+                pos += 1
+        sigs[all_idx] = torch.from_numpy(outS).to(device)
+        sig_len[all_idx] = torch.from_numpy(outL).to(device)
+
+    for name, idx in cats.items():
+        expected[idx] = C3_EXPECTED[name]
+    # compressed keys on a share of the valid lanes: 02/03 || X
+    ncomp = int((n - ncor) * C3_COMPRESSED_FRAC)
+    comp = perm[ncor:ncor + ncomp]
+    if comp.numel():
+        keys[comp, 0] = 2 + (keys[comp, 64] & 1)
+        keys[comp, 33:] = 0
+        key_len[comp] = 33
+    cats["compressed_valid"] = comp
+    return expected, cats

@@ -51,6 +51,9 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
                                const uint32_t* gr1, const uint8_t* pre_status, uint8_t* status,
                                unsigned long long* verdict, unsigned int* counters6, unsigned int* perm,
                                hipStream_t s);
+hipError_t launch_ecdsa_sign(const uint8_t* scheme, const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len,
+                             uint64_t n, const uint32_t* gk1, const uint32_t* gr1, uint8_t* keys, uint8_t* key_len,
+                             uint8_t* sigs, uint8_t* sig_len, hipStream_t s);
 }  // namespace cordahip
 
 using namespace cordahip;
@@ -608,6 +611,20 @@ int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_se
   return hip_err(launch_ed25519_sign(static_cast<const uint8_t*>(d_seeds), static_cast<const uint8_t*>(d_msgs),
                                      msg_len, n, d->btab, static_cast<uint8_t*>(d_pubs),
                                      static_cast<uint8_t*>(d_sigs), s));
+}
+
+int cordahip_ecdsa_sign_device(cordahip_ctx* ctx, int device, const void* d_scheme, const void* d_seeds,
+                               const void* d_msgs, uint32_t msg_len, uint64_t n, void* d_keys, void* d_key_len,
+                               void* d_sigs, void* d_sig_len, void* hip_stream) {
+  Device* d = dev_at(ctx, device);
+  if (!d || (n && (!d_scheme || !d_seeds || !d_keys || !d_key_len || !d_sigs || !d_sig_len || (msg_len && !d_msgs))))
+    return CORDAHIP_ERR_INVALID_ARG;
+  if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  return hip_err(launch_ecdsa_sign(static_cast<const uint8_t*>(d_scheme), static_cast<const uint8_t*>(d_seeds),
+                                   static_cast<const uint8_t*>(d_msgs), msg_len, n, d->gtab_k1, d->gtab_r1,
+                                   static_cast<uint8_t*>(d_keys), static_cast<uint8_t*>(d_key_len),
+                                   static_cast<uint8_t*>(d_sigs), static_cast<uint8_t*>(d_sig_len),
+                                   static_cast<hipStream_t>(hip_stream)));
 }
 
 int cordahip_tx_ids(cordahip_ctx* ctx, const cordahip_txid_batch* batch) {

@@ -490,6 +490,143 @@ CDEV uint8_t ecdsa_verify_lane(const uint8_t* __restrict__ key, uint32_t key_len
   return kStatusBadSig;
 }
 
+// ---- signing (corpus generation for the C3 / C5 benchmarks) -----------------
+// d = SHA-256(seed) mod n, k = SHA-256(seed || msg) mod n (deterministic
+// synthetic nonces: this is test-data generation, not a production signer).
+template <class C>
+CDEV void fixed_base_g(jpt& acc, const u256& k, const uint32_t* __restrict__ gtab) {
+  u256 kk;
+  bool neg;
+  split_sign<typename C::N>(kk, neg, k);
+  acc.inf = true;
+  for (int j = 31; j >= 0; j--) {
+    if (j != 31)
+      for (int t = 0; t < 8; t++) jdbl<C>(acc, acc);
+    const int d = booth_digit<8>(kk.v, j);
+    if (d != 0) {
+      u256 gx, gy;
+      load_g(gx, gy, gtab, d < 0 ? -d : d);
+      if ((d < 0) != neg) mod_neg<typename C::P>(gy, gy);
+      jmadd<C>(acc, acc, gx, gy);
+    }
+  }
+}
+
+template <class C>
+CDEV void to_affine(u256& x, u256& y, const jpt& p) {  // plain (non-Montgomery) coordinates
+  using P = typename C::P;
+  u256 zi, zi2;
+  mont_pow_const<P, typename C::Pm2>(zi, p.Z);
+  mont_sqr<P>(zi2, zi);
+  mont_mul<P>(x, p.X, zi2);
+  mont_mul<P>(zi2, zi2, zi);
+  mont_mul<P>(y, p.Y, zi2);
+  from_mont<P>(x, x);
+  from_mont<P>(y, y);
+}
+
+CDEV void put_be32(uint8_t* o, const u256& v) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t w = v.v[7 - i];
+    o[4 * i] = w >> 24;
+    o[4 * i + 1] = w >> 16;
+    o[4 * i + 2] = w >> 8;
+    o[4 * i + 3] = w;
+  }
+}
+// minimal DER INTEGER of a positive value < 2^256; returns bytes written
+CDEV uint32_t der_put_int(uint8_t* o, const u256& v) {
+  uint8_t be[32];
+  put_be32(be, v);
+  int start = 0;
+  while (start < 31 && be[start] == 0) start++;
+  const bool pad = be[start] >= 0x80;
+  const uint32_t len = (32 - start) + (pad ? 1 : 0);
+  o[0] = 0x02;
+  o[1] = (uint8_t)len;
+  uint32_t p = 2;
+  if (pad) o[p++] = 0;
+  for (int i = start; i < 32; i++) o[p++] = be[i];
+  return p;
+}
+
+template <class C>
+CDEV u256 hash_mod_n(const uint8_t* p, uint64_t len) {
+  uint32_t hw[8];
+  sha256_bytes(hw, p, len);
+  u256 e, t;
+#pragma unroll
+  for (int i = 0; i < 8; i++) e.v[i] = hw[7 - i];
+  if (!u256_sub(t, e, mod_m<typename C::N>())) e = t;
+  if (u256_iszero(e)) e.v[0] = 1;
+  return e;
+}
+
+template <class C>
+CDEV void ecdsa_sign_lane(const uint8_t* __restrict__ seed, const uint8_t* __restrict__ msg, uint32_t msg_len,
+                          const uint32_t* __restrict__ gtab, uint8_t* key_out, uint8_t* key_len_out, uint8_t* sig_out,
+                          uint8_t* sig_len_out) {
+  using N = typename C::N;
+  uint8_t buf[32 + 64];
+  for (int i = 0; i < 32; i++) buf[i] = seed[i];
+  const u256 d = hash_mod_n<C>(buf, 32);
+  const uint32_t ml = msg_len <= 64 ? msg_len : 64;
+  for (uint32_t i = 0; i < ml; i++) buf[32 + i] = msg[i];
+  const u256 k = hash_mod_n<C>(buf, 32 + ml);
+  jpt Q, R;
+  fixed_base_g<C>(Q, d, gtab);
+  fixed_base_g<C>(R, k, gtab);
+  u256 qx, qy, rx, ry;
+  to_affine<C>(qx, qy, Q);
+  to_affine<C>(rx, ry, R);
+  key_out[0] = 4;
+  put_be32(key_out + 1, qx);
+  put_be32(key_out + 33, qy);
+  *key_len_out = 65;
+  u256 r = rx, t;
+  if (!u256_sub(t, r, mod_m<N>())) r = t;  // r = x mod n
+  uint32_t hw[8];
+  sha256_bytes(hw, msg, msg_len);
+  u256 e;
+#pragma unroll
+  for (int i = 0; i < 8; i++) e.v[i] = hw[7 - i];
+  if (!u256_sub(t, e, mod_m<N>())) e = t;
+  // s = k^-1 (e + r d) mod n
+  u256 km, kinv, rm, rd, sum, s;
+  to_mont<N>(km, k);
+  mont_pow_const<N, typename C::Nm2>(kinv, km);
+  to_mont<N>(rm, r);
+  mont_mul<N>(rd, rm, d);
+  mod_add<N>(sum, e, rd);
+  mont_mul<N>(s, kinv, sum);
+  uint8_t body[70];
+  uint32_t p = der_put_int(body, r);
+  p += der_put_int(body + p, s);
+  sig_out[0] = 0x30;
+  sig_out[1] = (uint8_t)p;
+  for (uint32_t i = 0; i < p; i++) sig_out[2 + i] = body[i];
+  *sig_len_out = (uint8_t)(p + 2);
+}
+
+__global__ void __launch_bounds__(256) ecdsa_sign_kernel(const uint8_t* __restrict__ scheme,
+                                                        const uint8_t* __restrict__ seeds,
+                                                        const uint8_t* __restrict__ msgs, uint32_t msg_len,
+                                                        uint64_t n, const uint32_t* __restrict__ gk1,
+                                                        const uint32_t* __restrict__ gr1, uint8_t* __restrict__ keys,
+                                                        uint8_t* __restrict__ key_len, uint8_t* __restrict__ sigs,
+                                                        uint8_t* __restrict__ sig_len) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* msg = msgs + i * (uint64_t)msg_len;
+  if (scheme[i] == 2)
+    ecdsa_sign_lane<Curve<2>>(seeds + i * 32, msg, msg_len, gk1, keys + i * 65, key_len + i, sigs + i * 72,
+                              sig_len + i);
+  else
+    ecdsa_sign_lane<Curve<3>>(seeds + i * 32, msg, msg_len, gr1, keys + i * 65, key_len + i, sigs + i * 72,
+                              sig_len + i);
+}
+
 // ---- device-side scheme partition (wave-aggregated atomics) -----------------
 CDEV int scheme_class(uint8_t s) { return s == 2 ? 0 : s == 3 ? 1 : 2; }
 
@@ -563,6 +700,15 @@ __global__ void __launch_bounds__(256) verdict_kernel(const uint8_t* __restrict_
 
 // ---------------------------------------------------------------------------
 size_t ecdsa_gtable_bytes() { return (size_t)kGEntries * kGEntryWords * sizeof(uint32_t); }
+
+hipError_t launch_ecdsa_sign(const uint8_t* scheme, const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len,
+                             uint64_t n, const uint32_t* gk1, const uint32_t* gr1, uint8_t* keys, uint8_t* key_len,
+                             uint8_t* sigs, uint8_t* sig_len, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(ecdsa_sign_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, scheme, seeds, msgs,
+                     msg_len, n, gk1, gr1, keys, key_len, sigs, sig_len);
+  return hipGetLastError();
+}
 
 hipError_t launch_ecdsa_gtables(uint32_t* k1, uint32_t* r1, hipStream_t s) {
   hipLaunchKernelGGL(ecdsa_gtable_kernel<Curve<2>>, dim3((kGEntries + 63) / 64), dim3(64), 0, s, k1);

@@ -101,6 +101,14 @@ class Engine:
                                                  msgs.shape[1], n, pubs.data_ptr(), sigs.data_ptr(), s),
               "cordahip_ed25519_sign_device")
 
+    def ecdsa_sign_device(self, scheme, seeds, msgs, keys, key_len, sigs, sig_len, device: int = 0, stream=None):
+        """Device tensors: scheme[n] u8 (2/3), seeds[n,32], msgs[n,L] -> keys[n,65], key_len[n], sigs[n,72], sig_len[n]."""
+        n = seeds.shape[0]
+        s = stream.cuda_stream if stream is not None else 0
+        check(lib().cordahip_ecdsa_sign_device(self._ctx, device, scheme.data_ptr(), seeds.data_ptr(), msgs.data_ptr(),
+                                               msgs.shape[1], n, keys.data_ptr(), key_len.data_ptr(), sigs.data_ptr(),
+                                               sig_len.data_ptr(), s), "cordahip_ecdsa_sign_device")
+
     # ---- transactions: WireTransaction.id and SignedTransaction verification ---
     def _tx_arrays(self, txs: Sequence[Sequence[bytes]]):
         leaves = [leaf for tx in txs for leaf in tx]

@@ -136,6 +136,14 @@ int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_sc
 int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_seeds, const void* d_msgs,
                                  uint32_t msg_len, uint64_t n, void* d_pubs, void* d_sigs, void* hip_stream);
 
+/* ECDSA keygen + sign (device memory), corpus generation: per lane scheme 2/3,
+ * d = SHA-256(seed) mod n, k = SHA-256(seed || msg[:64]) mod n; writes the
+ * uncompressed SEC1 key (65-byte slot, key_len = 65) and the DER signature
+ * (72-byte slot + sig_len). Not a production signer (deterministic synthetic nonce). */
+int cordahip_ecdsa_sign_device(cordahip_ctx* ctx, int device, const void* d_scheme, const void* d_seeds,
+                               const void* d_msgs, uint32_t msg_len, uint64_t n, void* d_keys, void* d_key_len,
+                               void* d_sigs, void* d_sig_len, void* hip_stream);
+
 /* ---- transaction ids and SignedTransaction batches ----------------------- */
 /* tx-level statuses (tx_status[t]) in addition to the lane statuses above */
 #define CORDAHIP_TX_NO_LEAVES 6     /* MerkleTreeException: empty component list (MerkleTree.kt:49-50) */

@@ -86,3 +86,35 @@ def test_device_path(engine, oracle):
     v = verdict.cpu().numpy().view(np.uint64)
     for i in range(n):
         assert ((int(v[i // 64]) >> (i % 64)) & 1) == (want[i] == 0)
+
+
+def test_device_signer_matches_oracle(engine):
+    """cordahip_ecdsa_sign_device (C3 corpus generator) vs the Python oracle, then
+    its output through the device verifier."""
+    import torch
+    import bc_ecdsa as ec
+    n, L = 192, 32
+    rng = np.random.default_rng(9)
+    scheme = np.where(rng.random(n) < 0.5, 2, 3).astype(np.uint8)
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(v).to(dev) for k, v in (("scheme", scheme), ("seeds", seeds), ("msgs", msgs))}
+    keys = torch.zeros((n, 65), dtype=torch.uint8, device=dev)
+    kl = torch.zeros(n, dtype=torch.uint8, device=dev)
+    sigs = torch.zeros((n, 72), dtype=torch.uint8, device=dev)
+    sl = torch.zeros(n, dtype=torch.uint8, device=dev)
+    engine.ecdsa_sign_device(t["scheme"], t["seeds"], t["msgs"], keys, kl, sigs, sl)
+    torch.cuda.synchronize()
+    K, KL, S, SL = (x.cpu().numpy() for x in (keys, kl, sigs, sl))
+    for i in range(n):
+        c = ec.CURVES[int(scheme[i])]
+        d = int.from_bytes(hashlib.sha256(seeds[i].tobytes()).digest(), "big") % c.n or 1
+        k = int.from_bytes(hashlib.sha256(seeds[i].tobytes() + msgs[i].tobytes()).digest(), "big") % c.n or 1
+        assert KL[i] == 65 and K[i].tobytes() == ec.keypair(int(scheme[i]), d), i
+        want = ec.der_encode(*ec.sign(int(scheme[i]), d, msgs[i].tobytes(), k))
+        assert S[i, :SL[i]].tobytes() == want, i
+    st = torch.zeros(n, dtype=torch.uint8, device=dev)
+    engine.ecdsa_verify_device(t["scheme"], keys, kl, sigs, sl, t["msgs"], st)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
