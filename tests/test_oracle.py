@@ -11,6 +11,7 @@ import ctypes
 import hashlib
 import random
 
+import numpy as np
 import pytest
 
 import i2p_ed25519 as ed
@@ -150,6 +151,24 @@ def test_ecdsa_c_oracle_matches_golden(oracle, ec_vectors):
         p, s, m = v["pub"], v["sig"], v["msg"]
         got = oracle.oracle_ecdsa_verify(v["scheme"], p, len(p), s, len(s), m, len(m))
         assert got == v["status"], (v["cat"], v["scheme"], v["note"], got, v["status"])
+
+
+def test_ecdsa_c_oracle_batch_matches_golden(oracle, ec_vectors):
+    """The threaded CSR batch entry (bench.py's C3 cpu_baseline) agrees with the goldens."""
+    vs = ec_vectors
+    n = len(vs)
+
+    def csr(field):
+        b = np.frombuffer(b"".join(v[field] for v in vs) or b"\0", np.uint8).copy()
+        off = np.zeros(n + 1, np.uint64)
+        off[1:] = np.cumsum([len(v[field]) for v in vs])
+        return b, off
+    sc = np.array([v["scheme"] for v in vs], np.uint8)
+    (kb, ko), (sb, so), (mb, mo) = csr("pub"), csr("sig"), csr("msg")
+    out = np.full(n, 255, np.uint8)
+    oracle.oracle_ecdsa_verify_batch(n, sc.ctypes.data, kb.ctypes.data, ko.ctypes.data, sb.ctypes.data,
+                                     so.ctypes.data, mb.ctypes.data, mo.ctypes.data, out.ctypes.data, 4)
+    assert [int(x) for x in out] == [v["status"] for v in vs]
 
 
 def test_ecdsa_python_oracle_sample(ec_vectors):
