@@ -285,7 +285,7 @@ CDEV uint8_t ed25519_verify_lane(const uint32_t key[8], const uint32_t sig[16], 
 }
 
 // ---------------------------------------------------------------------------
-// Half-size scalars (the default path). With R decoded strictly,
+// Half-size scalars (A/B alternative, CORDAHIP_ED25519_LADDER=half). With R decoded strictly,
 //   encode([S]B - [h]A) == R_bytes  <=>  P := [S]B - [h]A - R == O.
 // For any (c0, c1) with c0 == c1*h (mod 8L) and c1 odd, c1 != 0 (mod L):
 //   [c1]P == [c1*S mod L]B - [c0]A - [c1]R,   and   [c1]P == O <=> P == O
