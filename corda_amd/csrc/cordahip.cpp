@@ -32,7 +32,8 @@ hipError_t launch_ed25519_btable(uint32_t* tab, hipStream_t s);
 size_t ed25519_btable_bytes();
 hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
                                  uint64_t n, const uint32_t* btab, const uint8_t* pre_status, uint8_t* status,
-                                 unsigned long long* verdict, hipStream_t s);
+                                 unsigned long long* verdict, uint32_t* ws, uint64_t ws_lanes, hipStream_t s);
+size_t ed25519_ws_lane_bytes();
 hipError_t launch_ed25519_sign(const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len, uint64_t n,
                                const uint32_t* btab, uint8_t* pubs, uint8_t* sigs, hipStream_t s);
 hipError_t launch_sha256_leaves(const uint8_t* bytes, const uint64_t* off, uint64_t nleaves, uint32_t* hashes,
@@ -105,7 +106,37 @@ struct Device {
   Stage stage[2];
   std::mutex tx_mu;  // serialises use of tx
   TxWork tx;
+  // Ed25519 split-kernel workspace, shared by every stream that verifies on
+  // this device: ed_mu orders the enqueues, ed_ev makes each user's stream
+  // wait for the previous user's kernels before it reuses the buffer.
+  std::mutex ed_mu;
+  DevBuf ed_ws;
+  hipEvent_t ed_ev = nullptr;
 };
+
+constexpr uint64_t kEdWsLanes = 1ull << 20;  // 3.1 GB of workspace per device
+
+// Enqueue Ed25519 verification of n dense lanes on stream s (device already current).
+hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
+                             uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
+                             unsigned long long* verdict, hipStream_t s) {
+  std::lock_guard<std::mutex> g(d.ed_mu);
+  const uint64_t lanes = std::min<uint64_t>(kEdWsLanes, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
+  if (d.ed_ws.cap < lanes * ed25519_ws_lane_bytes()) {
+    // a smaller buffer may still be in use by an earlier stream
+    hipError_t e = d.ed_ev ? hipEventSynchronize(d.ed_ev) : hipSuccess;
+    if (e != hipSuccess) return e;
+    e = d.ed_ws.ensure(std::max<uint64_t>(lanes, kEdWsLanes / 8) * ed25519_ws_lane_bytes());
+    if (e != hipSuccess) return e;
+  }
+  if (!d.ed_ev && hipEventCreateWithFlags(&d.ed_ev, hipEventDisableTiming) != hipSuccess) return hipErrorUnknown;
+  hipError_t e = hipStreamWaitEvent(s, d.ed_ev, 0);
+  e = e ? e
+        : launch_ed25519_verify(keys, sigs, msgs, msg_len, n, d.btab, pre, status, verdict, d.ed_ws.as<uint32_t>(),
+                                d.ed_ws.cap / ed25519_ws_lane_bytes() / 64 * 64, s);
+  e = e ? e : hipEventRecord(d.ed_ev, s);
+  return e;
+}
 
 int hip_err(hipError_t e) { return e == hipSuccess ? CORDAHIP_SUCCESS : CORDAHIP_ERR_HIP; }
 
@@ -148,9 +179,9 @@ int verify_shard_host(Device& d, const uint8_t* keys, const uint8_t* sigs, const
     if (pre) e = e ? e : hipMemcpyAsync(st.pre.p, pre + off, c, hipMemcpyHostToDevice, s);
     const bool aligned = (off % 64) == 0;
     e = e ? e
-          : launch_ed25519_verify(st.keys.as<uint8_t>(), st.sigs.as<uint8_t>(), st.msgs.as<uint8_t>(), msg_len, c,
-                                  d.btab, pre ? st.pre.as<uint8_t>() : nullptr, st.status.as<uint8_t>(),
-                                  st.verdict.as<unsigned long long>(), s);
+          : ed_verify_enqueue(d, st.keys.as<uint8_t>(), st.sigs.as<uint8_t>(), st.msgs.as<uint8_t>(), msg_len, c,
+                              pre ? st.pre.as<uint8_t>() : nullptr, st.status.as<uint8_t>(),
+                              st.verdict.as<unsigned long long>(), s);
     e = e ? e : hipMemcpyAsync(status + off, st.status.p, c, hipMemcpyDeviceToHost, s);
     if (verdict && aligned)
       e = e ? e : hipMemcpyAsync(verdict + off / 64, st.verdict.p, ((c + 63) / 64) * 8, hipMemcpyDeviceToHost, s);
@@ -486,6 +517,8 @@ void cordahip_shutdown(cordahip_ctx* ctx) {
     if (d->gtab_k1) (void)hipFree(d->gtab_k1);
     if (d->gtab_r1) (void)hipFree(d->gtab_r1);
     if (d->btab) (void)hipFree(d->btab);
+    if (d->ed_ws.p) (void)hipFree(d->ed_ws.p);
+    if (d->ed_ev) (void)hipEventDestroy(d->ed_ev);
     if (d->ev0) (void)hipEventDestroy(d->ev0);
     if (d->ev1) (void)hipEventDestroy(d->ev1);
     if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -558,9 +591,9 @@ int cordahip_ed25519_verify_device(cordahip_ctx* ctx, int device, const void* d_
   hipStream_t s = static_cast<hipStream_t>(hip_stream);  // NULL = the device's null stream
   hipError_t e = hipEventRecord(d->ev0, s);
   e = e ? e
-        : launch_ed25519_verify(static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
-                                static_cast<const uint8_t*>(d_msgs), msg_len, n, d->btab, nullptr,
-                                static_cast<uint8_t*>(d_status), static_cast<unsigned long long*>(d_verdict), s);
+        : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
+                            static_cast<const uint8_t*>(d_msgs), msg_len, n, nullptr, static_cast<uint8_t*>(d_status),
+                            static_cast<unsigned long long*>(d_verdict), s);
   e = e ? e : hipEventRecord(d->ev1, s);
   return hip_err(e);
 }
@@ -658,9 +691,9 @@ int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, cons
                                  static_cast<uint8_t*>(d_txid), static_cast<uint8_t*>(d_tx_status), s);
   e = e ? e : launch_gather_txid(static_cast<const uint8_t*>(d_txid), static_cast<const uint64_t*>(d_tx_sig_off), ntx,
                                  d->tx.msgs.as<uint8_t>(), s);
-  e = e ? e : launch_ed25519_verify(static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
-                                    d->tx.msgs.as<uint8_t>(), 32, nsig, d->btab, nullptr,
-                                    static_cast<uint8_t*>(d_sig_status), nullptr, s);
+  e = e ? e : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
+                                d->tx.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status),
+                                nullptr, s);
   e = e ? e : launch_tx_reduce(static_cast<const uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off),
                                ntx, static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);
   e = e ? e : hipEventRecord(d->ev1, s);

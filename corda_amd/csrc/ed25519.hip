@@ -16,6 +16,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <string>
+
 #include "fe25519.hpp"
 #include "ge25519.hpp"
 #include "sc25519.hpp"
@@ -122,7 +124,7 @@ CDEV void load_niels(ge_niels& n, const uint32_t* __restrict__ tab, int idx) {
 // conditional negation of a niels / cached point: swap (y+x, y-x), negate t
 CDEV void niels_cneg(ge_niels& n, bool neg) {
   fe nt;
-  fe_neg(nt, n.xy2d);
+  fe_neg_loose(nt, n.xy2d);  // 2x: only ever the g-operand of fe_mul
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     const uint32_t a = n.ypx.v[i], b = n.ymx.v[i];
@@ -133,7 +135,7 @@ CDEV void niels_cneg(ge_niels& n, bool neg) {
 }
 CDEV void cached_cneg(ge_cached& c, bool neg) {
   fe nt;
-  fe_neg(nt, c.T2d);
+  fe_neg_loose(nt, c.T2d);
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     const uint32_t a = c.YpX.v[i], b = c.YmX.v[i];
@@ -619,6 +621,380 @@ __global__ void __launch_bounds__(256) ed25519_verify_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Split verification (the default): two kernels per chunk of lanes.
+//
+//   prep   : key decode, canonical Abyte, SHA-512, h mod L, S_eff, and the
+//            per-lane table [0..8](-A) in cached form -> per-lane workspace
+//            record in HBM (AoS, 1520 B), early statuses -> status[]
+//   ladder : the 64-window Straus ladder, B table staged in LDS, the next
+//            window's -A entry prefetched from the workspace while the four
+//            doublings run; encode(R') == R; status + verdict ballot.
+//
+// Splitting gives each phase its own register allocation: the fused kernel
+// is pinned at 512 registers (1 wave/SIMD) by SHA-512 / decompression and
+// keeps its dynamically indexed table in scratch; the ladder alone has
+// neither. The workspace traffic (1.5 KB written, 64 x 160 B gathered per
+// lane) is cache-friendly: each lane reads whole 160-B entries.
+static constexpr int kWsTabWords = 9 * 40;                  // [0..8](-A), cached (YpX, YmX, Z, T2d)
+static constexpr int kWsH = kWsTabWords;                     // h (8 words)
+static constexpr int kWsS = kWsTabWords + 8;                 // S_eff (8 words)
+static constexpr int kWsLaneWords = kWsTabWords + 16 + 4;    // 380 words = 1520 B (16-B aligned)
+static constexpr int kLdsBStride = 36;                       // words per B entry in LDS (bank spread)
+static constexpr uint8_t kStatusPending = 0xff;
+
+CDEV void store_cached(uint32_t* __restrict__ o, const ge_cached& c) {
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+  uint32_t w[40];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    w[i] = c.YpX.v[i];
+    w[10 + i] = c.YmX.v[i];
+    w[20 + i] = c.Z.v[i];
+    w[30 + i] = c.T2d.v[i];
+  }
+#pragma unroll
+  for (int q = 0; q < 10; q++) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+CDEV void load_cached(ge_cached& c, const uint32_t* __restrict__ p) {
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);
+  uint32_t w[40];
+#pragma unroll
+  for (int q = 0; q < 10; q++) {
+    const uint4 v = p4[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    c.YpX.v[i] = w[i];
+    c.YmX.v[i] = w[10 + i];
+    c.Z.v[i] = w[20 + i];
+    c.T2d.v[i] = w[30 + i];
+  }
+}
+
+// lanes [base, base + m) of the batch; ws holds m records
+__global__ void __launch_bounds__(256) ed25519_prep_kernel(
+    const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
+    uint32_t msg_len, uint64_t base, uint64_t m, const uint8_t* __restrict__ pre_status,
+    uint8_t* __restrict__ status, uint32_t* __restrict__ ws) {
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= m) return;
+  const uint64_t i = base + li;
+  const uint4* k4 = reinterpret_cast<const uint4*>(keys + i * 32);
+  const uint4* s4 = reinterpret_cast<const uint4*>(sigs + i * 64);
+  const uint4 ka = k4[0], kb = k4[1];
+  const uint32_t key[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+  const uint4 r0 = s4[0], r1 = s4[1], q0 = s4[2], q1 = s4[3];
+  const uint32_t R[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+  const uint32_t S[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+  uint8_t st = kStatusPending;
+  ge_p3 A;
+  if (!ge_frombytes_i2p(A, key)) {  // i2p GroupElement(Curve, byte[]), before doVerify (Kryo.kt:389-392)
+    st = kStatusBadKey;
+    ge_identity(A);
+  } else if (pre_status && pre_status[i] != kStatusOk) {
+    st = pre_status[i];  // EMPTY / MALFORMED decided by the host
+  } else if (msg_len == 0) {
+    st = kStatusEmpty;  // Crypto.kt:476
+  }
+  uint32_t* rec = ws + li * kWsLaneWords;
+  uint32_t h[8], se[8];
+  if (st == kStatusPending) {
+    uint32_t abyte[8];  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
+    fe_tobytes(abyte, A.Y);
+    abyte[7] |= fe_isnegative(A.X) << 31;
+    uint32_t hd[16];
+    sha512_segments(hd, R, abyte, true, msgs + i * (uint64_t)msg_len, msg_len);
+    sc_reduce512(h, hd);
+    sc_effective_S(se, S, slide_drops_carry(S));
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; q++) h[q] = se[q] = 0;
+  }
+  status[i] = st;
+  // table [k](-A), k = 0..8
+  ge_p3 An = A;
+  fe_neg(An.X, A.X);
+  fe_neg(An.T, A.T);
+  ge_cached c;
+  fe_set(c.YpX, 1);
+  fe_set(c.YmX, 1);
+  fe_set(c.Z, 1);
+  fe_set(c.T2d, 0);
+  store_cached(rec, c);
+  ge_cached c1;
+  ge_to_cached(c1, An);
+  store_cached(rec + 40, c1);
+  ge_p3 Q;
+  ge_dbl<true>(Q, An);
+  ge_to_cached(c, Q);
+  store_cached(rec + 80, c);
+  for (int k = 3; k <= 8; k++) {
+    ge_add<true>(Q, Q, c1);
+    ge_to_cached(c, Q);
+    store_cached(rec + 40 * k, c);
+  }
+  uint4* o4 = reinterpret_cast<uint4*>(rec + kWsH);
+  o4[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  o4[1] = make_uint4(h[4], h[5], h[6], h[7]);
+  o4[2] = make_uint4(se[0], se[1], se[2], se[3]);
+  o4[3] = make_uint4(se[4], se[5], se[6], se[7]);
+}
+
+CDEV void lds_niels(ge_niels& n, const uint32_t* lds, int idx) {
+  const uint4* e = reinterpret_cast<const uint4*>(lds + idx * kLdsBStride);
+  uint32_t w[32];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint4 v = e[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    n.ypx.v[i] = w[i];
+    n.ymx.v[i] = w[10 + i];
+    n.xy2d.v[i] = w[20 + i];
+  }
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_ladder_kernel(
+    const uint8_t* __restrict__ sigs, uint64_t base, uint64_t m, const uint32_t* __restrict__ btab,
+    const uint32_t* __restrict__ ws, uint8_t* __restrict__ status, unsigned long long* __restrict__ verdict) {
+  __shared__ __attribute__((aligned(16))) uint32_t bl[kBTableEntries * kLdsBStride];
+  for (int t = threadIdx.x; t < kBTableEntries * 8; t += blockDim.x) {
+    const int e = t >> 3, q = t & 7;
+    reinterpret_cast<uint4*>(bl + e * kLdsBStride)[q] = reinterpret_cast<const uint4*>(btab + e * kBEntryWords)[q];
+  }
+  __syncthreads();
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = li < m;
+  const uint64_t lc = active ? li : m - 1;  // inactive lanes replay the last record, discard it
+  const uint32_t* rec = ws + lc * kWsLaneWords;
+  uint32_t h[8], s[8];
+  {
+    const uint4* p4 = reinterpret_cast<const uint4*>(rec + kWsH);
+    const uint4 a = p4[0], b = p4[1], c = p4[2], d = p4[3];
+    h[0] = a.x; h[1] = a.y; h[2] = a.z; h[3] = a.w; h[4] = b.x; h[5] = b.y; h[6] = b.z; h[7] = b.w;
+    s[0] = c.x; s[1] = c.y; s[2] = c.z; s[3] = c.w; s[4] = d.x; s[5] = d.y; s[6] = d.z; s[7] = d.w;
+  }
+  ge_p3 P;
+  ge_identity(P);
+  for (int j = 63; j >= 0; j--) {
+    // issue this window's -A entry load first: the four doublings hide it
+    const int da = booth_digit<4>(h, j);
+    ge_cached cur;
+    load_cached(cur, rec + 40 * (da < 0 ? -da : da));
+    if (j != 63) {
+      ge_dbl<false>(P, P);
+      ge_dbl<false>(P, P);
+      ge_dbl<false>(P, P);
+      ge_dbl<true>(P, P);
+    }
+    cached_cneg(cur, da < 0);
+    if ((j & 1) == 0) {
+      ge_add<true>(P, P, cur);
+      const int db = booth_digit<8>(s, j >> 1);
+      ge_niels nb;
+      lds_niels(nb, bl, db < 0 ? -db : db);
+      niels_cneg(nb, db < 0);
+      ge_madd<false>(P, P, nb);
+    } else {
+      ge_add<false>(P, P, cur);
+    }
+  }
+  uint32_t enc[8];
+  ge_tobytes(enc, P);
+  const uint4* s4 = reinterpret_cast<const uint4*>(sigs + (base + lc) * 64);
+  const uint4 r0 = s4[0], r1 = s4[1];
+  const uint32_t diff = (enc[0] ^ r0.x) | (enc[1] ^ r0.y) | (enc[2] ^ r0.z) | (enc[3] ^ r0.w) | (enc[4] ^ r1.x) |
+                        (enc[5] ^ r1.y) | (enc[6] ^ r1.z) | (enc[7] ^ r1.w);
+  const uint64_t i = base + li;
+  uint8_t st = kStatusBadSig;
+  if (active) {
+    st = status[i];
+    if (st == kStatusPending) {
+      st = diff == 0 ? kStatusOk : kStatusBadSig;
+      status[i] = st;
+    }
+  }
+  const unsigned long long ok = __ballot(active && st == kStatusOk);
+  // base is a multiple of 64 (chunk sizes are), so lane 0 of a wave owns a whole verdict word
+  if ((threadIdx.x & 63) == 0 && active && verdict) verdict[i >> 6] = ok;
+}
+
+// ---------------------------------------------------------------------------
+// Split half-size-scalar verification: same prep/ladder split, ladder over
+// [e]B + [c0](+-A) + [c1](-R) with ~128-bit c0, c1 (see half_scalars): 128
+// doublings instead of 252 and no final inversion (P == O is X == 0, Y == Z).
+static constexpr int kWhTabA = 0;                            // [0..8](+-A)
+static constexpr int kWhTabR = 9 * 40;                       // [0..8](-R)
+static constexpr int kWhKa = 18 * 40;                        // |c0|, c1, e (8 words each)
+static constexpr int kWhKr = kWhKa + 8;
+static constexpr int kWhE = kWhKa + 16;
+static constexpr int kWhLaneWords = kWhKa + 24;              // 744 words = 2976 B
+
+CDEV void store_table9(uint32_t* __restrict__ rec, const ge_p3& base) {
+  ge_cached c;
+  fe_set(c.YpX, 1);
+  fe_set(c.YmX, 1);
+  fe_set(c.Z, 1);
+  fe_set(c.T2d, 0);
+  store_cached(rec, c);
+  ge_cached c1;
+  ge_to_cached(c1, base);
+  store_cached(rec + 40, c1);
+  ge_p3 Q;
+  ge_dbl<true>(Q, base);
+  ge_to_cached(c, Q);
+  store_cached(rec + 80, c);
+  for (int k = 3; k <= 8; k++) {
+    ge_add<true>(Q, Q, c1);
+    ge_to_cached(c, Q);
+    store_cached(rec + 40 * k, c);
+  }
+}
+
+CDEV void store8(uint32_t* __restrict__ o, const uint32_t v[8]) {
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+  o4[0] = make_uint4(v[0], v[1], v[2], v[3]);
+  o4[1] = make_uint4(v[4], v[5], v[6], v[7]);
+}
+CDEV void load8(uint32_t v[8], const uint32_t* __restrict__ p) {
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);
+  const uint4 a = p4[0], b = p4[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+__global__ void __launch_bounds__(256) ed25519_prep_half_kernel(
+    const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
+    uint32_t msg_len, uint64_t base, uint64_t m, const uint8_t* __restrict__ pre_status,
+    uint8_t* __restrict__ status, uint32_t* __restrict__ ws) {
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= m) return;
+  const uint64_t i = base + li;
+  const uint4* k4 = reinterpret_cast<const uint4*>(keys + i * 32);
+  const uint4* s4 = reinterpret_cast<const uint4*>(sigs + i * 64);
+  const uint4 ka4 = k4[0], kb4 = k4[1];
+  const uint32_t key[8] = {ka4.x, ka4.y, ka4.z, ka4.w, kb4.x, kb4.y, kb4.z, kb4.w};
+  const uint4 r0 = s4[0], r1 = s4[1], q0 = s4[2], q1 = s4[3];
+  const uint32_t Rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+  const uint32_t S[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+  uint8_t st = kStatusPending;
+  ge_p3 A, R;
+  if (!ge_frombytes_i2p(A, key)) st = kStatusBadKey;  // key decode precedes doVerify (Kryo.kt:389-392)
+  else if (pre_status && pre_status[i] != kStatusOk) st = pre_status[i];
+  else if (msg_len == 0) st = kStatusEmpty;  // Crypto.kt:476
+  else if (!ge_frombytes_strict(R, Rw)) st = kStatusBadSig;  // no canonical point encodes to these bytes
+  uint32_t ka[8], kr[8], e[8];
+  bool c0neg = false;
+  if (st == kStatusPending) {
+    uint32_t abyte[8];  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
+    fe_tobytes(abyte, A.Y);
+    abyte[7] |= fe_isnegative(A.X) << 31;
+    uint32_t hd[16], h[8], se[8], zero[8];
+    sha512_segments(hd, Rw, abyte, true, msgs + i * (uint64_t)msg_len, msg_len);
+    sc_reduce512(h, hd);
+    sc_effective_S(se, S, slide_drops_carry(S));
+    half_scalars(ka, c0neg, kr, h);
+#pragma unroll
+    for (int q = 0; q < 8; q++) zero[q] = 0;
+    sc_muladd(e, kr, se, zero);  // e = c1 S_eff mod L
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; q++) ka[q] = kr[q] = e[q] = 0;
+    ge_identity(A);
+    ge_identity(R);
+  }
+  status[i] = st;
+  // [e]B + [c0](-A) + [c1](-R): -A when c0 > 0, A when c0 < 0; always -R
+  if (!c0neg) {
+    fe_neg(A.X, A.X);
+    fe_neg(A.T, A.T);
+  }
+  fe_neg(R.X, R.X);
+  fe_neg(R.T, R.T);
+  uint32_t* rec = ws + li * kWhLaneWords;
+  store_table9(rec + kWhTabA, A);
+  store_table9(rec + kWhTabR, R);
+  store8(rec + kWhKa, ka);
+  store8(rec + kWhKr, kr);
+  store8(rec + kWhE, e);
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_ladder_half_kernel(
+    uint64_t base, uint64_t m, const uint32_t* __restrict__ btab, const uint32_t* __restrict__ ws,
+    uint8_t* __restrict__ status, unsigned long long* __restrict__ verdict) {
+  __shared__ __attribute__((aligned(16))) uint32_t bl[2 * kBTableEntries * kLdsBStride];
+  for (int t = threadIdx.x; t < 2 * kBTableEntries * 8; t += blockDim.x) {
+    const int e = t >> 3, q = t & 7;
+    reinterpret_cast<uint4*>(bl + e * kLdsBStride)[q] = reinterpret_cast<const uint4*>(btab + e * kBEntryWords)[q];
+  }
+  __syncthreads();
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = li < m;
+  const uint64_t lc = active ? li : m - 1;  // inactive lanes replay the last record, discard it
+  const uint32_t* rec = ws + lc * kWhLaneWords;
+  uint32_t ka[8], kr[8], e[8];
+  load8(ka, rec + kWhKa);
+  load8(kr, rec + kWhKr);
+  load8(e, rec + kWhE);
+  const int bits = max(mp8_bitlen(ka), mp8_bitlen(kr));
+  const int W = max(wave_max((bits + 1 + 3) / 4), 1);
+  const uint32_t* bl128 = bl + kBTableEntries * kLdsBStride;
+  ge_p3 P;
+  ge_identity(P);
+  for (int j = W - 1; j >= 0; j--) {
+    const int da = booth_digit<4>(ka, j), dr = booth_digit<4>(kr, j);
+    ge_cached ca, cr;  // issued before the doublings, consumed after them
+    load_cached(ca, rec + kWhTabA + 40 * (da < 0 ? -da : da));
+    load_cached(cr, rec + kWhTabR + 40 * (dr < 0 ? -dr : dr));
+    if (j != W - 1) {
+      ge_dbl<false>(P, P);
+      ge_dbl<false>(P, P);
+      ge_dbl<false>(P, P);
+      ge_dbl<true>(P, P);
+    }
+    cached_cneg(ca, da < 0);
+    ge_add<true>(P, P, ca);
+    cached_cneg(cr, dr < 0);
+    if ((j & 1) == 0 && j < 32) {
+      ge_add<true>(P, P, cr);
+      const int d0 = booth_digit<8>(e, j >> 1), d1 = booth_digit<8>(e, (j >> 1) + 16);
+      ge_niels nb;
+      lds_niels(nb, bl, d0 < 0 ? -d0 : d0);
+      niels_cneg(nb, d0 < 0);
+      ge_madd<true>(P, P, nb);
+      lds_niels(nb, bl128, d1 < 0 ? -d1 : d1);
+      niels_cneg(nb, d1 < 0);
+      ge_madd<false>(P, P, nb);
+    } else {
+      ge_add<false>(P, P, cr);
+    }
+  }
+  fe d;
+  fe_sub(d, P.Y, P.Z);
+  const bool zero = fe_iszero(P.X) && fe_iszero(d);
+  const uint64_t i = base + li;
+  uint8_t st = kStatusBadSig;
+  if (active) {
+    st = status[i];
+    if (st == kStatusPending) {
+      st = zero ? kStatusOk : kStatusBadSig;
+      status[i] = st;
+    }
+  }
+  const unsigned long long ok = __ballot(active && st == kStatusOk);
+  if ((threadIdx.x & 63) == 0 && active && verdict) verdict[i >> 6] = ok;
+}
+
+// ---------------------------------------------------------------------------
 // RFC 8032 keygen + sign (Crypto.doSign / deriveKeyPairFromEntropy for
 // Ed25519): the GPU corpus generator for bench.py and the C5 stream.
 CDEV void fixed_base_mult(ge_p3& P, const uint32_t k[8], const uint32_t* __restrict__ btab) {
@@ -732,22 +1108,58 @@ hipError_t launch_ed25519_btable(uint32_t* tab, hipStream_t s) {
 }
 size_t ed25519_btable_bytes() { return 2 * (size_t)kBTableEntries * kBEntryWords * sizeof(uint32_t); }
 
-// CORDAHIP_ED25519_LADDER=full selects the full-length (252-doubling) ladder
-// instead of the half-size-scalar one; both are bit-exact, kept for A/B runs.
-static bool use_half_ladder() {
-  static const bool half = [] {
+// CORDAHIP_ED25519_LADDER selects the verification kernels (all bit-exact):
+//   split (default): prep + ladder kernels over a per-lane HBM workspace
+//   split-half     : the same split with the half-size-scalar ladder
+//   fused          : one kernel, full 252-doubling ladder (round-1 baseline)
+//   half           : one kernel, half-size-scalar ladder
+// profiles/r01_bench_c2_ab.json holds the A/B measurements.
+enum class Ladder { kSplit, kSplitHalf, kFused, kHalf };
+static Ladder ladder_mode() {
+  static const Ladder m = [] {
     const char* v = getenv("CORDAHIP_ED25519_LADDER");
-    return v && v[0] == 'h';  // default: full ladder (measured faster, profiles/r01_bench_c2_ab.json)
+    if (!v) return Ladder::kSplit;
+    const std::string s(v);
+    if (s == "split-half") return Ladder::kSplitHalf;
+    if (s == "half") return Ladder::kHalf;
+    if (s == "fused") return Ladder::kFused;
+    return Ladder::kSplit;
   }();
-  return half;
+  return m;
 }
 
+// workspace record size (the larger of the two split layouts)
+size_t ed25519_ws_lane_bytes() { return kWhLaneWords * sizeof(uint32_t); }
+
+// ws: ws_lanes * ed25519_ws_lane_bytes() of device memory (ws_lanes a multiple
+// of 64), used only by the split kernels; the caller serialises its users.
 hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
                                  uint64_t n, const uint32_t* btab, const uint8_t* pre_status, uint8_t* status,
-                                 unsigned long long* verdict, hipStream_t s) {
+                                 unsigned long long* verdict, uint32_t* ws, uint64_t ws_lanes, hipStream_t s) {
   if (n == 0) return hipSuccess;
+  const Ladder mode = (ws && ws_lanes >= 64) ? ladder_mode() : Ladder::kFused;
+  if (mode == Ladder::kSplit || mode == Ladder::kSplitHalf) {
+    for (uint64_t base = 0; base < n; base += ws_lanes) {
+      const uint64_t m = n - base < ws_lanes ? n - base : ws_lanes;
+      const uint32_t blocks = (uint32_t)((m + 255) / 256);
+      if (mode == Ladder::kSplit) {
+        hipLaunchKernelGGL(ed25519_prep_kernel, dim3(blocks), dim3(256), 0, s, keys, sigs, msgs, msg_len, base, m,
+                           pre_status, status, ws);
+        hipLaunchKernelGGL(ed25519_ladder_kernel, dim3(blocks), dim3(256), 0, s, sigs, base, m, btab, ws, status,
+                           verdict);
+      } else {
+        hipLaunchKernelGGL(ed25519_prep_half_kernel, dim3(blocks), dim3(256), 0, s, keys, sigs, msgs, msg_len, base,
+                           m, pre_status, status, ws);
+        hipLaunchKernelGGL(ed25519_ladder_half_kernel, dim3(blocks), dim3(256), 0, s, base, m, btab, ws, status,
+                           verdict);
+      }
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   const uint64_t blocks = (n + 255) / 256;
-  if (use_half_ladder())
+  if (mode == Ladder::kHalf)
     hipLaunchKernelGGL(ed25519_verify_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0, s, keys, sigs, msgs,
                        msg_len, n, btab, pre_status, status, verdict);
   else

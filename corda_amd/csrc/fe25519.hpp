@@ -18,6 +18,10 @@
 //   sum < 2^62.5.
 //   fe_sub(a, b) = a + 4p - b followed by a 32-bit carry pass: b may be
 //   loose (4p limbs >= 2^27), output tight.
+//   fe_mul(r, f, g) is asymmetric: g (scaled by 19) must stay <= 3.3x tight,
+//   f may be up to ~5x (column sums then stay below 2^63). The group
+//   formulas use carry-free fe_sub_loose / fe_neg_loose wherever the
+//   result only feeds such an operand (bounds: tools/proto/fe_bounds.py).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -69,6 +73,21 @@ CDEV void fe_sub(fe& r, const fe& a, const fe& b) {
 #pragma unroll
   for (int i = 1; i < 10; i++) r.v[i] = a.v[i] + ((i & 1) ? 4u * M25 : 4u * M26) - b.v[i];
   fe_carry(r);
+}
+
+// r = a + 2p - b with NO carry pass: b must be tight (2p limbs >= tight
+// limbs); the result is at most a + 2p. Only for values that go straight into
+// fe_mul / fe_sq within the operand bounds checked in tools/proto/fe_bounds.py.
+CDEV void fe_sub_loose(fe& r, const fe& a, const fe& b) {
+  r.v[0] = a.v[0] + (2u * ((1u << 26) - 19)) - b.v[0];
+#pragma unroll
+  for (int i = 1; i < 10; i++) r.v[i] = a.v[i] + ((i & 1) ? 2u * M25 : 2u * M26) - b.v[i];
+}
+// r = 2p - a (a tight), no carry: <= 2x tight
+CDEV void fe_neg_loose(fe& r, const fe& a) {
+  r.v[0] = (2u * ((1u << 26) - 19)) - a.v[0];
+#pragma unroll
+  for (int i = 1; i < 10; i++) r.v[i] = ((i & 1) ? 2u * M25 : 2u * M26) - a.v[i];
 }
 
 CDEV void fe_neg(fe& r, const fe& a) {

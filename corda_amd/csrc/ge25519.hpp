@@ -45,12 +45,12 @@ CDEV void ge_dbl(ge_p3& r, const ge_p3& p) {
   fe_sq(c, p.Z);
   fe_add(t, p.X, p.Y);
   fe_sq(t, t);
-  fe_add(h, a, b);   // H' = A + B        (= -H)
-  fe_sub(e, h, t);   // E' = A + B - (X+Y)^2 (= -E)
-  fe_sub(g, a, b);   // G' = A - B        (= -G)
+  fe_add(h, a, b);         // H' = A + B          (= -H), 2x
+  fe_sub(e, h, t);         // E' = A + B - (X+Y)^2 (= -E), tight
+  fe_sub_loose(g, a, b);   // G' = A - B          (= -G), <= 3x
   fe_add(f, c, c);
-  fe_add(f, f, g);   // F' = 2Z^2 + G'    (= -F)
-  fe_mul(r.X, e, f);
+  fe_add(f, f, g);         // F' = 2Z^2 + G'      (= -F), <= 5x: f-operand only
+  fe_mul(r.X, f, e);
   fe_mul(r.Y, g, h);
   fe_mul(r.Z, f, g);
   if (WANT_T) fe_mul(r.T, e, h);
@@ -60,18 +60,18 @@ CDEV void ge_dbl(ge_p3& r, const ge_p3& p) {
 template <bool WANT_T>
 CDEV void ge_add(ge_p3& r, const ge_p3& p, const ge_cached& q) {
   fe a, b, c, d, e, f, g, h, t;
-  fe_sub(t, p.Y, p.X);
+  fe_sub_loose(t, p.Y, p.X);  // <= 3x
   fe_mul(a, t, q.YmX);
   fe_add(t, p.Y, p.X);
   fe_mul(b, t, q.YpX);
   fe_mul(c, p.T, q.T2d);
   fe_mul(d, p.Z, q.Z);
-  fe_add(d, d, d);
-  fe_sub(e, b, a);
-  fe_sub(f, d, c);
-  fe_add(g, d, c);
-  fe_add(h, b, a);
-  fe_mul(r.X, e, f);
+  fe_add(d, d, d);            // 2x
+  fe_sub_loose(e, b, a);      // <= 3x
+  fe_sub_loose(f, d, c);      // <= 4x: f-operand only
+  fe_add(g, d, c);            // <= 3x
+  fe_add(h, b, a);            // 2x
+  fe_mul(r.X, f, e);
   fe_mul(r.Y, g, h);
   fe_mul(r.Z, f, g);
   if (WANT_T) fe_mul(r.T, e, h);
@@ -81,17 +81,17 @@ CDEV void ge_add(ge_p3& r, const ge_p3& p, const ge_cached& q) {
 template <bool WANT_T>
 CDEV void ge_madd(ge_p3& r, const ge_p3& p, const ge_niels& q) {
   fe a, b, c, d, e, f, g, h, t;
-  fe_sub(t, p.Y, p.X);
+  fe_sub_loose(t, p.Y, p.X);
   fe_mul(a, t, q.ymx);
   fe_add(t, p.Y, p.X);
   fe_mul(b, t, q.ypx);
   fe_mul(c, p.T, q.xy2d);
   fe_add(d, p.Z, p.Z);
-  fe_sub(e, b, a);
-  fe_sub(f, d, c);
+  fe_sub_loose(e, b, a);
+  fe_sub_loose(f, d, c);
   fe_add(g, d, c);
   fe_add(h, b, a);
-  fe_mul(r.X, e, f);
+  fe_mul(r.X, f, e);
   fe_mul(r.Y, g, h);
   fe_mul(r.Z, f, g);
   if (WANT_T) fe_mul(r.T, e, h);
