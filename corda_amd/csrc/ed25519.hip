@@ -175,6 +175,7 @@ CDEV void sha512_segments(uint32_t out_le[16], const uint32_t s0[8], const uint3
     w[15] = total * 8;
     sha512_block(h, w);
   } else {
+#ifndef ED_NO_GENERIC_SHA
     const uint64_t nblocks = (total + 17 + 127) / 128;
     for (uint64_t b = 0; b < nblocks; b++) {
       for (int q = 0; q < 16; q++) {
@@ -194,6 +195,7 @@ CDEV void sha512_segments(uint32_t out_le[16], const uint32_t s0[8], const uint3
       }
       sha512_block(h, w);
     }
+#endif
   }
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -306,15 +308,6 @@ CDEV bool mp8_ge(const uint32_t a[8], const uint32_t b[8]) {
   }
   return gt || eq;
 }
-CDEV void mp8_sub(uint32_t a[8], const uint32_t b[8]) {
-  uint64_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint64_t d = (uint64_t)a[i] - b[i] - br;
-    a[i] = (uint32_t)d;
-    br = (d >> 63) & 1;
-  }
-}
 CDEV void mp8_add(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
   uint64_t c = 0;
 #pragma unroll
@@ -323,19 +316,6 @@ CDEV void mp8_add(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
     r[i] = (uint32_t)c;
     c >>= 32;
   }
-}
-CDEV uint32_t mp8_shl1(uint32_t r[8], const uint32_t a[8]) {
-  const uint32_t out = a[7] >> 31;
-#pragma unroll
-  for (int i = 7; i > 0; i--) r[i] = (a[i] << 1) | (a[i - 1] >> 31);
-  r[0] = a[0] << 1;
-  return out;
-}
-CDEV void mp8_shr1(uint32_t a[8], bool arith) {
-  const uint32_t top = arith ? (a[7] & 0x80000000u) : 0u;
-#pragma unroll
-  for (int i = 0; i < 7; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 31);
-  a[7] = (a[7] >> 1) | top;
 }
 CDEV void mp8_neg(uint32_t a[8]) {
   uint64_t c = 1;
@@ -364,28 +344,62 @@ CDEV int mp8_absbits(const uint32_t a[8]) {
   return mp8_bitlen(t);
 }
 
-// rp <- rp mod rc,  tp <- tp - (rp div rc) * tc   (bit-serial long division;
-// Euclid's partial quotients are small: ~1.7 quotient bits per step)
-CDEV void euclid_divstep(uint32_t rp[8], const uint32_t rc[8], uint32_t tp[8], const uint32_t tc[8]) {
-  uint32_t T[8], Tt[8];
-  mp8_copy(T, rc);
-  mp8_copy(Tt, tc);
-  int k = 0;
-  while (true) {
-    uint32_t T2[8];
-    const uint32_t c = mp8_shl1(T2, T);
-    if (c || !mp8_ge(rp, T2)) break;
-    mp8_copy(T, T2);
-    mp8_shl1(Tt, Tt);
-    k++;
+// value of an 8-word integer as a double (relative error < 2^-49)
+CDEV double mp8_f64(const uint32_t a[8]) {
+  double d = (double)a[7];
+#pragma unroll
+  for (int i = 6; i >= 0; i--) d = fma(d, 4294967296.0, (double)a[i]);
+  return d;
+}
+// a -= q * b  (mod 2^256), q < 2^32
+CDEV void mp8_submul(uint32_t a[8], const uint32_t b[8], uint32_t q) {
+  uint64_t pc = 0;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t p = (uint64_t)q * b[i] + pc;
+    pc = p >> 32;
+    const uint64_t d = (uint64_t)a[i] - (uint32_t)p - br;
+    a[i] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
   }
-  for (; k >= 0; k--) {
-    if (mp8_ge(rp, T)) {
-      mp8_sub(rp, T);
-      mp8_sub(tp, Tt);
+}
+// o = b << k  (mod 2^256), 0 <= k < 256
+CDEV void mp8_shl_dyn(uint32_t o[8], const uint32_t b[8], int k) {
+  const int ws = k >> 5, bs = k & 31;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t lo = (i - ws >= 0) ? word_sel(b, i - ws) : 0u;
+    const uint32_t lo2 = (i - ws - 1 >= 0) ? word_sel(b, i - ws - 1) : 0u;
+    o[i] = bs ? ((lo << bs) | (lo2 >> (32 - bs))) : lo;
+  }
+}
+
+// rp <- rp mod rc,  tp <- tp - (rp div rc) * tc   (mod 2^256), rc > 0.
+// The quotient comes from a double-precision estimate scaled down by
+// (1 - 2^-40): it never exceeds the true quotient (relative error of the
+// estimate < 2^-48), so rp stays non-negative, and the loop repeats until
+// rp < rc. Euclid's partial quotients are small (~1.7 bits per step), so one
+// pass is the rule; a quotient >= 2^32 is taken 31 bits at a time.
+CDEV void euclid_divstep(uint32_t rp[8], const uint32_t rc[8], uint32_t tp[8], const uint32_t tc[8]) {
+  const double inv = 1.0 / mp8_f64(rc);
+  while (mp8_ge(rp, rc)) {
+    const double qd = mp8_f64(rp) * inv * (1.0 - 0x1p-40);
+    if (qd < 4294967296.0) {
+      uint32_t q = (uint32_t)qd;
+      q = q ? q : 1u;
+      mp8_submul(rp, rc, q);
+      mp8_submul(tp, tc, q);
+    } else {
+      const int e = (int)((__double_as_longlong(qd) >> 52) & 0x7ff) - 1023;  // qd in [2^e, 2^(e+1))
+      const int k = e - 31;
+      const uint32_t q = (uint32_t)(qd * __longlong_as_double((long long)(1023 - k) << 52));  // qd / 2^k
+      uint32_t bs[8], ts[8];
+      mp8_shl_dyn(bs, rc, k);
+      mp8_shl_dyn(ts, tc, k);
+      mp8_submul(rp, bs, q);
+      mp8_submul(tp, ts, q);
     }
-    mp8_shr1(T, false);
-    mp8_shr1(Tt, true);
   }
 }
 
@@ -676,38 +690,74 @@ CDEV void load_cached(ge_cached& c, const uint32_t* __restrict__ p) {
   }
 }
 
-// lanes [base, base + m) of the batch; ws holds m records
-__global__ void __launch_bounds__(256) ed25519_prep_kernel(
+// stops the machine scheduler from interleaving the phases on either side
+// (independent phases interleaved = both phases' registers live at once)
+#define PHASE_BARRIER() __builtin_amdgcn_sched_barrier(0)
+
+CDEV void store_table9(uint32_t* __restrict__ rec, const ge_p3& base) {
+  ge_cached c;
+  fe_set(c.YpX, 1);
+  fe_set(c.YmX, 1);
+  fe_set(c.Z, 1);
+  fe_set(c.T2d, 0);
+  store_cached(rec, c);
+  ge_cached c1;
+  ge_to_cached(c1, base);
+  store_cached(rec + 40, c1);
+  ge_p3 Q;
+  ge_dbl<true>(Q, base);
+  ge_to_cached(c, Q);
+  store_cached(rec + 80, c);
+  for (int k = 3; k <= 8; k++) {
+    ge_add<true>(Q, Q, c1);
+    ge_to_cached(c, Q);
+    store_cached(rec + 40 * k, c);
+  }
+}
+
+CDEV void store8(uint32_t* __restrict__ o, const uint32_t v[8]) {
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+  o4[0] = make_uint4(v[0], v[1], v[2], v[3]);
+  o4[1] = make_uint4(v[4], v[5], v[6], v[7]);
+}
+CDEV void load8(uint32_t v[8], const uint32_t* __restrict__ p) {
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);
+  const uint4 a = p4[0], b = p4[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// lanes [base, base + m) of the batch; ws holds m records. Phases (see
+// PHASE_BARRIER): decode A -> table [k](-A) | SHA-512, h, S_eff.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_prep_kernel(
     const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
     uint32_t msg_len, uint64_t base, uint64_t m, const uint8_t* __restrict__ pre_status,
     uint8_t* __restrict__ status, uint32_t* __restrict__ ws) {
   const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= m) return;
   const uint64_t i = base + li;
-  const uint4* k4 = reinterpret_cast<const uint4*>(keys + i * 32);
-  const uint4* s4 = reinterpret_cast<const uint4*>(sigs + i * 64);
-  const uint4 ka = k4[0], kb = k4[1];
-  const uint32_t key[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
-  const uint4 r0 = s4[0], r1 = s4[1], q0 = s4[2], q1 = s4[3];
-  const uint32_t R[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-  const uint32_t S[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-  uint8_t st = kStatusPending;
-  ge_p3 A;
-  if (!ge_frombytes_i2p(A, key)) {  // i2p GroupElement(Curve, byte[]), before doVerify (Kryo.kt:389-392)
-    st = kStatusBadKey;
-    ge_identity(A);
-  } else if (pre_status && pre_status[i] != kStatusOk) {
-    st = pre_status[i];  // EMPTY / MALFORMED decided by the host
-  } else if (msg_len == 0) {
-    st = kStatusEmpty;  // Crypto.kt:476
-  }
   uint32_t* rec = ws + li * kWsLaneWords;
+  uint8_t st = kStatusPending;
+  uint32_t abyte[8];
+  {
+    uint32_t key[8];
+    load8(key, reinterpret_cast<const uint32_t*>(keys + i * 32));
+    ge_p3 A;
+    if (!ge_frombytes_i2p(A, key)) st = kStatusBadKey;  // i2p GroupElement(Curve, byte[]), before doVerify (Kryo.kt:389-392)
+    else if (pre_status && pre_status[i] != kStatusOk) st = pre_status[i];  // EMPTY / MALFORMED decided by the host
+    else if (msg_len == 0) st = kStatusEmpty;  // Crypto.kt:476
+    fe_tobytes(abyte, A.Y);  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
+    abyte[7] |= fe_isnegative(A.X) << 31;
+    if (st != kStatusPending) ge_identity(A);
+    fe_neg(A.X, A.X);
+    fe_neg(A.T, A.T);
+    store_table9(rec, A);  // [k](-A), k = 0..8
+  }
+  PHASE_BARRIER();
   uint32_t h[8], se[8];
   if (st == kStatusPending) {
-    uint32_t abyte[8];  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
-    fe_tobytes(abyte, A.Y);
-    abyte[7] |= fe_isnegative(A.X) << 31;
-    uint32_t hd[16];
+    uint32_t R[8], S[8], hd[16];
+    load8(R, reinterpret_cast<const uint32_t*>(sigs + i * 64));
+    load8(S, reinterpret_cast<const uint32_t*>(sigs + i * 64 + 32));
     sha512_segments(hd, R, abyte, true, msgs + i * (uint64_t)msg_len, msg_len);
     sc_reduce512(h, hd);
     sc_effective_S(se, S, slide_drops_carry(S));
@@ -716,33 +766,8 @@ __global__ void __launch_bounds__(256) ed25519_prep_kernel(
     for (int q = 0; q < 8; q++) h[q] = se[q] = 0;
   }
   status[i] = st;
-  // table [k](-A), k = 0..8
-  ge_p3 An = A;
-  fe_neg(An.X, A.X);
-  fe_neg(An.T, A.T);
-  ge_cached c;
-  fe_set(c.YpX, 1);
-  fe_set(c.YmX, 1);
-  fe_set(c.Z, 1);
-  fe_set(c.T2d, 0);
-  store_cached(rec, c);
-  ge_cached c1;
-  ge_to_cached(c1, An);
-  store_cached(rec + 40, c1);
-  ge_p3 Q;
-  ge_dbl<true>(Q, An);
-  ge_to_cached(c, Q);
-  store_cached(rec + 80, c);
-  for (int k = 3; k <= 8; k++) {
-    ge_add<true>(Q, Q, c1);
-    ge_to_cached(c, Q);
-    store_cached(rec + 40 * k, c);
-  }
-  uint4* o4 = reinterpret_cast<uint4*>(rec + kWsH);
-  o4[0] = make_uint4(h[0], h[1], h[2], h[3]);
-  o4[1] = make_uint4(h[4], h[5], h[6], h[7]);
-  o4[2] = make_uint4(se[0], se[1], se[2], se[3]);
-  o4[3] = make_uint4(se[4], se[5], se[6], se[7]);
+  store8(rec + kWsH, h);
+  store8(rec + kWsS, se);
 }
 
 CDEV void lds_niels(ge_niels& n, const uint32_t* lds, int idx) {
@@ -833,72 +858,59 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
 // Split half-size-scalar verification: same prep/ladder split, ladder over
 // [e]B + [c0](+-A) + [c1](-R) with ~128-bit c0, c1 (see half_scalars): 128
 // doublings instead of 252 and no final inversion (P == O is X == 0, Y == Z).
-static constexpr int kWhTabA = 0;                            // [0..8](+-A)
+static constexpr int kWhTabA = 0;                            // [0..8](-A)
 static constexpr int kWhTabR = 9 * 40;                       // [0..8](-R)
 static constexpr int kWhKa = 18 * 40;                        // |c0|, c1, e (8 words each)
 static constexpr int kWhKr = kWhKa + 8;
 static constexpr int kWhE = kWhKa + 16;
-static constexpr int kWhLaneWords = kWhKa + 24;              // 744 words = 2976 B
+static constexpr int kWhFlags = kWhKa + 24;                  // bit 0: c0 < 0
+static constexpr int kWhLaneWords = kWhKa + 28;              // 748 words = 2992 B (16-B multiple)
 
-CDEV void store_table9(uint32_t* __restrict__ rec, const ge_p3& base) {
-  ge_cached c;
-  fe_set(c.YpX, 1);
-  fe_set(c.YmX, 1);
-  fe_set(c.Z, 1);
-  fe_set(c.T2d, 0);
-  store_cached(rec, c);
-  ge_cached c1;
-  ge_to_cached(c1, base);
-  store_cached(rec + 40, c1);
-  ge_p3 Q;
-  ge_dbl<true>(Q, base);
-  ge_to_cached(c, Q);
-  store_cached(rec + 80, c);
-  for (int k = 3; k <= 8; k++) {
-    ge_add<true>(Q, Q, c1);
-    ge_to_cached(c, Q);
-    store_cached(rec + 40 * k, c);
-  }
-}
-
-CDEV void store8(uint32_t* __restrict__ o, const uint32_t v[8]) {
-  uint4* o4 = reinterpret_cast<uint4*>(o);
-  o4[0] = make_uint4(v[0], v[1], v[2], v[3]);
-  o4[1] = make_uint4(v[4], v[5], v[6], v[7]);
-}
-CDEV void load8(uint32_t v[8], const uint32_t* __restrict__ p) {
-  const uint4* p4 = reinterpret_cast<const uint4*>(p);
-  const uint4 a = p4[0], b = p4[1];
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-
-__global__ void __launch_bounds__(256) ed25519_prep_half_kernel(
+// Phases, each finished (and its table written to the workspace) before the
+// next starts: decode A -> table [k](-A) | strict decode R -> table [k](-R) |
+// SHA-512, h, S_eff, lattice reduction, e = c1 S_eff mod L. Lanes whose
+// status is already decided run the phases on the identity / zero scalars.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_prep_half_kernel(
     const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
     uint32_t msg_len, uint64_t base, uint64_t m, const uint8_t* __restrict__ pre_status,
     uint8_t* __restrict__ status, uint32_t* __restrict__ ws) {
   const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= m) return;
   const uint64_t i = base + li;
-  const uint4* k4 = reinterpret_cast<const uint4*>(keys + i * 32);
-  const uint4* s4 = reinterpret_cast<const uint4*>(sigs + i * 64);
-  const uint4 ka4 = k4[0], kb4 = k4[1];
-  const uint32_t key[8] = {ka4.x, ka4.y, ka4.z, ka4.w, kb4.x, kb4.y, kb4.z, kb4.w};
-  const uint4 r0 = s4[0], r1 = s4[1], q0 = s4[2], q1 = s4[3];
-  const uint32_t Rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-  const uint32_t S[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+  uint32_t* rec = ws + li * kWhLaneWords;
   uint8_t st = kStatusPending;
-  ge_p3 A, R;
-  if (!ge_frombytes_i2p(A, key)) st = kStatusBadKey;  // key decode precedes doVerify (Kryo.kt:389-392)
-  else if (pre_status && pre_status[i] != kStatusOk) st = pre_status[i];
-  else if (msg_len == 0) st = kStatusEmpty;  // Crypto.kt:476
-  else if (!ge_frombytes_strict(R, Rw)) st = kStatusBadSig;  // no canonical point encodes to these bytes
+  uint32_t abyte[8];
+  {
+    uint32_t key[8];
+    load8(key, reinterpret_cast<const uint32_t*>(keys + i * 32));
+    ge_p3 A;
+    if (!ge_frombytes_i2p(A, key)) st = kStatusBadKey;  // key decode precedes doVerify (Kryo.kt:389-392)
+    else if (pre_status && pre_status[i] != kStatusOk) st = pre_status[i];
+    else if (msg_len == 0) st = kStatusEmpty;  // Crypto.kt:476
+    fe_tobytes(abyte, A.Y);  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
+    abyte[7] |= fe_isnegative(A.X) << 31;
+    if (st != kStatusPending) ge_identity(A);
+    fe_neg(A.X, A.X);
+    fe_neg(A.T, A.T);
+    store_table9(rec + kWhTabA, A);
+  }
+  PHASE_BARRIER();
+  uint32_t Rw[8];
+  load8(Rw, reinterpret_cast<const uint32_t*>(sigs + i * 64));
+  {
+    ge_p3 R;
+    if (st == kStatusPending && !ge_frombytes_strict(R, Rw)) st = kStatusBadSig;  // no canonical point encodes to Rw
+    if (st != kStatusPending) ge_identity(R);
+    fe_neg(R.X, R.X);
+    fe_neg(R.T, R.T);
+    store_table9(rec + kWhTabR, R);
+  }
+  PHASE_BARRIER();
   uint32_t ka[8], kr[8], e[8];
   bool c0neg = false;
   if (st == kStatusPending) {
-    uint32_t abyte[8];  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
-    fe_tobytes(abyte, A.Y);
-    abyte[7] |= fe_isnegative(A.X) << 31;
-    uint32_t hd[16], h[8], se[8], zero[8];
+    uint32_t S[8], hd[16], h[8], se[8], zero[8];
+    load8(S, reinterpret_cast<const uint32_t*>(sigs + i * 64 + 32));
     sha512_segments(hd, Rw, abyte, true, msgs + i * (uint64_t)msg_len, msg_len);
     sc_reduce512(h, hd);
     sc_effective_S(se, S, slide_drops_carry(S));
@@ -909,23 +921,12 @@ __global__ void __launch_bounds__(256) ed25519_prep_half_kernel(
   } else {
 #pragma unroll
     for (int q = 0; q < 8; q++) ka[q] = kr[q] = e[q] = 0;
-    ge_identity(A);
-    ge_identity(R);
   }
   status[i] = st;
-  // [e]B + [c0](-A) + [c1](-R): -A when c0 > 0, A when c0 < 0; always -R
-  if (!c0neg) {
-    fe_neg(A.X, A.X);
-    fe_neg(A.T, A.T);
-  }
-  fe_neg(R.X, R.X);
-  fe_neg(R.T, R.T);
-  uint32_t* rec = ws + li * kWhLaneWords;
-  store_table9(rec + kWhTabA, A);
-  store_table9(rec + kWhTabR, R);
   store8(rec + kWhKa, ka);
   store8(rec + kWhKr, kr);
   store8(rec + kWhE, e);
+  reinterpret_cast<uint4*>(rec + kWhFlags)[0] = make_uint4(c0neg ? 1u : 0u, 0u, 0u, 0u);
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_ladder_half_kernel(
@@ -945,6 +946,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
   load8(ka, rec + kWhKa);
   load8(kr, rec + kWhKr);
   load8(e, rec + kWhE);
+  const bool c0neg = rec[kWhFlags] & 1u;  // [c0](-A) with c0 < 0 is [|c0|]A: flip the digit signs
   const int bits = max(mp8_bitlen(ka), mp8_bitlen(kr));
   const int W = max(wave_max((bits + 1 + 3) / 4), 1);
   const uint32_t* bl128 = bl + kBTableEntries * kLdsBStride;
@@ -961,7 +963,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
       ge_dbl<false>(P, P);
       ge_dbl<true>(P, P);
     }
-    cached_cneg(ca, da < 0);
+    cached_cneg(ca, (da < 0) != c0neg);
     ge_add<true>(P, P, ca);
     cached_cneg(cr, dr < 0);
     if ((j & 1) == 0 && j < 32) {
@@ -1109,8 +1111,9 @@ hipError_t launch_ed25519_btable(uint32_t* tab, hipStream_t s) {
 size_t ed25519_btable_bytes() { return 2 * (size_t)kBTableEntries * kBEntryWords * sizeof(uint32_t); }
 
 // CORDAHIP_ED25519_LADDER selects the verification kernels (all bit-exact):
-//   split (default): prep + ladder kernels over a per-lane HBM workspace
-//   split-half     : the same split with the half-size-scalar ladder
+//   split-half (default): prep + ladder kernels over a per-lane HBM workspace,
+//                   half-size-scalar ladder (~132 doublings)
+//   split          : the same split with the full 252-doubling ladder
 //   fused          : one kernel, full 252-doubling ladder (round-1 baseline)
 //   half           : one kernel, half-size-scalar ladder
 // profiles/r01_bench_c2_ab.json holds the A/B measurements.
@@ -1118,12 +1121,12 @@ enum class Ladder { kSplit, kSplitHalf, kFused, kHalf };
 static Ladder ladder_mode() {
   static const Ladder m = [] {
     const char* v = getenv("CORDAHIP_ED25519_LADDER");
-    if (!v) return Ladder::kSplit;
+    if (!v) return Ladder::kSplitHalf;
     const std::string s(v);
-    if (s == "split-half") return Ladder::kSplitHalf;
+    if (s == "split") return Ladder::kSplit;
     if (s == "half") return Ladder::kHalf;
     if (s == "fused") return Ladder::kFused;
-    return Ladder::kSplit;
+    return Ladder::kSplitHalf;
   }();
   return m;
 }

@@ -120,13 +120,65 @@ CDEV void fe_carry64(fe& r, uint64_t h[10]) {
   for (int i = 0; i < 10; i++) r.v[i] = (uint32_t)h[i];
 }
 
+// Carry-chained column reduction (default, FE_CARRY_CHAIN != 0): column k's
+// 64-bit accumulator STARTS at the carry out of column k-1, so the carry
+// costs no add (it rides in v_mad_u64_u32's 64-bit addend) — one shift and
+// one mask per limb, plus one fold of 19 * carry(limb 9) into limbs 0/1.
+// Bounds: column sums < 2^62.5 plus a carry < 2^38; the final carry c < 2^38,
+// 19c < 2^42.3, so limb 1 grows by < 2^16.4 -> output tight.
+#ifndef FE_CARRY_CHAIN
+#define FE_CARRY_CHAIN 1
+#endif
+
+// 19 * x, opaque to LLVM: with a visible constant factor InstCombine
+// factors sums of wrapped products as 19 * (64-bit sum), which costs a 64x32
+// multiply per column instead of one 32-bit multiply per limb.
+CDEV uint32_t mul19(uint32_t x) {
+  uint32_t r;
+  asm("v_mul_lo_u32 %0, %1, 19" : "=v"(r) : "v"(x));
+  return r;
+}
+
+CDEV void fe_fold_top(fe& r, uint64_t c) {
+  const uint64_t t = (uint64_t)r.v[0] + c * 19u;
+  r.v[0] = (uint32_t)t & M26;
+  r.v[1] += (uint32_t)(t >> 26);
+}
+
 // h = f * g. Column k collects f_i g_j with i + j == k (mod 10); wrapped
 // terms carry 2^255 == 19, and odd*odd terms carry an extra 2 (radix 2^25.5).
 CDEV void fe_mul(fe& r, const fe& f, const fe& g) {
+#if FE_CARRY_CHAIN
   uint32_t g19[10], f2[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    g19[i] = g.v[i] * 19u;
+    g19[i] = mul19(g.v[i]);
+    f2[i] = f.v[i] << 1;
+  }
+  fe o;
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    uint64_t acc = c;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const int j = (k - i + 10) % 10;
+      const bool wrap = (i + j) >= 10;
+      const bool oo = (i & 1) && (j & 1);
+      const uint32_t a = oo ? f2[i] : f.v[i];
+      const uint32_t b = wrap ? g19[j] : g.v[j];
+      acc += (uint64_t)a * b;
+    }
+    o.v[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
+    c = acc >> limb_bits(k);
+  }
+  fe_fold_top(o, c);
+  r = o;  // r may alias f or g
+#else
+  uint32_t g19[10], f2[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    g19[i] = mul19(g.v[i]);
     f2[i] = f.v[i] << 1;
   }
   uint64_t h[10];
@@ -145,6 +197,7 @@ CDEV void fe_mul(fe& r, const fe& f, const fe& g) {
     h[k] = acc;
   }
   fe_carry64(r, h);
+#endif
 }
 
 // h = f^2 (55 products)
@@ -154,8 +207,31 @@ CDEV void fe_sq(fe& r, const fe& f) {
   for (int i = 0; i < 10; i++) {
     f2[i] = f.v[i] << 1;
     f4[i] = f.v[i] << 2;
-    f19[i] = f.v[i] * 19u;
+    f19[i] = mul19(f.v[i]);
   }
+#if FE_CARRY_CHAIN
+  fe o;
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    uint64_t acc = c;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const int j = (k - i + 10) % 10;
+      if (j < i) continue;
+      const bool wrap = (i + j) >= 10;
+      const bool oo = (i & 1) && (j & 1);
+      const int mult = (i < j ? 2 : 1) * (oo ? 2 : 1);  // 1, 2 or 4
+      const uint32_t a = mult == 1 ? f.v[i] : (mult == 2 ? f2[i] : f4[i]);
+      const uint32_t b = wrap ? f19[j] : f.v[j];
+      acc += (uint64_t)a * b;
+    }
+    o.v[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
+    c = acc >> limb_bits(k);
+  }
+  fe_fold_top(o, c);
+  r = o;  // r may alias f or g
+#else
   uint64_t h[10];
 #pragma unroll
   for (int k = 0; k < 10; k++) {
@@ -174,10 +250,14 @@ CDEV void fe_sq(fe& r, const fe& f) {
     h[k] = acc;
   }
   fe_carry64(r, h);
+#endif
 }
 
+// n squarings, kept as a loop: a fully unrolled chain lets the scheduler
+// interleave successive squarings and blows the register budget.
 CDEV void fe_sqn(fe& r, const fe& a, int n) {
   fe_sq(r, a);
+#pragma unroll 1
   for (int i = 1; i < n; i++) fe_sq(r, r);
 }
 
