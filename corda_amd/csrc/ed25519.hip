@@ -299,14 +299,13 @@ CDEV uint8_t ed25519_verify_lane(const uint32_t key[8], const uint32_t sig[16], 
 // stopped below sqrt(8L), gives |c0|, |c1| ~ 2^128: the ladder needs ~128
 // doublings instead of ~252 (idea: T. Pornin, ePrint 2020/454). The
 // equivalence is checked on the golden catalogue in tools/proto/half_scalar.py.
+// a >= b as the absence of a borrow out of a - b (branch-free: a
+// short-circuit word compare becomes divergent control flow on the GPU)
 CDEV bool mp8_ge(const uint32_t a[8], const uint32_t b[8]) {
-  bool gt = false, eq = true;
+  uint32_t br = 0;
 #pragma unroll
-  for (int i = 7; i >= 0; i--) {
-    gt = gt || (eq && a[i] > b[i]);
-    eq = eq && (a[i] == b[i]);
-  }
-  return gt || eq;
+  for (int i = 0; i < 8; i++) br = (uint32_t)(((uint64_t)a[i] - b[i] - br) >> 63);
+  return br == 0;
 }
 CDEV void mp8_add(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
   uint64_t c = 0;
@@ -415,16 +414,23 @@ CDEV void half_scalars(uint32_t c0abs[8], bool& c0neg, uint32_t c1[8], const uin
     tp[i] = 0;
     tc[i] = i == 0;
   }
+  // Euclid, unrolled by two so the remainders never move between registers:
+  // stop at the first remainder below sqrt(8L); (rc, tc) <- that remainder's
+  // vector, (rp, tp) <- the previous one.
   while (mp8_ge(rc, kS)) {
-    euclid_divstep(rp, rc, tp, tc);
+    euclid_divstep(rp, rc, tp, tc);  // rp <- rp mod rc
+    if (!mp8_ge(rp, kS)) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const uint32_t a = rp[i], b = tp[i];
-      rp[i] = rc[i];
-      rc[i] = a;
-      tp[i] = tc[i];
-      tc[i] = b;
+      for (int i = 0; i < 8; i++) {
+        const uint32_t a = rp[i], b = tp[i];
+        rp[i] = rc[i];
+        rc[i] = a;
+        tp[i] = tc[i];
+        tc[i] = b;
+      }
+      break;
     }
+    euclid_divstep(rc, rp, tc, tp);  // rc <- rc mod rp
   }
   uint32_t a0[8], a1[8];  // chosen (c0, c1), two's complement
   mp8_copy(a0, rc);
@@ -472,6 +478,14 @@ CDEV void half_scalars(uint32_t c0abs[8], bool& c0neg, uint32_t c1[8], const uin
 // Strict R decode: the reference never decodes R, it compares encode(R')
 // with the 32 bytes; those equal only when the bytes are the canonical
 // encoding of a curve point: y < p, on the curve, not (x == 0 with bit 255).
+// the extra conditions of a strict decode, given R = ge_frombytes_i2p(w) succeeded
+CDEV bool ge_strict_ok(const ge_p3& R, const uint32_t w[8]) {
+  uint32_t all_ones = (w[7] & 0x7fffffffu) == 0x7fffffffu;
+#pragma unroll
+  for (int i = 1; i < 7; i++) all_ones &= (w[i] == 0xffffffffu);
+  if (all_ones && w[0] >= 0xffffffedu) return false;  // y >= p
+  return !((w[7] >> 31) && fe_iszero(R.X));
+}
 CDEV bool ge_frombytes_strict(ge_p3& R, const uint32_t w[8]) {
   bool all_ones = (w[7] & 0x7fffffffu) == 0x7fffffffu;
 #pragma unroll
@@ -879,33 +893,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
   const uint64_t i = base + li;
   uint32_t* rec = ws + li * kWhLaneWords;
   uint8_t st = kStatusPending;
-  uint32_t abyte[8];
-  {
-    uint32_t key[8];
-    load8(key, reinterpret_cast<const uint32_t*>(keys + i * 32));
-    ge_p3 A;
-    if (!ge_frombytes_i2p(A, key)) st = kStatusBadKey;  // key decode precedes doVerify (Kryo.kt:389-392)
-    else if (pre_status && pre_status[i] != kStatusOk) st = pre_status[i];
-    else if (msg_len == 0) st = kStatusEmpty;  // Crypto.kt:476
-    fe_tobytes(abyte, A.Y);  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
-    abyte[7] |= fe_isnegative(A.X) << 31;
-    if (st != kStatusPending) ge_identity(A);
-    fe_neg(A.X, A.X);
-    fe_neg(A.T, A.T);
-    store_table9(rec + kWhTabA, A);
-  }
-  PHASE_BARRIER();
-  uint32_t Rw[8];
+  uint32_t abyte[8], Rw[8];
   load8(Rw, reinterpret_cast<const uint32_t*>(sigs + i * 64));
-  {
-    ge_p3 R;
-    if (st == kStatusPending && !ge_frombytes_strict(R, Rw)) st = kStatusBadSig;  // no canonical point encodes to Rw
-    if (st != kStatusPending) ge_identity(R);
-    fe_neg(R.X, R.X);
-    fe_neg(R.T, R.T);
-    store_table9(rec + kWhTabR, R);
+  // pass 0: A (i2p decode: y not range checked), pass 1: R (strict decode:
+  // encode(R') == Rw only if Rw is a canonical point encoding). One loop body
+  // keeps a single copy of the decompression + table code in the I-cache.
+#pragma unroll 1
+  for (int pass = 0; pass < 2; pass++) {
+    uint32_t w[8];
+    if (pass == 0) load8(w, reinterpret_cast<const uint32_t*>(keys + i * 32));
+    else mp8_copy(w, Rw);
+    ge_p3 P;
+    const bool ok = ge_frombytes_i2p(P, w);
+    if (pass == 0) {
+      if (!ok) st = kStatusBadKey;  // key decode precedes doVerify (Kryo.kt:389-392)
+      else if (pre_status && pre_status[i] != kStatusOk) st = pre_status[i];
+      else if (msg_len == 0) st = kStatusEmpty;  // Crypto.kt:476
+      fe_tobytes(abyte, P.Y);  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
+      abyte[7] |= fe_isnegative(P.X) << 31;
+    } else if (st == kStatusPending && !(ok && ge_strict_ok(P, w))) {
+      st = kStatusBadSig;  // no canonical point encodes to Rw
+    }
+    if (st != kStatusPending) ge_identity(P);
+    fe_neg(P.X, P.X);
+    fe_neg(P.T, P.T);
+    store_table9(rec + (pass ? kWhTabR : kWhTabA), P);
+    PHASE_BARRIER();
   }
-  PHASE_BARRIER();
   uint32_t ka[8], kr[8], e[8];
   bool c0neg = false;
   if (st == kStatusPending) {

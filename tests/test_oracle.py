@@ -90,6 +90,46 @@ def test_slide_c_vs_python(oracle):
         assert dropped == (ed.slide_value(ab) != a)
 
 
+def _slide_drops_n(s: int, n: int) -> bool:
+    """ed.slide()'s recoding at width n (256 in i2p): does a carry run past bit n-1?"""
+    r = [(s >> i) & 1 for i in range(n)]
+    for i in range(n):
+        if r[i]:
+            b = 1
+            while b <= 6 and i + b < n:
+                if r[i + b]:
+                    if r[i] + (r[i + b] << b) <= 15:
+                        r[i] += r[i + b] << b
+                        r[i + b] = 0
+                    elif r[i] - (r[i + b] << b) >= -15:
+                        r[i] -= r[i + b] << b
+                        for k in range(i + b, n + 1):
+                            if k == n:
+                                return True
+                            if not r[k]:
+                                r[k] = 1
+                                break
+                            r[k] = 0
+                    else:
+                        break
+                b += 1
+    return False
+
+
+def test_slide_drop_needs_top_bit():
+    """The K1 kernels skip the slide() emulation when bit 255 of S is clear
+    (sc25519.hpp slide_drops_carry). Pinned here: exhaustively over every S at
+    widths 8..15, a carry is dropped only when the top bit is set (and the
+    width-256 recoding agrees with ed.slide on random S)."""
+    for n in range(8, 16):
+        assert not any(_slide_drops_n(s, n) for s in range(1 << (n - 1))), n
+        assert any(_slide_drops_n(s, n) for s in range(1 << (n - 1), 1 << n)), n
+    rng = random.Random(12)
+    for _ in range(200):
+        a = rng.getrandbits(256)
+        assert _slide_drops_n(a, 256) == (ed.slide_value(a.to_bytes(32, "little")) != a)
+
+
 def _merkle_py(leaves):
     """MerkleTree.kt:27-66 restated in Python (independent of oracle/c)."""
     if not leaves:

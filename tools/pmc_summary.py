@@ -1,0 +1,20 @@
+"""Sum rocprofv3 counter_collection.csv rows per (kernel, counter) -> JSON (dev tool)."""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+tot = defaultdict(lambda: defaultdict(float))
+disp = defaultdict(set)
+for path in sys.argv[1:]:
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0]
+        tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add((path, r["Dispatch_Id"]))
+out = {}
+for k, c in tot.items():
+    if not k.startswith("cordahip::") and "cordahip" not in k:
+        continue
+    out[k] = dict(c)
+    out[k]["dispatches_per_pass"] = len(disp[k]) / max(1, len(sys.argv) - 1)
+print(json.dumps(out, indent=1))
