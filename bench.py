@@ -51,8 +51,10 @@ def _cores():
 
 # ---- C2: Ed25519 ---------------------------------------------------------------
 class C2:
-    kernel = "ed25519_verify_kernel"
-    pmc = "r01_pmc_ed25519_verify.json"
+    # one step = the split verification pass: prep (decode A/R, SHA-512, lattice
+    # reduction -> per-lane workspace) + ladder, one launch pair per 2^20 lanes
+    kernel = "ed25519_prep_half_kernel + ed25519_ladder_half_kernel"
+    pmc = "r01_pmc_ed25519_split.json"
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -176,8 +178,8 @@ class C3:
 
 # ---- C4: SignedTransaction.verifySignatures on cash-issue transactions --------
 class C4:
-    kernel = "ed25519_verify_kernel"
-    pmc = "r01_pmc_ed25519_verify.json"
+    kernel = "sha256_leaves + merkle_root + ed25519 prep/ladder + tx_reduce"
+    pmc = "r01_pmc_c4.json"
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -347,11 +349,14 @@ def main():
     if rank == 0:
         value = world * wl.units * args.steps / elapsed
         achieved = wl.macs * wl.units / (kernel_ms * 1e-3) / 1e12
+        # HBM bytes per step from the committed PMC passes (tools/gpu_pmc.sh:
+        # FETCH_SIZE and WRITE_SIZE in separate passes), scaled to this step
         traffic = None
         pmc_file = os.path.join(ROOT, "profiles", wl.pmc)
         if os.path.exists(pmc_file):
             with open(pmc_file) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                per_unit = json.load(f).get("hbm_bytes_per_unit")
+            traffic = per_unit * wl.units if per_unit else None
         out = {
             "metric": METRIC,
             "value": value,

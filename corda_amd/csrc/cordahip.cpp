@@ -51,7 +51,8 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
                                const uint64_t* msg_off, uint32_t msg_len, uint64_t n, const uint32_t* gk1,
                                const uint32_t* gr1, const uint8_t* pre_status, uint8_t* status,
                                unsigned long long* verdict, unsigned int* counters6, unsigned int* perm,
-                               hipStream_t s);
+                               uint32_t* ws, uint64_t ws_slots, hipStream_t s);
+size_t ecdsa_ws_slot_bytes();
 hipError_t launch_ecdsa_sign(const uint8_t* scheme, const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len,
                              uint64_t n, const uint32_t* gk1, const uint32_t* gr1, uint8_t* keys, uint8_t* key_len,
                              uint8_t* sigs, uint8_t* sig_len, hipStream_t s);
@@ -90,6 +91,8 @@ struct TxWork {  // device buffers of the transaction paths (grow-only)
 
 struct EcWork {  // device buffers of the ECDSA paths (grow-only)
   DevBuf scheme, keys, key_len, sigs, sig_len, msgs, msg_off, pre, status, counters, perm;
+  DevBuf ws;                 // split-kernel workspace (kEcWsSlots records)
+  hipEvent_t ev = nullptr;   // last enqueued user of counters/perm/ws (cross-stream reuse)
 };
 
 struct Device {
@@ -115,6 +118,34 @@ struct Device {
 };
 
 constexpr uint64_t kEdWsLanes = 1ull << 20;  // 3.1 GB of workspace per device
+constexpr uint64_t kEcWsSlots = 1ull << 20;  // 0.9 GB of ECDSA workspace per device
+
+// Enqueue ECDSA verification of n slot-layout lanes on stream s (device current,
+// d.ec_mu held): the shared work buffers are reused only after their previous
+// user's kernels (on whatever stream) have finished.
+hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
+                             const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs, const uint64_t* msg_off,
+                             uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
+                             unsigned long long* verdict, hipStream_t s) {
+  EcWork& w = d.ec;
+  const uint64_t slots = std::min<uint64_t>(kEcWsSlots, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
+  if (w.ws.cap < slots * ecdsa_ws_slot_bytes() || w.perm.cap < std::max<uint64_t>(n, 1) * 4) {
+    hipError_t e = w.ev ? hipEventSynchronize(w.ev) : hipSuccess;  // a smaller buffer may still be in use
+    if (e != hipSuccess) return e;
+    if (w.ws.ensure(std::max<uint64_t>(slots, kEcWsSlots / 16) * ecdsa_ws_slot_bytes()) ||
+        w.perm.ensure(std::max<uint64_t>(n, 1) * 4))
+      return hipErrorOutOfMemory;
+  }
+  if (w.counters.ensure(64)) return hipErrorOutOfMemory;
+  if (!w.ev && hipEventCreateWithFlags(&w.ev, hipEventDisableTiming) != hipSuccess) return hipErrorUnknown;
+  hipError_t e = hipStreamWaitEvent(s, w.ev, 0);
+  e = e ? e
+        : launch_ecdsa_verify(scheme, keys, key_len, sigs, sig_len, msgs, msg_off, msg_len, n, d.gtab_k1, d.gtab_r1,
+                              pre, status, verdict, w.counters.as<unsigned int>(), w.perm.as<unsigned int>(),
+                              w.ws.as<uint32_t>(), w.ws.cap / ecdsa_ws_slot_bytes() / 64 * 64, s);
+  e = e ? e : hipEventRecord(w.ev, s);
+  return e;
+}
 
 // Enqueue Ed25519 verification of n dense lanes on stream s (device already current).
 hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
@@ -265,11 +296,12 @@ int ecdsa_host_lanes(cordahip_ctx* ctx, const cordahip_sig_batch* b, const std::
   std::lock_guard<std::mutex> g(d.ec_mu);
   if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
   EcWork& w = d.ec;
+  hipStream_t s = d.stream;
+  if (w.ev && hipEventSynchronize(w.ev) != hipSuccess) return CORDAHIP_ERR_HIP;  // staging buffers below are shared
   if (w.scheme.ensure(m) || w.keys.ensure(m * 65) || w.key_len.ensure(m) || w.sigs.ensure(m * 72) ||
       w.sig_len.ensure(m) || w.msgs.ensure(msgs.size()) || w.msg_off.ensure((m + 1) * 8) || w.pre.ensure(m) ||
-      w.status.ensure(m) || w.counters.ensure(64) || w.perm.ensure(m * 4))
+      w.status.ensure(m))
     return CORDAHIP_ERR_OUT_OF_MEMORY;
-  hipStream_t s = d.stream;
   hipError_t e = hipMemcpyAsync(w.scheme.p, sch.data(), m, hipMemcpyHostToDevice, s);
   e = e ? e : hipMemcpyAsync(w.keys.p, keys.data(), m * 65, hipMemcpyHostToDevice, s);
   e = e ? e : hipMemcpyAsync(w.key_len.p, klen.data(), m, hipMemcpyHostToDevice, s);
@@ -279,11 +311,9 @@ int ecdsa_host_lanes(cordahip_ctx* ctx, const cordahip_sig_batch* b, const std::
   e = e ? e : hipMemcpyAsync(w.msg_off.p, moff.data(), (m + 1) * 8, hipMemcpyHostToDevice, s);
   e = e ? e : hipMemcpyAsync(w.pre.p, pre.data(), m, hipMemcpyHostToDevice, s);
   e = e ? e
-        : launch_ecdsa_verify(w.scheme.as<uint8_t>(), w.keys.as<uint8_t>(), w.key_len.as<uint8_t>(),
-                              w.sigs.as<uint8_t>(), w.sig_len.as<uint8_t>(), w.msgs.as<uint8_t>(),
-                              w.msg_off.as<uint64_t>(), 0, m, d.gtab_k1, d.gtab_r1, w.pre.as<uint8_t>(),
-                              w.status.as<uint8_t>(), nullptr, w.counters.as<unsigned int>(),
-                              w.perm.as<unsigned int>(), s);
+        : ec_verify_enqueue(d, w.scheme.as<uint8_t>(), w.keys.as<uint8_t>(), w.key_len.as<uint8_t>(),
+                            w.sigs.as<uint8_t>(), w.sig_len.as<uint8_t>(), w.msgs.as<uint8_t>(), w.msg_off.as<uint64_t>(),
+                            0, m, w.pre.as<uint8_t>(), w.status.as<uint8_t>(), nullptr, s);
   e = e ? e : hipMemcpyAsync(st.data(), w.status.p, m, hipMemcpyDeviceToHost, s);
   e = e ? e : hipStreamSynchronize(s);
   if (e != hipSuccess) return CORDAHIP_ERR_HIP;
@@ -512,8 +542,9 @@ void cordahip_shutdown(cordahip_ctx* ctx) {
                       &d->tx.tx_status, &d->tx.tx_sig_off, &d->tx.msgs})
       if (b->p) (void)hipFree(b->p);
     for (DevBuf* b : {&d->ec.scheme, &d->ec.keys, &d->ec.key_len, &d->ec.sigs, &d->ec.sig_len, &d->ec.msgs,
-                      &d->ec.msg_off, &d->ec.pre, &d->ec.status, &d->ec.counters, &d->ec.perm})
+                      &d->ec.msg_off, &d->ec.pre, &d->ec.status, &d->ec.counters, &d->ec.perm, &d->ec.ws})
       if (b->p) (void)hipFree(b->p);
+    if (d->ec.ev) (void)hipEventDestroy(d->ec.ev);
     if (d->gtab_k1) (void)hipFree(d->gtab_k1);
     if (d->gtab_r1) (void)hipFree(d->gtab_r1);
     if (d->btab) (void)hipFree(d->btab);
@@ -606,16 +637,14 @@ int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_sc
     return CORDAHIP_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(d->ec_mu);
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
-  if (d->ec.counters.ensure(64) || d->ec.perm.ensure(std::max<uint64_t>(n, 1) * 4)) return CORDAHIP_ERR_OUT_OF_MEMORY;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   hipError_t e = hipEventRecord(d->ev0, s);
   e = e ? e
-        : launch_ecdsa_verify(static_cast<const uint8_t*>(d_scheme), static_cast<const uint8_t*>(d_keys),
-                              static_cast<const uint8_t*>(d_key_len), static_cast<const uint8_t*>(d_sigs),
-                              static_cast<const uint8_t*>(d_sig_len), static_cast<const uint8_t*>(d_msgs), nullptr,
-                              msg_len, n, d->gtab_k1, d->gtab_r1, nullptr, static_cast<uint8_t*>(d_status),
-                              static_cast<unsigned long long*>(d_verdict), d->ec.counters.as<unsigned int>(),
-                              d->ec.perm.as<unsigned int>(), s);
+        : ec_verify_enqueue(*d, static_cast<const uint8_t*>(d_scheme), static_cast<const uint8_t*>(d_keys),
+                            static_cast<const uint8_t*>(d_key_len), static_cast<const uint8_t*>(d_sigs),
+                            static_cast<const uint8_t*>(d_sig_len), static_cast<const uint8_t*>(d_msgs), nullptr,
+                            msg_len, n, nullptr, static_cast<uint8_t*>(d_status),
+                            static_cast<unsigned long long*>(d_verdict), s);
   e = e ? e : hipEventRecord(d->ev1, s);
   return hip_err(e);
 }

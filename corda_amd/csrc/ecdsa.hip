@@ -15,6 +15,9 @@
 // diverges inside a wave except at the single boundary wave.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <string>
 
 #include "der.hpp"
 #include "mp256.hpp"
@@ -698,8 +701,255 @@ __global__ void __launch_bounds__(256) verdict_kernel(const uint8_t* __restrict_
   if ((threadIdx.x & 63) == 0 && i < n) verdict[i >> 6] = m;
 }
 
+// ---- split verification (default): prep -> batch inversion -> ladder --------
+// Slots are the curve-partitioned order (perm), processed in chunks of
+// ws_slots; each slot owns a 896-B workspace record in HBM.
+static constexpr int kEcTab = 0;             // [k]Q, k = 1..8: Jacobian X, Y, Z (Montgomery), 24 words each
+static constexpr int kEcS = 8 * 24;          // s, Montgomery form mod n (batch-inversion input)
+static constexpr int kEcW = kEcS + 8;        // prefix products, then w = s^-1 (Montgomery form mod n)
+static constexpr int kEcE = kEcW + 8;        // e = SHA-256(msg) mod n
+static constexpr int kEcR = kEcE + 8;        // r
+static constexpr int kEcWords = kEcR + 8;    // 224 words = 896 B
+static constexpr int kEcInvBatch = 16;       // signatures per thread in the batch inversion
+static constexpr uint8_t kEcPending = 0xff;  // slot whose verdict the ladder decides
+
+CDEV void st256(uint32_t* __restrict__ o, const u256& v) {
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+  o4[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+  o4[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+}
+CDEV void ld256(u256& v, const uint32_t* __restrict__ p) {
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);
+  const uint4 a = p4[0], b = p4[1];
+  v.v[0] = a.x; v.v[1] = a.y; v.v[2] = a.z; v.v[3] = a.w;
+  v.v[4] = b.x; v.v[5] = b.y; v.v[6] = b.z; v.v[7] = b.w;
+}
+CDEV void st_jpt(uint32_t* __restrict__ o, const jpt& p) {
+  st256(o, p.X);
+  st256(o + 8, p.Y);
+  st256(o + 16, p.Z);
+}
+CDEV void ld_jpt(jpt& p, const uint32_t* __restrict__ o) {
+  ld256(p.X, o);
+  ld256(p.Y, o + 8);
+  ld256(p.Z, o + 16);
+  p.inf = false;
+}
+
+// Everything before the scalar multiplication, in the reference's order (key
+// decode, Crypto.doVerify's require()s, DER, range checks), then e, s, r and
+// the [k]Q table go to the slot's record. Decided lanes store s = 1 so the
+// batch product stays invertible.
+template <class C>
+CDEV uint8_t ecdsa_prep_lane(const uint8_t* __restrict__ key, uint32_t key_len, const uint8_t* __restrict__ sig,
+                             uint32_t sig_len, const uint8_t* __restrict__ msg, uint64_t msg_len, uint8_t pre_status,
+                             uint32_t* __restrict__ rec) {
+  using N = typename C::N;
+  u256 sm;
+  {
+    u256 one;
+#pragma unroll
+    for (int q = 0; q < 8; q++) one.v[q] = q == 0;
+    to_mont<N>(sm, one);
+  }
+  jpt Q;
+  uint8_t st = kEcPending;
+  u256 r, s;
+  if (!decode_key<C>(Q, key, key_len)) {
+    st = kStatusBadKey;  // key built before verify
+  } else if (pre_status != kStatusOk) {
+    st = pre_status;
+  } else if (sig_len == 0 || msg_len == 0) {
+    st = kStatusEmpty;  // Crypto.kt:475-476
+  } else {
+    DerInt dr, ds;
+    if (!der_decode_sig(sig, sig_len, dr, ds)) {
+      st = kStatusMalformedSig;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        r.v[q] = dr.v[q];
+        s.v[q] = ds.v[q];
+      }
+      const u256 nm = mod_m<N>();
+      if (dr.neg || dr.big || ds.neg || ds.big || u256_iszero(r) || u256_iszero(s) || u256_geq(r, nm) ||
+          u256_geq(s, nm))
+        st = kStatusBadSig;
+    }
+  }
+  if (st == kEcPending) {
+    uint32_t hw[8];
+    sha256_bytes(hw, msg, msg_len);
+    u256 e, t;
+#pragma unroll
+    for (int q = 0; q < 8; q++) e.v[q] = hw[7 - q];
+    if (!u256_sub(t, e, mod_m<N>())) e = t;
+    to_mont<N>(sm, s);
+    st256(rec + kEcE, e);
+    st256(rec + kEcR, r);
+    st_jpt(rec + kEcTab, Q);
+    jpt T;
+    jdbl<C>(T, Q);
+    st_jpt(rec + kEcTab + 24, T);
+    for (int k = 3; k <= 8; k++) {
+      jadd<C>(T, T, Q);
+      st_jpt(rec + kEcTab + 24 * (k - 1), T);
+    }
+  }
+  st256(rec + kEcS, sm);
+  return st;
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ecdsa_prep_kernel(
+    const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, const uint8_t* __restrict__ keys,
+    const uint8_t* __restrict__ key_len, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ sig_len,
+    const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ msg_off, uint32_t msg_len, uint64_t base,
+    uint64_t m, const uint8_t* __restrict__ pre_status, uint8_t* __restrict__ status, uint32_t* __restrict__ ws) {
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= m) return;
+  const uint64_t slot = base + li;
+  const uint64_t i = perm ? perm[slot] : slot;
+  const uint8_t sch = scheme[i];
+  const uint8_t* key = keys + i * 65;
+  const uint8_t* sig = sigs + i * 72;
+  const uint8_t* msg = msg_off ? msgs + msg_off[i] : msgs + i * (uint64_t)msg_len;
+  const uint64_t ml = msg_off ? msg_off[i + 1] - msg_off[i] : msg_len;
+  const uint8_t pre = pre_status ? pre_status[i] : kStatusOk;
+  uint32_t* rec = ws + li * kEcWords;
+  uint8_t st;
+  if (sch == 2)
+    st = ecdsa_prep_lane<Curve<2>>(key, key_len[i], sig, sig_len[i], msg, ml, pre, rec);
+  else if (sch == 3)
+    st = ecdsa_prep_lane<Curve<3>>(key, key_len[i], sig, sig_len[i], msg, ml, pre, rec);
+  else
+    st = kStatusUnsupported;
+  status[i] = st;
+}
+
+// Montgomery's trick over chunk-relative slots [a, b) of one curve: prefix
+// products into W, ONE Fermat inversion, then back-substitution: every slot's
+// W becomes s^-1, at 3 multiplications per slot plus 1/(b-a) of an inversion.
+template <class C>
+CDEV void ecdsa_inv_run(uint32_t* __restrict__ ws, uint64_t a, uint64_t b) {
+  using N = typename C::N;
+  u256 acc, x;
+  ld256(acc, ws + a * kEcWords + kEcS);
+  st256(ws + a * kEcWords + kEcW, acc);
+  for (uint64_t j = a + 1; j < b; j++) {
+    ld256(x, ws + j * kEcWords + kEcS);
+    mont_mul<N>(acc, acc, x);
+    st256(ws + j * kEcWords + kEcW, acc);
+  }
+  u256 inv;
+  mont_pow_const<N, typename C::Nm2>(inv, acc);
+  for (uint64_t j = b - 1; j > a; j--) {
+    ld256(x, ws + (j - 1) * kEcWords + kEcW);
+    u256 wj;
+    mont_mul<N>(wj, inv, x);
+    st256(ws + j * kEcWords + kEcW, wj);
+    ld256(x, ws + j * kEcWords + kEcS);
+    mont_mul<N>(inv, inv, x);
+  }
+  st256(ws + a * kEcWords + kEcW, inv);
+}
+
+// kEcInvBatch consecutive slots per thread; curve runs from the partition
+// counts (slots [0, c1) secp256k1, [c1, c1 + c2) P-256, the rest unsupported)
+__global__ void __launch_bounds__(256) ecdsa_inv_kernel(uint64_t base, uint64_t m,
+                                                       const unsigned int* __restrict__ counts,
+                                                       uint32_t* __restrict__ ws) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t lo = t * kEcInvBatch;
+  if (lo >= m) return;
+  const uint64_t hi = lo + kEcInvBatch < m ? lo + kEcInvBatch : m;
+  const uint64_t c1 = counts[0], c2 = c1 + counts[1];
+  const uint64_t k1_end = c1 > base ? (c1 - base < m ? c1 - base : m) : 0;
+  const uint64_t r1_end = c2 > base ? (c2 - base < m ? c2 - base : m) : 0;
+  {
+    const uint64_t a = lo, b = hi < k1_end ? hi : k1_end;
+    if (a < b) ecdsa_inv_run<Curve<2>>(ws, a, b);
+  }
+  {
+    const uint64_t a = lo > k1_end ? lo : k1_end, b = hi < r1_end ? hi : r1_end;
+    if (a < b) ecdsa_inv_run<Curve<3>>(ws, a, b);
+  }
+}
+
+// P = u1 G + u2 Q with w = s^-1 from the batch inversion; x(P) mod n == r
+template <class C>
+CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ gtab) {
+  using P = typename C::P;
+  using N = typename C::N;
+  u256 w, e, r, u1, u2;
+  ld256(w, rec + kEcW);
+  ld256(e, rec + kEcE);
+  ld256(r, rec + kEcR);
+  mont_mul<N>(u1, e, w);  // plain e * s^-1 (one Montgomery factor cancels)
+  mont_mul<N>(u2, r, w);
+  bool neg1, neg2;
+  split_sign<N>(u1, neg1, u1);
+  split_sign<N>(u2, neg2, u2);
+  jpt acc;
+  acc.inf = true;
+  for (int j = 63; j >= 0; j--) {
+    const int dq = booth_digit<4>(u2.v, j);
+    const int aq = dq < 0 ? -dq : dq;
+    jpt T;  // issued before the doublings, consumed after them
+    ld_jpt(T, rec + kEcTab + 24 * (aq > 0 ? aq - 1 : 0));
+    if (j != 63) {
+      jdbl<C>(acc, acc);
+      jdbl<C>(acc, acc);
+      jdbl<C>(acc, acc);
+      jdbl<C>(acc, acc);
+    }
+    if (dq != 0) {
+      if ((dq < 0) != neg2) mod_neg<P>(T.Y, T.Y);
+      jadd<C>(acc, acc, T);
+    }
+    if ((j & 1) == 0) {
+      const int dg = booth_digit<8>(u1.v, j >> 1);
+      if (dg != 0) {
+        u256 gx, gy;
+        load_g(gx, gy, gtab, dg < 0 ? -dg : dg);
+        if ((dg < 0) != neg1) mod_neg<P>(gy, gy);
+        jmadd<C>(acc, acc, gx, gy);
+      }
+    }
+  }
+  if (acc.inf) return kStatusBadSig;
+  // x(P) mod n == r  <=>  X == r Z^2  or (r < p - n and X == (r + n) Z^2)
+  const u256 nm = mod_m<N>();
+  u256 z2, rm, t;
+  mont_sqr<P>(z2, acc.Z);
+  to_mont<P>(rm, r);
+  mont_mul<P>(t, rm, z2);
+  if (u256_eq(t, acc.X)) return kStatusOk;
+  if (!u256_geq(r, limbs_of<typename C::PmN>())) {
+    u256 rn;
+    u256_add(rn, r, nm);
+    to_mont<P>(rm, rn);
+    mont_mul<P>(t, rm, z2);
+    if (u256_eq(t, acc.X)) return kStatusOk;
+  }
+  return kStatusBadSig;
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ecdsa_ladder_kernel(
+    const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, uint64_t base, uint64_t m,
+    const uint32_t* __restrict__ gtab_k1, const uint32_t* __restrict__ gtab_r1, const uint32_t* __restrict__ ws,
+    uint8_t* __restrict__ status) {
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= m) return;
+  const uint64_t slot = base + li;
+  const uint64_t i = perm ? perm[slot] : slot;
+  if (status[i] != kEcPending) return;
+  const uint32_t* rec = ws + li * kEcWords;
+  status[i] = scheme[i] == 2 ? ecdsa_ladder_lane<Curve<2>>(rec, gtab_k1) : ecdsa_ladder_lane<Curve<3>>(rec, gtab_r1);
+}
+
 // ---------------------------------------------------------------------------
 size_t ecdsa_gtable_bytes() { return (size_t)kGEntries * kGEntryWords * sizeof(uint32_t); }
+size_t ecdsa_ws_slot_bytes() { return kEcWords * sizeof(uint32_t); }
 
 hipError_t launch_ecdsa_sign(const uint8_t* scheme, const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len,
                              uint64_t n, const uint32_t* gk1, const uint32_t* gr1, uint8_t* keys, uint8_t* key_len,
@@ -716,21 +966,43 @@ hipError_t launch_ecdsa_gtables(uint32_t* k1, uint32_t* r1, hipStream_t s) {
   return hipGetLastError();
 }
 
-// partition + verify + verdict; work: counts[3] + cursors[3] (zeroed here) and perm[n]
+// partition + verify + verdict; work: counts[3] + cursors[3] (zeroed here) and perm[n].
+// ws (ws_slots * ecdsa_ws_slot_bytes() of device memory) selects the split
+// path (prep -> batch inversion -> ladder per chunk of ws_slots); without it,
+// or with CORDAHIP_ECDSA=fused, the single fused kernel runs (A/B baseline).
 hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
                                const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs,
                                const uint64_t* msg_off, uint32_t msg_len, uint64_t n, const uint32_t* gk1,
                                const uint32_t* gr1, const uint8_t* pre_status, uint8_t* status,
                                unsigned long long* verdict, unsigned int* counters6, unsigned int* perm,
-                               hipStream_t s) {
+                               uint32_t* ws, uint64_t ws_slots, hipStream_t s) {
   if (n == 0) return hipSuccess;
+  static const bool fused = [] {
+    const char* v = getenv("CORDAHIP_ECDSA");
+    return v && std::string(v) == "fused";
+  }();
   const dim3 grid((uint32_t)((n + 255) / 256));
   hipError_t e = hipMemsetAsync(counters6, 0, 6 * sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(ecdsa_count_kernel, grid, dim3(256), 0, s, scheme, n, counters6);
   hipLaunchKernelGGL(ecdsa_scatter_kernel, grid, dim3(256), 0, s, scheme, n, counters6, counters6 + 3, perm);
-  hipLaunchKernelGGL(ecdsa_verify_kernel, grid, dim3(256), 0, s, perm, scheme, keys, key_len, sigs, sig_len, msgs,
-                     msg_off, msg_len, n, gk1, gr1, pre_status, status);
+  if (fused || !ws || ws_slots < 64) {
+    hipLaunchKernelGGL(ecdsa_verify_kernel, grid, dim3(256), 0, s, perm, scheme, keys, key_len, sigs, sig_len, msgs,
+                       msg_off, msg_len, n, gk1, gr1, pre_status, status);
+  } else {
+    for (uint64_t base = 0; base < n; base += ws_slots) {
+      const uint64_t m = n - base < ws_slots ? n - base : ws_slots;
+      const dim3 g((uint32_t)((m + 255) / 256));
+      hipLaunchKernelGGL(ecdsa_prep_kernel, g, dim3(256), 0, s, perm, scheme, keys, key_len, sigs, sig_len, msgs,
+                         msg_off, msg_len, base, m, pre_status, status, ws);
+      const uint64_t nt = (m + kEcInvBatch - 1) / kEcInvBatch;
+      hipLaunchKernelGGL(ecdsa_inv_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, s, base, m, counters6,
+                         ws);
+      hipLaunchKernelGGL(ecdsa_ladder_kernel, g, dim3(256), 0, s, perm, scheme, base, m, gk1, gr1, ws, status);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+  }
   if (verdict) hipLaunchKernelGGL(verdict_kernel, grid, dim3(256), 0, s, status, n, verdict);
   return hipGetLastError();
 }

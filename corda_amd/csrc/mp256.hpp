@@ -45,14 +45,13 @@ CDEV void mac_const(uint64_t& acc, uint32_t& hi, uint32_t q, int j) {
   mac(acc, hi, q, m);
 }
 
+// a >= b: no borrow out of a - b (branch-free; a short-circuit word compare
+// becomes divergent control flow on the GPU)
 CDEV bool u256_geq(const u256& a, const u256& b) {
-  bool gt = false, eq = true;
+  uint32_t br = 0;
 #pragma unroll
-  for (int i = 7; i >= 0; i--) {
-    gt = gt || (eq && a.v[i] > b.v[i]);
-    eq = eq && (a.v[i] == b.v[i]);
-  }
-  return gt || eq;
+  for (int i = 0; i < 8; i++) br = (uint32_t)(((uint64_t)a.v[i] - b.v[i] - br) >> 63);
+  return br == 0;
 }
 CDEV bool u256_iszero(const u256& a) {
   uint32_t x = 0;

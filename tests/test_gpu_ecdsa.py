@@ -118,3 +118,16 @@ def test_device_signer_matches_oracle(engine):
     engine.ecdsa_verify_device(t["scheme"], keys, kl, sigs, sl, t["msgs"], st)
     torch.cuda.synchronize()
     assert (st.cpu().numpy() == 0).all()
+
+
+def test_batch_inversion_boundaries(engine, ec_vectors):
+    """The split path inverts s in runs of 16 slots per thread (Montgomery's
+    trick) over the curve-partitioned order: odd batch sizes, runs that straddle
+    the secp256k1 / P-256 boundary and runs full of already-decided lanes must
+    all give the golden statuses."""
+    rng = random.Random(21)
+    for n in (1, 2, 15, 16, 17, 31, 33, 63, 65, 130, 257):
+        vs = [ec_vectors[rng.randrange(len(ec_vectors))] for _ in range(n)]
+        st, _ = engine.verify_batch([v["scheme"] for v in vs], [v["pub"] for v in vs], [v["sig"] for v in vs],
+                                    [v["msg"] for v in vs])
+        assert [int(x) for x in st] == [v["status"] for v in vs], n
