@@ -276,7 +276,84 @@ class C4:
                 "wall_s": dt, "txs_per_s": ntx / dt, "gpu_vs_port_mismatches_on_sample": mism}
 
 
-WORKLOADS = {"c2": C2, "c3": C3, "c4": C4}
+# ---- C5: verifier-module queue drain, mixed schemes, pinned host memory -------
+class C5:
+    kernel = "ed25519 prep/ladder + ecdsa prep/inv/ladder, 3-stage H2D/kernel/D2H pipeline"
+    pmc = None
+    host_timed = True  # the drain is synchronous and owns its streams: wall time, PCIe included
+
+    def __init__(self, eng, device, stream, rank, args):
+        import torch
+        from corda_amd.corpus import make_c2_corpus, make_c3_corpus
+        self.torch, self.eng = torch, eng
+        n = 1 << args.batch_log2
+        n_ec = n // 5  # 80% Ed25519 / 10% P-256 / 10% secp256k1
+        n_ed = n - n_ec
+        pubs, sigs, msgs, self.exp_ed, _ = make_c2_corpus(eng, n_ed, 0xC0DA0005 + rank, device, stream=stream)
+        (scheme, keys, key_len, esigs, sig_len, emsgs, self.exp_ec,
+         _) = make_c3_corpus(eng, n_ec, 0xC0DA0105 + rank, device, stream=stream)
+        torch.cuda.synchronize(device)
+        pin = lambda t: t.cpu().contiguous().pin_memory()
+        self.ed = [pin(t) for t in (pubs, sigs, msgs)] + [torch.zeros(n_ed, dtype=torch.uint8).pin_memory()]
+        self.ec = [pin(t) for t in (scheme, keys, key_len, esigs, sig_len, emsgs)] + \
+                  [torch.zeros(n_ec, dtype=torch.uint8).pin_memory()]
+        self.exp_ed, self.exp_ec = self.exp_ed.cpu(), self.exp_ec.cpu()
+        del pubs, sigs, msgs, scheme, keys, key_len, esigs, sig_len, emsgs
+        self.n_ed, self.n_ec = n_ed, n_ec
+        self.units = n
+        self.macs = (n_ed * LIMB_MACS["ed25519"] + n_ec * (LIMB_MACS["p256"] + LIMB_MACS["secp256k1"]) // 2) // n
+        self.workload = ("C5: verifier-module queue drain, 2^%d mixed sigs per GPU per step (80%% Ed25519, 10%% P-256, "
+                         "10%% secp256k1, 1%% corrupted) streamed from pinned host memory, H2D/D2H included"
+                         % args.batch_log2)
+        self.data = "synthetic: C2 and C3 corpora (GPU-signed), copied to pinned host memory before timing"
+        self.config = {"batch_per_gpu": n, "ed25519": n_ed, "ecdsa": n_ec, "chunk": 1 << 22, "stages": 3}
+
+    def step(self):
+        self.eng.stream_verify(self.ed, self.ec)
+
+    def check(self):
+        from corda_amd.corpus import REJECT_ANY
+        t = self.torch
+        st_ed = self.ed[3].to(t.int16)
+        st_ec = self.ec[6].to(t.int16)
+        k = self.exp_ed >= 0
+        ex = self.exp_ec >= 0
+        return {"mismatches_vs_construction": int((st_ed[k] != self.exp_ed[k]).sum())
+                + int((st_ec[ex] != self.exp_ec[ex]).sum()) + int((st_ec[self.exp_ec == REJECT_ANY] == 0).sum()),
+                "accepted": int((st_ed == 0).sum()) + int((st_ec == 0).sum())}
+
+    def cpu_baseline(self, sample):
+        import numpy as np
+        orc = _oracle()
+        se, sc = sample - sample // 5, sample // 5
+        k, s, m = (x[:se].numpy() for x in self.ed[:3])
+        out = np.zeros(se, np.uint8)
+        cores = _cores()
+        t0 = time.perf_counter()
+        orc.oracle_ed25519_verify_batch(se, k.ctypes.data, s.ctypes.data, m.ctypes.data, 32, out.ctypes.data, cores)
+        t_ed = time.perf_counter() - t0
+        sch, K, KL, S, SL, M = (x[:sc].numpy() for x in self.ec[:6])
+        kb = np.ascontiguousarray(np.concatenate([K[i, :KL[i]] for i in range(sc)]))
+        sb = np.ascontiguousarray(np.concatenate([S[i, :SL[i]] for i in range(sc)]))
+        ko = np.zeros(sc + 1, np.uint64)
+        so = np.zeros(sc + 1, np.uint64)
+        ko[1:] = np.cumsum(KL.astype(np.uint64))
+        so[1:] = np.cumsum(SL.astype(np.uint64))
+        mo = np.arange(sc + 1, dtype=np.uint64) * 32
+        out2 = np.zeros(sc, np.uint8)
+        Mc = np.ascontiguousarray(M)
+        t0 = time.perf_counter()
+        orc.oracle_ecdsa_verify_batch(sc, sch.ctypes.data, kb.ctypes.data, ko.ctypes.data, sb.ctypes.data,
+                                      so.ctypes.data, Mc.ctypes.data, mo.ctypes.data, out2.ctypes.data, cores)
+        t_ec = time.perf_counter() - t0
+        mism = int((out != self.ed[3][:se].numpy()).sum()) + int((out2 != self.ec[6][:sc].numpy()).sum())
+        return {"value": sample / (t_ed + t_ec), "unit": "verifications/s", "cores": cores, "kind": "port",
+                "sample": "first %d Ed25519 + %d ECDSA lanes of the rank-0 C5 queue (oracle/c, %d threads)"
+                          % (se, sc, cores),
+                "wall_s": t_ed + t_ec, "gpu_vs_port_mismatches_on_sample": mism}
+
+
+WORKLOADS = {"c2": C2, "c3": C3, "c4": C4, "c5": C5}
 
 
 def main():
@@ -342,6 +419,8 @@ def main():
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    if getattr(wl, "host_timed", False):
+        kernel_ms = elapsed * 1e3 / args.steps  # synchronous host-buffer drain: the wall clock is the measure
     chk = wl.check()
     elapsed = max_over_ranks(elapsed, device)
     chk["mismatches_vs_construction"] = int(max_over_ranks(float(chk["mismatches_vs_construction"]), device))
@@ -352,8 +431,8 @@ def main():
         # HBM bytes per step from the committed PMC passes (tools/gpu_pmc.sh:
         # FETCH_SIZE and WRITE_SIZE in separate passes), scaled to this step
         traffic = None
-        pmc_file = os.path.join(ROOT, "profiles", wl.pmc)
-        if os.path.exists(pmc_file):
+        pmc_file = os.path.join(ROOT, "profiles", wl.pmc) if wl.pmc else None
+        if pmc_file and os.path.exists(pmc_file):
             with open(pmc_file) as f:
                 per_unit = json.load(f).get("hbm_bytes_per_unit")
             traffic = per_unit * wl.units if per_unit else None
@@ -382,7 +461,7 @@ def main():
             "corpus_gen_s": t_gen,
         }
         if world == 1 and not args.no_cpu_baseline:
-            sample = args.cpu_sample or {"c2": 1 << 17, "c3": 1 << 16, "c4": 1 << 16}[args.workload]
+            sample = args.cpu_sample or {"c2": 1 << 17, "c3": 1 << 16, "c4": 1 << 16, "c5": 1 << 16}[args.workload]
             out["cpu_baseline"] = wl.cpu_baseline(min(sample, wl.units))
         print(json.dumps(out), flush=True)
     eng.close()

@@ -29,7 +29,7 @@ EXPORTS = [
     "cordahip_wait", "cordahip_poll", "cordahip_sig_verify", "cordahip_ed25519_verify_device",
     "cordahip_ed25519_verify_host", "cordahip_ed25519_sign_device", "cordahip_ecdsa_sign_device", "cordahip_last_kernel_ms",
     "cordahip_tx_ids", "cordahip_signed_tx_verify", "cordahip_signed_tx_verify_ed25519_device",
-    "cordahip_ecdsa_verify_device",
+    "cordahip_ecdsa_verify_device", "cordahip_stream_verify",
 ]
 TX_NO_LEAVES, TX_NO_SIGNATURES = 6, 7
 
@@ -72,6 +72,18 @@ class SignedTxBatch(ctypes.Structure):
         ("key", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
         ("sig", ctypes.c_void_p), ("sig_off", ctypes.c_void_p),
         ("sig_status", ctypes.c_void_p), ("first_bad_sig", ctypes.c_void_p),
+    ]
+
+
+class StreamBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_ed", ctypes.c_uint64),
+        ("ed_keys", ctypes.c_void_p), ("ed_sigs", ctypes.c_void_p), ("ed_msgs", ctypes.c_void_p),
+        ("ed_msg_len", ctypes.c_uint32), ("ed_status", ctypes.c_void_p),
+        ("n_ec", ctypes.c_uint64),
+        ("ec_scheme", ctypes.c_void_p), ("ec_keys", ctypes.c_void_p), ("ec_key_len", ctypes.c_void_p),
+        ("ec_sigs", ctypes.c_void_p), ("ec_sig_len", ctypes.c_void_p), ("ec_msgs", ctypes.c_void_p),
+        ("ec_msg_len", ctypes.c_uint32), ("ec_status", ctypes.c_void_p),
     ]
 
 
@@ -119,6 +131,7 @@ def lib() -> ctypes.CDLL:
                                                            vp, vp, vp]),
         "cordahip_ecdsa_verify_device": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, u32, u64, vp, vp, vp]),
         "cordahip_ecdsa_sign_device": (i32, [vp, i32, vp, vp, vp, u32, u64, vp, vp, vp, vp, vp]),
+        "cordahip_stream_verify": (i32, [vp, ctypes.POINTER(StreamBatch)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(l, name)

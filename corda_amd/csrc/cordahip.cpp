@@ -14,6 +14,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <future>
 #include <map>
@@ -85,6 +86,15 @@ struct Stage {  // one pipeline slot: device buffers + its stream
   DevBuf keys, sigs, msgs, pre, status, verdict;
 };
 
+// one stage of the C5 streaming pipeline (cordahip_stream_verify)
+struct StreamStage {
+  hipStream_t stream = nullptr;
+  DevBuf ed_keys, ed_sigs, ed_msgs, ed_status;
+  DevBuf ec_scheme, ec_keys, ec_key_len, ec_sigs, ec_sig_len, ec_msgs, ec_status;
+};
+constexpr int kStreamStages = 3;
+constexpr uint64_t kStreamChunk = 1ull << 22;  // lanes per chunk, both sections together
+
 struct TxWork {  // device buffers of the transaction paths (grow-only)
   DevBuf leaf_bytes, leaf_off, tx_leaf_off, hashes, txid, tx_status, tx_sig_off, msgs;
 };
@@ -115,6 +125,8 @@ struct Device {
   std::mutex ed_mu;
   DevBuf ed_ws;
   hipEvent_t ed_ev = nullptr;
+  std::mutex stream_mu;  // serialises use of sstage
+  StreamStage sstage[kStreamStages];
 };
 
 constexpr uint64_t kEdWsLanes = 1ull << 20;  // 3.1 GB of workspace per device
@@ -471,6 +483,94 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   return CORDAHIP_SUCCESS;
 }
 
+// C5: one device's contiguous shard of both sections, [e0, e1) Ed25519 and
+// [c0, c1) ECDSA lanes, streamed in chunks through kStreamStages stages. A
+// stage is reused only after its previous chunk (copies and kernels) is done,
+// so up to kStreamStages chunks are in flight: while one computes, the next
+// one's inputs and the previous one's statuses cross PCIe.
+int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_t e1, uint64_t c0, uint64_t c1) {
+  std::lock_guard<std::mutex> g(d.stream_mu);
+  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  const uint64_t ne = e1 - e0, nc = c1 - c0;
+  uint64_t chunk = kStreamChunk;  // CORDAHIP_STREAM_CHUNK: smaller chunks for tests of the pipeline itself
+  if (const char* v = getenv("CORDAHIP_STREAM_CHUNK")) chunk = std::max<uint64_t>(64, strtoull(v, nullptr, 10));
+  const uint64_t nchunks = std::max<uint64_t>(1, (ne + nc + chunk - 1) / chunk);
+  const uint64_t ce = ((ne + nchunks - 1) / nchunks + 63) / 64 * 64;
+  const uint64_t cc = ((nc + nchunks - 1) / nchunks + 63) / 64 * 64;
+  const uint64_t eml = b->ed_msg_len, cml = b->ec_msg_len;
+  for (StreamStage& st : d.sstage) {
+    if (!st.stream && hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)
+      return CORDAHIP_ERR_HIP;
+    if ((ce && (st.ed_keys.ensure(ce * 32) || st.ed_sigs.ensure(ce * 64) ||
+                st.ed_msgs.ensure(std::max<uint64_t>(ce * eml, 16)) || st.ed_status.ensure(ce))) ||
+        (cc && (st.ec_scheme.ensure(cc) || st.ec_keys.ensure(cc * 65) || st.ec_key_len.ensure(cc) ||
+                st.ec_sigs.ensure(cc * 72) || st.ec_sig_len.ensure(cc) ||
+                st.ec_msgs.ensure(std::max<uint64_t>(cc * cml, 16)) || st.ec_status.ensure(cc))))
+      return CORDAHIP_ERR_OUT_OF_MEMORY;
+  }
+  const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
+  for (uint64_t k = 0; k < nchunks; k++) {
+    StreamStage& st = d.sstage[k % kStreamStages];
+    hipStream_t s = st.stream;
+    if (k >= (uint64_t)kStreamStages && hipStreamSynchronize(s) != hipSuccess) return CORDAHIP_ERR_HIP;
+    const uint64_t a = std::min(e1, e0 + k * ce), ma = std::min(e1, a + ce) - a;
+    const uint64_t c = std::min(c1, c0 + k * cc), mc = std::min(c1, c + cc) - c;
+    hipError_t e = hipSuccess;
+    if (ma) {
+      e = e ? e : hipMemcpyAsync(st.ed_keys.p, b->ed_keys + a * 32, ma * 32, h2d, s);
+      e = e ? e : hipMemcpyAsync(st.ed_sigs.p, b->ed_sigs + a * 64, ma * 64, h2d, s);
+      if (eml) e = e ? e : hipMemcpyAsync(st.ed_msgs.p, b->ed_msgs + a * eml, ma * eml, h2d, s);
+    }
+    if (mc) {
+      e = e ? e : hipMemcpyAsync(st.ec_scheme.p, b->ec_scheme + c, mc, h2d, s);
+      e = e ? e : hipMemcpyAsync(st.ec_keys.p, b->ec_keys + c * 65, mc * 65, h2d, s);
+      e = e ? e : hipMemcpyAsync(st.ec_key_len.p, b->ec_key_len + c, mc, h2d, s);
+      e = e ? e : hipMemcpyAsync(st.ec_sigs.p, b->ec_sigs + c * 72, mc * 72, h2d, s);
+      e = e ? e : hipMemcpyAsync(st.ec_sig_len.p, b->ec_sig_len + c, mc, h2d, s);
+      if (cml) e = e ? e : hipMemcpyAsync(st.ec_msgs.p, b->ec_msgs + c * cml, mc * cml, h2d, s);
+    }
+    if (ma)
+      e = e ? e
+            : ed_verify_enqueue(d, st.ed_keys.as<uint8_t>(), st.ed_sigs.as<uint8_t>(), st.ed_msgs.as<uint8_t>(),
+                                (uint32_t)eml, ma, nullptr, st.ed_status.as<uint8_t>(), nullptr, s);
+    if (mc && e == hipSuccess) {
+      std::lock_guard<std::mutex> ge(d.ec_mu);
+      e = ec_verify_enqueue(d, st.ec_scheme.as<uint8_t>(), st.ec_keys.as<uint8_t>(), st.ec_key_len.as<uint8_t>(),
+                            st.ec_sigs.as<uint8_t>(), st.ec_sig_len.as<uint8_t>(), st.ec_msgs.as<uint8_t>(), nullptr,
+                            (uint32_t)cml, mc, nullptr, st.ec_status.as<uint8_t>(), nullptr, s);
+    }
+    if (ma) e = e ? e : hipMemcpyAsync(b->ed_status + a, st.ed_status.p, ma, d2h, s);
+    if (mc) e = e ? e : hipMemcpyAsync(b->ec_status + c, st.ec_status.p, mc, d2h, s);
+    if (e != hipSuccess) return CORDAHIP_ERR_HIP;
+  }
+  for (StreamStage& st : d.sstage)
+    if (hipStreamSynchronize(st.stream) != hipSuccess) return CORDAHIP_ERR_HIP;
+  return CORDAHIP_SUCCESS;
+}
+
+int stream_verify_impl(cordahip_ctx* ctx, const cordahip_stream_batch* b) {
+  if ((b->n_ed && (!b->ed_keys || !b->ed_sigs || !b->ed_status || (b->ed_msg_len && !b->ed_msgs))) ||
+      (b->n_ec && (!b->ec_scheme || !b->ec_keys || !b->ec_key_len || !b->ec_sigs || !b->ec_sig_len ||
+                   !b->ec_status || (b->ec_msg_len && !b->ec_msgs))))
+    return CORDAHIP_ERR_INVALID_ARG;
+  const uint64_t nd = ctx->devs.size();
+  const uint64_t pe = ((b->n_ed + nd - 1) / nd + 63) / 64 * 64, pc = ((b->n_ec + nd - 1) / nd + 63) / 64 * 64;
+  std::vector<std::future<int>> fs;
+  for (uint64_t i = 0; i < nd; i++) {
+    const uint64_t e0 = std::min(b->n_ed, i * pe), e1 = std::min(b->n_ed, e0 + pe);
+    const uint64_t c0 = std::min(b->n_ec, i * pc), c1 = std::min(b->n_ec, c0 + pc);
+    if (e0 >= e1 && c0 >= c1) break;
+    Device* d = ctx->devs[i].get();
+    fs.push_back(std::async(std::launch::async, [=] { return stream_shard(*d, b, e0, e1, c0, c1); }));
+  }
+  int rc = CORDAHIP_SUCCESS;
+  for (auto& f : fs) {
+    const int r = f.get();
+    if (r != CORDAHIP_SUCCESS) rc = r;
+  }
+  return rc;
+}
+
 Device* dev_at(cordahip_ctx* ctx, int device) {
   if (!ctx || device < 0 || device >= (int)ctx->devs.size()) return nullptr;
   return ctx->devs[device].get();
@@ -535,6 +635,12 @@ void cordahip_shutdown(cordahip_ctx* ctx) {
     (void)hipSetDevice(d->id);
     for (auto& st : d->stage) {
       for (DevBuf* b : {&st.keys, &st.sigs, &st.msgs, &st.pre, &st.status, &st.verdict})
+        if (b->p) (void)hipFree(b->p);
+      if (st.stream) (void)hipStreamDestroy(st.stream);
+    }
+    for (auto& st : d->sstage) {
+      for (DevBuf* b : {&st.ed_keys, &st.ed_sigs, &st.ed_msgs, &st.ed_status, &st.ec_scheme, &st.ec_keys,
+                        &st.ec_key_len, &st.ec_sigs, &st.ec_sig_len, &st.ec_msgs, &st.ec_status})
         if (b->p) (void)hipFree(b->p);
       if (st.stream) (void)hipStreamDestroy(st.stream);
     }
@@ -662,6 +768,11 @@ int cordahip_ed25519_verify_host(cordahip_ctx* ctx, const uint8_t* keys, const u
                                  uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict) {
   if (!ctx || (n && (!keys || !sigs || !status || (msg_len && !msgs)))) return CORDAHIP_ERR_INVALID_ARG;
   return ed25519_dense_host(ctx, keys, sigs, msgs, msg_len, nullptr, n, status, verdict);
+}
+
+int cordahip_stream_verify(cordahip_ctx* ctx, const cordahip_stream_batch* batch) {
+  if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
+  return stream_verify_impl(ctx, batch);
 }
 
 int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_seeds, const void* d_msgs,

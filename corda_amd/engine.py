@@ -13,7 +13,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import EngineError, SigBatch, SignedTxBatch, TxidBatch, check, lib
+from ._lib import EngineError, SigBatch, SignedTxBatch, StreamBatch, TxidBatch, check, lib
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -161,6 +161,21 @@ class Engine:
             self._ctx, device, scheme.data_ptr(), keys.data_ptr(), key_len.data_ptr(), sigs.data_ptr(),
             sig_len.data_ptr(), msgs.data_ptr(), msgs.shape[1], scheme.shape[0], status.data_ptr(),
             verdict.data_ptr() if verdict is not None else None, s), "cordahip_ecdsa_verify_device")
+
+    # ---- C5: streaming mixed-scheme drain (host, ideally pinned, memory) -------
+    def stream_verify(self, ed, ec):
+        """ed = (keys[n,32], sigs[n,64], msgs[n,L], status[n]) and ec = (scheme[n], keys[n,65],
+        key_len[n], sigs[n,72], sig_len[n], msgs[n,L], status[n]): host arrays (numpy or CPU torch
+        tensors; pin them for overlapped copies). Statuses are written in place."""
+        def p(x):
+            return x.data_ptr() if hasattr(x, "data_ptr") else x.ctypes.data
+
+        ek, es, em, est = ed
+        sc, ck, ckl, cs, csl, cm, cst = ec
+        b = StreamBatch(ek.shape[0], p(ek), p(es), p(em), em.shape[1] if ek.shape[0] else 0, p(est),
+                        sc.shape[0], p(sc), p(ck), p(ckl), p(cs), p(csl), p(cm), cm.shape[1] if sc.shape[0] else 0,
+                        p(cst))
+        check(lib().cordahip_stream_verify(self._ctx, ctypes.byref(b)), "cordahip_stream_verify")
 
     def last_kernel_ms(self, device: int = 0) -> float:
         return lib().cordahip_last_kernel_ms(self._ctx, device)

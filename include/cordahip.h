@@ -132,6 +132,37 @@ int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_sc
                                  const void* d_key_len, const void* d_sigs, const void* d_sig_len, const void* d_msgs,
                                  uint32_t msg_len, uint64_t n, void* d_status, void* d_verdict, void* hip_stream);
 
+/* ---- streaming mixed-scheme drain (verifier-module queue) ----- *
+ * Replaces the per-request Crypto.isValid calls a verifier would make for a
+ * queue of mixed-scheme requests (Crypto.kt:534-541; the out-of-process
+ * verifier's request loop, verifier/.../Verifier.kt:58-75).
+ * The producer writes requests straight into the two dense host layouts
+ * (pinned memory from cordahip_alloc_pinned, or the copies are not
+ * asynchronous): an Ed25519 section (as cordahip_ed25519_verify_host) and an
+ * ECDSA section (as cordahip_ecdsa_verify_device, 65/72-byte slots). Each
+ * context device takes a contiguous shard of both sections and streams it in
+ * chunks of up to 2^22 lanes through 3 stages (one HIP stream each), so the
+ * H2D copy of chunk k+1, the kernels of chunk k and the status D2H of chunk
+ * k-1 overlap. Synchronous; statuses land in ed_status / ec_status.          */
+typedef struct {
+  uint64_t n_ed;
+  const uint8_t* ed_keys; /* [n_ed*32] */
+  const uint8_t* ed_sigs; /* [n_ed*64] */
+  const uint8_t* ed_msgs; /* [n_ed*ed_msg_len] */
+  uint32_t ed_msg_len;
+  uint8_t* ed_status;     /* [n_ed] out */
+  uint64_t n_ec;
+  const uint8_t* ec_scheme;  /* [n_ec] 2 or 3 */
+  const uint8_t* ec_keys;    /* [n_ec*65] SEC1 in 65-byte slots */
+  const uint8_t* ec_key_len; /* [n_ec] */
+  const uint8_t* ec_sigs;    /* [n_ec*72] DER in 72-byte slots */
+  const uint8_t* ec_sig_len; /* [n_ec] */
+  const uint8_t* ec_msgs;    /* [n_ec*ec_msg_len] */
+  uint32_t ec_msg_len;
+  uint8_t* ec_status;        /* [n_ec] out */
+} cordahip_stream_batch;
+int cordahip_stream_verify(cordahip_ctx* ctx, const cordahip_stream_batch* batch);
+
 /* RFC 8032 keygen + sign from 32-byte seeds (device memory): corpus generation. */
 int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_seeds, const void* d_msgs,
                                  uint32_t msg_len, uint64_t n, void* d_pubs, void* d_sigs, void* hip_stream);
