@@ -29,9 +29,9 @@ EXPORTS = [
     "cordahip_wait", "cordahip_poll", "cordahip_sig_verify", "cordahip_ed25519_verify_device",
     "cordahip_ed25519_verify_host", "cordahip_ed25519_sign_device", "cordahip_ecdsa_sign_device", "cordahip_last_kernel_ms",
     "cordahip_tx_ids", "cordahip_signed_tx_verify", "cordahip_signed_tx_verify_ed25519_device",
-    "cordahip_ecdsa_verify_device", "cordahip_stream_verify",
+    "cordahip_ecdsa_verify_device", "cordahip_stream_verify", "cordahip_filtered_tx_verify",
 ]
-TX_NO_LEAVES, TX_NO_SIGNATURES = 6, 7
+TX_NO_LEAVES, TX_NO_SIGNATURES, TX_BAD_TREE = 6, 7, 8
 
 
 class EngineUnavailable(RuntimeError):
@@ -72,6 +72,15 @@ class SignedTxBatch(ctypes.Structure):
         ("key", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
         ("sig", ctypes.c_void_p), ("sig_off", ctypes.c_void_p),
         ("sig_status", ctypes.c_void_p), ("first_bad_sig", ctypes.c_void_p),
+    ]
+
+
+class FilteredTxBatch(ctypes.Structure):
+    _fields_ = [
+        ("ntx", ctypes.c_uint64),
+        ("leaf_bytes", ctypes.c_void_p), ("leaf_off", ctypes.c_void_p), ("tx_leaf_off", ctypes.c_void_p),
+        ("tok", ctypes.c_void_p), ("tok_hash", ctypes.c_void_p), ("tx_tok_off", ctypes.c_void_p),
+        ("root", ctypes.c_void_p), ("tx_status", ctypes.c_void_p),
     ]
 
 
@@ -132,6 +141,7 @@ def lib() -> ctypes.CDLL:
         "cordahip_ecdsa_verify_device": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, u32, u64, vp, vp, vp]),
         "cordahip_ecdsa_sign_device": (i32, [vp, i32, vp, vp, vp, u32, u64, vp, vp, vp, vp, vp]),
         "cordahip_stream_verify": (i32, [vp, ctypes.POINTER(StreamBatch)]),
+        "cordahip_filtered_tx_verify": (i32, [vp, ctypes.POINTER(FilteredTxBatch)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(l, name)

@@ -45,6 +45,9 @@ hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, u
                               hipStream_t s);
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
                             uint8_t* tx_status, hipStream_t s);
+hipError_t launch_pmt_verify(const uint32_t* leaf_hashes, const uint64_t* tx_leaf_off, const uint8_t* tok,
+                             const uint8_t* tok_hash, const uint64_t* tx_tok_off, const uint8_t* root, uint64_t ntx,
+                             uint32_t* stack, uint8_t* tx_status, hipStream_t s);
 size_t ecdsa_gtable_bytes();
 hipError_t launch_ecdsa_gtables(uint32_t* k1, uint32_t* r1, hipStream_t s);
 hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
@@ -97,6 +100,7 @@ constexpr uint64_t kStreamChunk = 1ull << 22;  // lanes per chunk, both sections
 
 struct TxWork {  // device buffers of the transaction paths (grow-only)
   DevBuf leaf_bytes, leaf_off, tx_leaf_off, hashes, txid, tx_status, tx_sig_off, msgs;
+  DevBuf tok, tok_hash, tx_tok_off, root, stack;  // filtered-tx (partial Merkle tree) path
 };
 
 struct EcWork {  // device buffers of the ECDSA paths (grow-only)
@@ -571,6 +575,72 @@ int stream_verify_impl(cordahip_ctx* ctx, const cordahip_stream_batch* b) {
   return rc;
 }
 
+// FilteredTransaction.verify for txs [t0, t1) on one device: K3 hashes the
+// filtered leaves, K6 evaluates each partial tree and compares.
+int filtered_tx_shard(Device& d, const cordahip_filtered_tx_batch* b, uint64_t t0, uint64_t t1) {
+  std::lock_guard<std::mutex> g(d.tx_mu);
+  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  const uint64_t ntx = t1 - t0;
+  const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
+  const uint64_t b0 = nleaves ? b->leaf_off[l0] : 0, b1 = nleaves ? b->leaf_off[l1] : 0;
+  const uint64_t k0 = b->tx_tok_off[t0], k1 = b->tx_tok_off[t1], ntok = k1 - k0;
+  std::vector<uint64_t> loff(nleaves + 1), toff(ntx + 1), koff(ntx + 1);
+  for (uint64_t i = 0; i <= nleaves; i++) loff[i] = nleaves ? b->leaf_off[l0 + i] - b0 : 0;
+  for (uint64_t i = 0; i <= ntx; i++) {
+    toff[i] = b->tx_leaf_off[t0 + i] - l0;
+    koff[i] = b->tx_tok_off[t0 + i] - k0;
+  }
+  TxWork& w = d.tx;
+  if (w.leaf_bytes.ensure(std::max<uint64_t>(b1 - b0, 16)) || w.leaf_off.ensure((nleaves + 1) * 8) ||
+      w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
+      w.tok.ensure(std::max<uint64_t>(ntok, 1)) || w.tok_hash.ensure(std::max<uint64_t>(ntok, 1) * 32) ||
+      w.tx_tok_off.ensure((ntx + 1) * 8) || w.root.ensure(ntx * 32) ||
+      w.stack.ensure(std::max<uint64_t>(ntok, 1) * 32) || w.tx_status.ensure(ntx))
+    return CORDAHIP_ERR_OUT_OF_MEMORY;
+  hipStream_t s = d.stream;
+  const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+  hipError_t e = hipSuccess;
+  if (b1 > b0) e = hipMemcpyAsync(w.leaf_bytes.p, b->leaf_bytes + b0, b1 - b0, h2d, s);
+  e = e ? e : hipMemcpyAsync(w.leaf_off.p, loff.data(), (nleaves + 1) * 8, h2d, s);
+  e = e ? e : hipMemcpyAsync(w.tx_leaf_off.p, toff.data(), (ntx + 1) * 8, h2d, s);
+  if (ntok) {
+    e = e ? e : hipMemcpyAsync(w.tok.p, b->tok + k0, ntok, h2d, s);
+    e = e ? e : hipMemcpyAsync(w.tok_hash.p, b->tok_hash + k0 * 32, ntok * 32, h2d, s);
+  }
+  e = e ? e : hipMemcpyAsync(w.tx_tok_off.p, koff.data(), (ntx + 1) * 8, h2d, s);
+  e = e ? e : hipMemcpyAsync(w.root.p, b->root + t0 * 32, ntx * 32, h2d, s);
+  e = e ? e : launch_sha256_leaves(w.leaf_bytes.as<uint8_t>(), w.leaf_off.as<uint64_t>(), nleaves,
+                                   w.hashes.as<uint32_t>(), s);
+  e = e ? e : launch_pmt_verify(w.hashes.as<uint32_t>(), w.tx_leaf_off.as<uint64_t>(), w.tok.as<uint8_t>(),
+                                w.tok_hash.as<uint8_t>(), w.tx_tok_off.as<uint64_t>(), w.root.as<uint8_t>(), ntx,
+                                w.stack.as<uint32_t>(), w.tx_status.as<uint8_t>(), s);
+  e = e ? e : hipMemcpyAsync(b->tx_status + t0, w.tx_status.p, ntx, hipMemcpyDeviceToHost, s);
+  e = e ? e : hipStreamSynchronize(s);
+  return hip_err(e);
+}
+
+int filtered_tx_impl(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* b) {
+  const uint64_t n = b->ntx, nd = ctx->devs.size();
+  if (n == 0) return CORDAHIP_SUCCESS;
+  if (!b->leaf_off || !b->tx_leaf_off || !b->tx_tok_off || !b->root || !b->tx_status ||
+      (!b->tok && b->tx_tok_off[n]) || (!b->tok_hash && b->tx_tok_off[n]))
+    return CORDAHIP_ERR_INVALID_ARG;
+  const uint64_t per = (n + nd - 1) / nd;  // contiguous tx shards, independent trees
+  std::vector<std::future<int>> fs;
+  for (uint64_t i = 0; i < nd; i++) {
+    const uint64_t t0 = std::min(n, i * per), t1 = std::min(n, t0 + per);
+    if (t0 >= t1) break;
+    Device* d = ctx->devs[i].get();
+    fs.push_back(std::async(std::launch::async, [=] { return filtered_tx_shard(*d, b, t0, t1); }));
+  }
+  int rc = CORDAHIP_SUCCESS;
+  for (auto& f : fs) {
+    const int r = f.get();
+    if (r != CORDAHIP_SUCCESS) rc = r;
+  }
+  return rc;
+}
+
 Device* dev_at(cordahip_ctx* ctx, int device) {
   if (!ctx || device < 0 || device >= (int)ctx->devs.size()) return nullptr;
   return ctx->devs[device].get();
@@ -645,7 +715,8 @@ void cordahip_shutdown(cordahip_ctx* ctx) {
       if (st.stream) (void)hipStreamDestroy(st.stream);
     }
     for (DevBuf* b : {&d->tx.leaf_bytes, &d->tx.leaf_off, &d->tx.tx_leaf_off, &d->tx.hashes, &d->tx.txid,
-                      &d->tx.tx_status, &d->tx.tx_sig_off, &d->tx.msgs})
+                      &d->tx.tx_status, &d->tx.tx_sig_off, &d->tx.msgs, &d->tx.tok, &d->tx.tok_hash,
+                      &d->tx.tx_tok_off, &d->tx.root, &d->tx.stack})
       if (b->p) (void)hipFree(b->p);
     for (DevBuf* b : {&d->ec.scheme, &d->ec.keys, &d->ec.key_len, &d->ec.sigs, &d->ec.sig_len, &d->ec.msgs,
                       &d->ec.msg_off, &d->ec.pre, &d->ec.status, &d->ec.counters, &d->ec.perm, &d->ec.ws})
@@ -768,6 +839,11 @@ int cordahip_ed25519_verify_host(cordahip_ctx* ctx, const uint8_t* keys, const u
                                  uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict) {
   if (!ctx || (n && (!keys || !sigs || !status || (msg_len && !msgs)))) return CORDAHIP_ERR_INVALID_ARG;
   return ed25519_dense_host(ctx, keys, sigs, msgs, msg_len, nullptr, n, status, verdict);
+}
+
+int cordahip_filtered_tx_verify(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch) {
+  if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
+  return filtered_tx_impl(ctx, batch);
 }
 
 int cordahip_stream_verify(cordahip_ctx* ctx, const cordahip_stream_batch* batch) {

@@ -163,6 +163,114 @@ __global__ void __launch_bounds__(256) tx_reduce_kernel(const uint8_t* __restric
 }
 
 // ---------------------------------------------------------------------------
+// K6: FilteredTransaction.verify (MerkleTransaction.kt:134-140) ->
+// PartialMerkleTree.verify (PartialMerkleTree.kt:132-158), one lane per
+// filtered transaction. The partial tree arrives as its post-order token
+// stream (0 IncludedLeaf, 1 Leaf, 2 Node) and is evaluated with a stack kept in
+// HBM (the tx's own slice of `stack`, one 32-B slot per token): IncludedLeaf /
+// Leaf push their hash, Node pops right then left and pushes
+// hashConcat(left, right) = SHA-256(left || right) (SecureHash.kt:24). The
+// included hashes, in token order, are the reference's usedHashes; verify()
+// is true iff they equal the filtered leaves' hashes as multisets
+// (groupBy equality) and the computed root equals the claimed root.
+static constexpr uint8_t kTxBadTree = 8;
+static constexpr uint8_t kTokIncluded = 0, kTokLeaf = 1, kTokNode = 2;
+
+CDEV void load_hash_be(uint32_t w[8], const uint8_t* __restrict__ p) {  // 32 bytes -> SHA state words
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);
+  const uint4 a = p4[0], b = p4[1];
+  w[0] = bswap32(a.x); w[1] = bswap32(a.y); w[2] = bswap32(a.z); w[3] = bswap32(a.w);
+  w[4] = bswap32(b.x); w[5] = bswap32(b.y); w[6] = bswap32(b.z); w[7] = bswap32(b.w);
+}
+CDEV void st_words(uint32_t* __restrict__ o, const uint32_t w[8]) {
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+  o4[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  o4[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+CDEV void ld_words(uint32_t w[8], const uint32_t* __restrict__ p) {
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);
+  const uint4 a = p4[0], b = p4[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+CDEV bool words_eq(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) d |= a[k] ^ b[k];
+  return d == 0;
+}
+
+__global__ void __launch_bounds__(256) pmt_verify_kernel(const uint32_t* __restrict__ leaf_hashes,
+                                                        const uint64_t* __restrict__ tx_leaf_off,
+                                                        const uint8_t* __restrict__ tok,
+                                                        const uint8_t* __restrict__ tok_hash,
+                                                        const uint64_t* __restrict__ tx_tok_off,
+                                                        const uint8_t* __restrict__ root, uint64_t ntx,
+                                                        uint32_t* __restrict__ stack, uint8_t* __restrict__ tx_status) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;
+  const uint64_t l0 = tx_leaf_off[t], l1 = tx_leaf_off[t + 1];
+  if (l0 == l1) {  // filteredLeaves.availableComponentHashes empty: MerkleTreeException
+    tx_status[t] = kTxNoLeaves;
+    return;
+  }
+  const uint64_t k0 = tx_tok_off[t], k1 = tx_tok_off[t + 1];
+  uint32_t* stk = stack + k0 * 8;
+  uint64_t sp = 0, nincl = 0;
+  bool ok = true;
+  for (uint64_t k = k0; k < k1 && ok; k++) {
+    const uint8_t tk = tok[k];
+    if (tk == kTokIncluded || tk == kTokLeaf) {
+      uint32_t h[8];
+      load_hash_be(h, tok_hash + k * 32);
+      st_words(stk + sp * 8, h);
+      sp++;
+      nincl += tk == kTokIncluded;
+    } else if (tk == kTokNode && sp >= 2) {
+      uint32_t a[8], b[8], r[8];
+      ld_words(b, stk + (sp - 1) * 8);
+      ld_words(a, stk + (sp - 2) * 8);
+      sha256_node(r, a, b);
+      st_words(stk + (sp - 2) * 8, r);
+      sp--;
+    } else {
+      ok = false;
+    }
+  }
+  if (!ok || sp != 1) {
+    tx_status[t] = kTxBadTree;
+    return;
+  }
+  uint32_t want[8];
+  load_hash_be(want, root + t * 32);
+  bool match = words_eq(stk, want) && nincl == l1 - l0;
+  // multiset equality of the included token hashes and the leaf hashes
+  for (uint64_t k = k0; k < k1 && match; k++) {
+    if (tok[k] != kTokIncluded) continue;
+    uint32_t h[8];
+    load_hash_be(h, tok_hash + k * 32);
+    uint64_t in_tree = 0, in_leaves = 0;
+    for (uint64_t q = k0; q < k1; q++) {
+      if (tok[q] != kTokIncluded) continue;
+      uint32_t g[8];
+      load_hash_be(g, tok_hash + q * 32);
+      in_tree += words_eq(g, h);
+    }
+    for (uint64_t q = l0; q < l1; q++) in_leaves += words_eq(leaf_hashes + q * 8, h);
+    match = in_tree == in_leaves;
+  }
+  tx_status[t] = match ? kStatusOk : kStatusBadSig;
+}
+
+hipError_t launch_pmt_verify(const uint32_t* leaf_hashes, const uint64_t* tx_leaf_off, const uint8_t* tok,
+                             const uint8_t* tok_hash, const uint64_t* tx_tok_off, const uint8_t* root, uint64_t ntx,
+                             uint32_t* stack, uint8_t* tx_status, hipStream_t s) {
+  if (!ntx) return hipSuccess;
+  hipLaunchKernelGGL(pmt_verify_kernel, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, s, leaf_hashes,
+                     tx_leaf_off, tok, tok_hash, tx_tok_off, root, ntx, stack, tx_status);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 hipError_t launch_sha256_leaves(const uint8_t* bytes, const uint64_t* off, uint64_t nleaves, uint32_t* hashes,
                                 hipStream_t s) {
   if (!nleaves) return hipSuccess;

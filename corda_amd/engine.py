@@ -13,7 +13,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import EngineError, SigBatch, SignedTxBatch, StreamBatch, TxidBatch, check, lib
+from ._lib import EngineError, FilteredTxBatch, SigBatch, SignedTxBatch, StreamBatch, TxidBatch, check, lib
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -161,6 +161,27 @@ class Engine:
             self._ctx, device, scheme.data_ptr(), keys.data_ptr(), key_len.data_ptr(), sigs.data_ptr(),
             sig_len.data_ptr(), msgs.data_ptr(), msgs.shape[1], scheme.shape[0], status.data_ptr(),
             verdict.data_ptr() if verdict is not None else None, s), "cordahip_ecdsa_verify_device")
+
+    # ---- FilteredTransaction.verify / PartialMerkleTree.verify ----------------
+    def filtered_tx_verify(self, ftxs):
+        """ftxs[t] = (leaves: [bytes], tokens: [(tok, hash32 or None)], root: bytes32), tokens being the
+        post-order stream of the PartialMerkleTree (oracle/partial_merkle.py tokens()). Returns tx_status."""
+        leaves = [leaf for f in ftxs for leaf in f[0]]
+        lb, lo = self._csr(leaves)
+        to = np.zeros(len(ftxs) + 1, dtype=np.uint64)
+        ko = np.zeros(len(ftxs) + 1, dtype=np.uint64)
+        if ftxs:
+            to[1:] = np.cumsum([len(f[0]) for f in ftxs], dtype=np.uint64)
+            ko[1:] = np.cumsum([len(f[1]) for f in ftxs], dtype=np.uint64)
+        toks = [t for f in ftxs for t in f[1]]
+        tok = np.ascontiguousarray(np.array([t[0] for t in toks] or [0], dtype=np.uint8))
+        th = np.frombuffer(b"".join((t[1] or bytes(32)) for t in toks) or bytes(32), dtype=np.uint8).copy()
+        root = np.frombuffer(b"".join(f[2] for f in ftxs) or bytes(32), dtype=np.uint8).copy()
+        st = np.zeros(max(len(ftxs), 1), dtype=np.uint8)
+        b = FilteredTxBatch(len(ftxs), _ptr(lb), _ptr(lo), _ptr(to), _ptr(tok), _ptr(th), _ptr(ko), _ptr(root),
+                            _ptr(st))
+        check(lib().cordahip_filtered_tx_verify(self._ctx, ctypes.byref(b)), "cordahip_filtered_tx_verify")
+        return st[:len(ftxs)]
 
     # ---- C5: streaming mixed-scheme drain (host, ideally pinned, memory) -------
     def stream_verify(self, ed, ec):

@@ -220,6 +220,31 @@ int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, cons
                                              const void* d_sigs, uint64_t nsig, void* d_txid, void* d_tx_status,
                                              void* d_first_bad, void* d_sig_status, void* hip_stream);
 
+/* FilteredTransaction.verify over many filtered transactions:
+ *   FilteredTransaction.verify   core/.../transactions/MerkleTransaction.kt:134-140
+ *   PartialMerkleTree.verify     core/.../crypto/PartialMerkleTree.kt:132-158
+ * Per filtered tx t: the FilteredLeaves' serialised components (leaf CSR exactly
+ * as in cordahip_txid_batch; the GPU hashes them = availableComponentHashes),
+ * the PartialMerkleTree as its post-order token stream tok[k] (0 IncludedLeaf,
+ * 1 Leaf, 2 Node) with tok_hash[k*32 .. k*32+32) the hash of token k (ignored
+ * for Node), and the claimed rootHash. tx_status[t]: OK (verify() == true),
+ * BAD_SIG (verify() == false), CORDAHIP_TX_NO_LEAVES (MerkleTreeException,
+ * no included leaves), CORDAHIP_TX_BAD_TREE (the token stream is not a tree:
+ * no PartialMerkleTree serialises to it). */
+#define CORDAHIP_TX_BAD_TREE 8
+typedef struct {
+  uint64_t ntx;
+  const uint8_t* leaf_bytes;
+  const uint64_t* leaf_off;    /* [nleaves+1] */
+  const uint64_t* tx_leaf_off; /* [ntx+1] */
+  const uint8_t* tok;          /* [ntok] */
+  const uint8_t* tok_hash;     /* [ntok*32] */
+  const uint64_t* tx_tok_off;  /* [ntx+1] */
+  const uint8_t* root;         /* [ntx*32] claimed Merkle roots (FilteredTransaction.rootHash) */
+  uint8_t* tx_status;          /* [ntx] out */
+} cordahip_filtered_tx_batch;
+int cordahip_filtered_tx_verify(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch);
+
 /* Device time of the last kernel launched by the context on `device` (ms), measured
  * with HIP events on the stream the kernel ran on; -1 if unavailable. */
 double cordahip_last_kernel_ms(cordahip_ctx* ctx, int device);
