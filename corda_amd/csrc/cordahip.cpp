@@ -469,12 +469,12 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   for (uint64_t t = 0; t < ntx; t++) {
     const uint64_t lo = b->tx_sig_off[t], hi = b->tx_sig_off[t + 1];
     b->first_bad_sig[t] = -1;
-    if (b->tx.tx_status[t] != CORDAHIP_STATUS_OK) {  // tx.id threw before any signature was checked
-      for (uint64_t s = lo; s < hi; s++) b->sig_status[s] = b->tx.tx_status[t];
+    if (lo == hi) {  // require(sigs.isNotEmpty()) in the constructor (SignedTransaction.kt:37-39) precedes tx.id
+      b->tx.tx_status[t] = CORDAHIP_TX_NO_SIGNATURES;
       continue;
     }
-    if (lo == hi) {
-      b->tx.tx_status[t] = CORDAHIP_TX_NO_SIGNATURES;
+    if (b->tx.tx_status[t] != CORDAHIP_STATUS_OK) {  // tx.id threw before any signature was checked
+      for (uint64_t s = lo; s < hi; s++) b->sig_status[s] = b->tx.tx_status[t];
       continue;
     }
     for (uint64_t s = lo; s < hi; s++)

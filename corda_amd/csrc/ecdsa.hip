@@ -10,6 +10,11 @@
 //   sig: strict DER (der.hpp) else MALFORMED_SIG; r, s in [1, n-1] else BAD_SIG;
 //   e = SHA-256(msg); w = s^-1; P = (e w) G + (r w) Q; accept iff P != O and
 //   x(P) mod n == r, checked inversion-free as X == r Z^2 or (r + n) Z^2.
+// Arithmetic: the base field in fp29.hpp (9 x 29-bit limbs, Montgomery
+// R = 2^261, lazy reduction), the scalar field mod n in mp256.hpp.
+// secp256k1 lanes split both scalars with the GLV endomorphism
+// (u = k1 + k2 lambda with |k1|, |k2| < 2^129; phi(x, y) = (beta x, y) =
+// [lambda](x, y)), so their ladder runs 128 doublings instead of 252.
 // One lane per signature; lanes are permuted so each wave holds one curve
 // (device-side partition kernels below), so the two curves' code never
 // diverges inside a wave except at the single boundary wave.
@@ -20,6 +25,8 @@
 #include <string>
 
 #include "der.hpp"
+#include "fp29.hpp"
+#include "fp29_consts.hpp"
 #include "mp256.hpp"
 #include "sc25519.hpp"
 #include "sha2_device.hpp"
@@ -32,10 +39,10 @@ namespace cordahip {
     return i == 0 ? a0 : i == 1 ? a1 : i == 2 ? a2 : i == 3 ? a3 : i == 4 ? a4 : i == 5 ? a5 : i == 6 ? a6 : a7; \
   }
 
+// 8 x 32-bit moduli: p for range checks, n (with R^2 = 2^512 mod n) for the
+// scalar-field Montgomery arithmetic of mp256.hpp
 struct K1P {
   CH_LIMBS(limb, 0xfffffc2fu, 0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu)
-  CH_LIMBS(r2, 0x000e90a1u, 0x000007a2u, 0x00000001u, 0u, 0u, 0u, 0u, 0u)
-  static constexpr uint32_t kMinv = 0xd2253531u;
 };
 struct K1N {
   CH_LIMBS(limb, 0xd0364141u, 0xbfd25e8cu, 0xaf48a03bu, 0xbaaedce6u, 0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu)
@@ -44,8 +51,6 @@ struct K1N {
 };
 struct R1P {
   CH_LIMBS(limb, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u, 0x00000001u, 0xffffffffu)
-  CH_LIMBS(r2, 0x00000003u, 0u, 0xffffffffu, 0xfffffffbu, 0xfffffffeu, 0xffffffffu, 0xfffffffdu, 0x00000004u)
-  static constexpr uint32_t kMinv = 0x00000001u;
 };
 struct R1N {
   CH_LIMBS(limb, 0xfc632551u, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu, 0xffffffffu, 0xffffffffu, 0u, 0xffffffffu)
@@ -59,15 +64,9 @@ struct K1Nm2 { CH_LIMBS(limb, 0xd036413fu, 0xbfd25e8cu, 0xaf48a03bu, 0xbaaedce6u
 struct R1Sqrt { CH_LIMBS(limb, 0u, 0u, 0x40000000u, 0u, 0u, 0x40000000u, 0xc0000000u, 0x3fffffffu) };
 struct R1Pm2 { CH_LIMBS(limb, 0xfffffffdu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u, 0x00000001u, 0xffffffffu) };
 struct R1Nm2 { CH_LIMBS(limb, 0xfc63254fu, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu, 0xffffffffu, 0xffffffffu, 0u, 0xffffffffu) };
-
-struct K1B { CH_LIMBS(limb, 0x00001ab7u, 0x00000007u, 0u, 0u, 0u, 0u, 0u, 0u) };
+// p - n (x(P) mod n == r also holds for x = r + n when r < p - n)
 struct K1PmN { CH_LIMBS(limb, 0x22fc9baeu, 0x402da172u, 0x50b75fc4u, 0x45512319u, 0x00000001u, 0u, 0u, 0u) };
-struct K1Gx { CH_LIMBS(limb, 0x487e2097u, 0xd7362e5au, 0x29bc66dbu, 0x231e2953u, 0x33fd129cu, 0x979f48c0u, 0xe9089f48u, 0x9981e643u) };
-struct K1Gy { CH_LIMBS(limb, 0xd3dbabe2u, 0xb15ea6d2u, 0x1f1dc64du, 0x8dfc5d5du, 0xac19c136u, 0x70b6b59au, 0xd4a582d6u, 0xcf3f851fu) };
-struct R1B { CH_LIMBS(limb, 0x29c4bddfu, 0xd89cdf62u, 0x78843090u, 0xacf005cdu, 0xf7212ed6u, 0xe5a220abu, 0x04874834u, 0xdc30061du) };
 struct R1PmN { CH_LIMBS(limb, 0x039cdaaeu, 0x0c46353du, 0x58e8617bu, 0x43190553u, 0u, 0u, 0u, 0u) };
-struct R1Gx { CH_LIMBS(limb, 0x18a9143cu, 0x79e730d4u, 0x5fedb601u, 0x75ba95fcu, 0x77622510u, 0x79fb732bu, 0xa53755c6u, 0x18905f76u) };
-struct R1Gy { CH_LIMBS(limb, 0xce95560au, 0xddf25357u, 0xba19e45cu, 0x8b4ab8e4u, 0xdd21f325u, 0xd2e88688u, 0x25885d85u, 0x8571ff18u) };
 
 template <int SCHEME>
 struct Curve;
@@ -75,37 +74,36 @@ template <>
 struct Curve<2> {  // secp256k1: y^2 = x^3 + 7
   using P = K1P;
   using N = K1N;
+  using F = K1F;
   using Sqrt = K1Sqrt;
   using Pm2 = K1Pm2;
   using Nm2 = K1Nm2;
-  static constexpr bool kAm3 = false;
-  using B = K1B;
   using PmN = K1PmN;
-  using Gx = K1Gx;
-  using Gy = K1Gy;
+  static constexpr bool kAm3 = false;
+  static constexpr bool kGlv = true;
 };
 template <>
 struct Curve<3> {  // secp256r1 / P-256: y^2 = x^3 - 3x + b
   using P = R1P;
   using N = R1N;
+  using F = R1F;
   using Sqrt = R1Sqrt;
   using Pm2 = R1Pm2;
   using Nm2 = R1Nm2;
-  static constexpr bool kAm3 = true;
-  using B = R1B;
   using PmN = R1PmN;
-  using Gx = R1Gx;
-  using Gy = R1Gy;
+  static constexpr bool kAm3 = true;
+  static constexpr bool kGlv = false;
 };
 
-template <class F>
+template <class Fc>
 CDEV u256 limbs_of() {
   u256 r;
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = F::limb(i);
+  for (int i = 0; i < 8; i++) r.v[i] = Fc::limb(i);
   return r;
 }
 
+// scalar field (mod n) Montgomery conversions
 template <class M>
 CDEV void to_mont(u256& r, const u256& a) {
   u256 r2;
@@ -113,79 +111,83 @@ CDEV void to_mont(u256& r, const u256& a) {
   for (int i = 0; i < 8; i++) r2.v[i] = M::r2(i);
   mont_mul<M>(r, a, r2);
 }
-template <class M>
-CDEV void from_mont(u256& r, const u256& a) {
-  u256 one;
-#pragma unroll
-  for (int i = 0; i < 8; i++) one.v[i] = i == 0;
-  mont_mul<M>(r, a, one);
-}
 
-// ---- Jacobian points (Montgomery-form coordinates) --------------------------
+// ---- Jacobian points, coordinates in fp29 Montgomery form (norm, < 2p) -----
 struct jpt {
-  u256 X, Y, Z;
+  f29 X, Y, Z;
   bool inf;
 };
 
 // 2P. a = -3: dbl-2001-b (3M + 5S); a = 0: dbl-2009-l (2M + 5S). Prime-order
 // curves have no 2-torsion, so only the point at infinity is exceptional.
+// Every f29_sub / f29_red below respects fp29.hpp's operand bounds (value
+// bounds in units of p in the comments; modelled in tests/test_fp29_model.py).
 template <class C>
 CDEV void jdbl(jpt& r, const jpt& p) {
-  using P = typename C::P;
+  using F = typename C::F;
   if (p.inf) {
     r.inf = true;
     return;
   }
-  u256 x3, y3, z3;
-  if (C::kAm3) {
-    u256 delta, gamma, beta, alpha, t, u;
-    mont_sqr<P>(delta, p.Z);
-    mont_sqr<P>(gamma, p.Y);
-    mont_mul<P>(beta, p.X, gamma);
-    mod_sub<P>(t, p.X, delta);
-    mod_add<P>(u, p.X, delta);
-    mont_mul<P>(alpha, t, u);
-    mod_add<P>(t, alpha, alpha);
-    mod_add<P>(alpha, alpha, t);  // 3 (X - delta)(X + delta)
-    mont_sqr<P>(x3, alpha);
-    mod_add<P>(t, beta, beta);
-    mod_add<P>(t, t, t);          // 4 beta
-    mod_add<P>(u, t, t);          // 8 beta
-    mod_sub<P>(x3, x3, u);
-    mod_add<P>(z3, p.Y, p.Z);
-    mont_sqr<P>(z3, z3);
-    mod_sub<P>(z3, z3, gamma);
-    mod_sub<P>(z3, z3, delta);
-    mod_sub<P>(u, t, x3);
-    mont_mul<P>(y3, alpha, u);
-    mont_sqr<P>(u, gamma);
-    mod_add<P>(u, u, u);
-    mod_add<P>(u, u, u);
-    mod_add<P>(u, u, u);          // 8 gamma^2
-    mod_sub<P>(y3, y3, u);
+  f29 x3, y3, z3, t, u;
+  if constexpr (C::kAm3) {
+    f29 delta, gamma, beta, a3, b4;
+    f29_sqr<F>(delta, p.Z);
+    f29_sqr<F>(gamma, p.Y);
+    f29_mul<F>(beta, p.X, gamma);
+    f29_sub<F>(t, p.X, delta);  // < 4p
+    f29_add(u, p.X, delta);     // < 4p
+    f29_mul<F>(a3, t, u);
+    f29_add(t, a3, a3);
+    f29_add(t, t, a3);
+    f29_red<F>(a3, t);          // alpha = 3 (X - delta)(X + delta)
+    f29_sqr<F>(x3, a3);
+    f29_add(t, beta, beta);
+    f29_add(t, t, t);
+    f29_red<F>(b4, t);          // 4 beta
+    f29_sub<F>(x3, x3, b4);
+    f29_sub<F>(t, x3, b4);      // < 6p
+    f29_red<F>(x3, t);          // X3 = alpha^2 - 8 beta
+    f29_add(t, p.Y, p.Z);
+    f29_sqr<F>(t, t);
+    f29_sub<F>(t, t, gamma);
+    f29_sub<F>(t, t, delta);
+    f29_red<F>(z3, t);          // Z3 = (Y + Z)^2 - gamma - delta
+    f29_sub<F>(u, b4, x3);
+    f29_mul<F>(y3, a3, u);
+    f29_add(t, gamma, gamma);
+    f29_sqr<F>(u, t);           // 4 gamma^2
+    f29_sub<F>(y3, y3, u);
+    f29_sub<F>(t, y3, u);
+    f29_red<F>(y3, t);          // Y3 = alpha (4 beta - X3) - 8 gamma^2
   } else {
-    u256 A, B, Cc, D, E, F, t;
-    mont_sqr<P>(A, p.X);
-    mont_sqr<P>(B, p.Y);
-    mont_sqr<P>(Cc, B);
-    mod_add<P>(t, p.X, B);
-    mont_sqr<P>(t, t);
-    mod_sub<P>(t, t, A);
-    mod_sub<P>(t, t, Cc);
-    mod_add<P>(D, t, t);
-    mod_add<P>(E, A, A);
-    mod_add<P>(E, E, A);
-    mont_sqr<P>(F, E);
-    mod_add<P>(t, D, D);
-    mod_sub<P>(x3, F, t);
-    mod_sub<P>(t, D, x3);
-    mont_mul<P>(y3, E, t);
-    mod_add<P>(t, Cc, Cc);
-    mod_add<P>(t, t, t);
-    mod_add<P>(t, t, t);          // 8 C
-    mod_sub<P>(y3, y3, t);
-    mont_mul<P>(z3, p.Y, p.Z);
-    mod_add<P>(z3, z3, z3);
+    f29 A, B, Cc, D, E;
+    f29_sqr<F>(A, p.X);
+    f29_sqr<F>(B, p.Y);
+    f29_sqr<F>(Cc, B);
+    f29_add(t, p.X, B);
+    f29_sqr<F>(t, t);
+    f29_sub<F>(t, t, A);
+    f29_sub<F>(t, t, Cc);       // < 6p
+    f29_add(t, t, t);           // < 12p
+    f29_red<F>(D, t);           // D = 2 ((X + B)^2 - A - C)
+    f29_add(t, A, A);
+    f29_add(t, t, A);
+    f29_red<F>(E, t);           // E = 3 A
+    f29_sqr<F>(x3, E);
+    f29_sub<F>(x3, x3, D);
+    f29_sub<F>(t, x3, D);
+    f29_red<F>(x3, t);          // X3 = E^2 - 2 D
+    f29_sub<F>(t, D, x3);
+    f29_mul<F>(y3, E, t);
+    f29_add(t, Cc, Cc);
+    f29_add(t, t, t);
+    f29_red<F>(u, t);           // 4 C
+    f29_sub<F>(y3, y3, u);
+    f29_sub<F>(t, y3, u);
+    f29_red<F>(y3, t);          // Y3 = E (D - X3) - 8 C
+    f29_add(t, p.Y, p.Y);
+    f29_mul<F>(z3, t, p.Z);     // Z3 = 2 Y Z
   }
   r.X = x3;
   r.Y = y3;
@@ -196,7 +198,7 @@ CDEV void jdbl(jpt& r, const jpt& p) {
 // P + Q, both Jacobian (add-2007-bl, 11M + 5S), with the exceptional cases
 template <class C>
 CDEV void jadd(jpt& r, const jpt& p, const jpt& q) {
-  using P = typename C::P;
+  using F = typename C::F;
   if (p.inf) {
     r = q;
     return;
@@ -205,45 +207,49 @@ CDEV void jadd(jpt& r, const jpt& p, const jpt& q) {
     r = p;
     return;
   }
-  u256 z1z1, z2z2, u1, u2, s1, s2, h, rr, t;
-  mont_sqr<P>(z1z1, p.Z);
-  mont_sqr<P>(z2z2, q.Z);
-  mont_mul<P>(u1, p.X, z2z2);
-  mont_mul<P>(u2, q.X, z1z1);
-  mont_mul<P>(t, p.Y, q.Z);
-  mont_mul<P>(s1, t, z2z2);
-  mont_mul<P>(t, q.Y, p.Z);
-  mont_mul<P>(s2, t, z1z1);
-  mod_sub<P>(h, u2, u1);
-  mod_sub<P>(rr, s2, s1);
-  if (u256_iszero(h)) {
-    if (u256_iszero(rr)) {
+  f29 z1z1, z2z2, u1, u2, s1, s2, h, rr, t;
+  f29_sqr<F>(z1z1, p.Z);
+  f29_sqr<F>(z2z2, q.Z);
+  f29_mul<F>(u1, p.X, z2z2);
+  f29_mul<F>(u2, q.X, z1z1);
+  f29_mul<F>(t, p.Y, q.Z);
+  f29_mul<F>(s1, t, z2z2);
+  f29_mul<F>(t, q.Y, p.Z);
+  f29_mul<F>(s2, t, z1z1);
+  f29_sub<F>(t, u2, u1);
+  f29_red<F>(h, t);
+  f29_sub<F>(t, s2, s1);
+  f29_red<F>(rr, t);
+  if (f29_iszero<F>(h)) {
+    if (f29_iszero<F>(rr)) {
       jdbl<C>(r, p);
     } else {
       r.inf = true;
     }
     return;
   }
-  u256 i, j, v, x3, y3, z3;
-  mod_add<P>(t, h, h);
-  mont_sqr<P>(i, t);
-  mont_mul<P>(j, h, i);
-  mod_add<P>(rr, rr, rr);
-  mont_mul<P>(v, u1, i);
-  mont_sqr<P>(x3, rr);
-  mod_sub<P>(x3, x3, j);
-  mod_sub<P>(x3, x3, v);
-  mod_sub<P>(x3, x3, v);
-  mod_sub<P>(t, v, x3);
-  mont_mul<P>(y3, rr, t);
-  mont_mul<P>(t, s1, j);
-  mod_add<P>(t, t, t);
-  mod_sub<P>(y3, y3, t);
-  mod_add<P>(t, p.Z, q.Z);
-  mont_sqr<P>(t, t);
-  mod_sub<P>(t, t, z1z1);
-  mod_sub<P>(t, t, z2z2);
-  mont_mul<P>(z3, t, h);
+  f29 i, j, v, x3, y3, z3;
+  f29_add(t, h, h);
+  f29_sqr<F>(i, t);             // I = (2H)^2
+  f29_mul<F>(j, h, i);          // J = H I
+  f29_add(rr, rr, rr);          // r = 2 (S2 - S1), < 4p
+  f29_mul<F>(v, u1, i);         // V = U1 I
+  f29_sqr<F>(x3, rr);
+  f29_sub<F>(x3, x3, j);
+  f29_sub<F>(x3, x3, v);
+  f29_sub<F>(t, x3, v);         // < 8p
+  f29_red<F>(x3, t);            // X3 = r^2 - J - 2V
+  f29_sub<F>(t, v, x3);
+  f29_mul<F>(y3, rr, t);
+  f29_mul<F>(t, s1, j);
+  f29_sub<F>(y3, y3, t);
+  f29_sub<F>(y3, y3, t);
+  f29_red<F>(y3, y3);           // Y3 = r (V - X3) - 2 S1 J
+  f29_add(t, p.Z, q.Z);
+  f29_sqr<F>(t, t);
+  f29_sub<F>(t, t, z1z1);
+  f29_sub<F>(t, t, z2z2);       // < 6p
+  f29_mul<F>(z3, t, h);         // Z3 = ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H
   r.X = x3;
   r.Y = y3;
   r.Z = z3;
@@ -252,145 +258,172 @@ CDEV void jadd(jpt& r, const jpt& p, const jpt& q) {
 
 // P + (x2, y2) affine (madd-2007-bl, 7M + 4S)
 template <class C>
-CDEV void jmadd(jpt& r, const jpt& p, const u256& x2, const u256& y2) {
-  using P = typename C::P;
+CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
+  using F = typename C::F;
   if (p.inf) {
     r.X = x2;
     r.Y = y2;
-    u256 one;  // Z = 1, i.e. 2^256 mod p in Montgomery form
-#pragma unroll
-    for (int i = 0; i < 8; i++) one.v[i] = i == 0;
-    to_mont<P>(r.Z, one);
+    f29_const_one<F>(r.Z);
     r.inf = false;
     return;
   }
-  u256 z1z1, u2, s2, h, hh, i, j, rr, v, t, x3, y3, z3;
-  mont_sqr<P>(z1z1, p.Z);
-  mont_mul<P>(u2, x2, z1z1);
-  mont_mul<P>(t, y2, p.Z);
-  mont_mul<P>(s2, t, z1z1);
-  mod_sub<P>(h, u2, p.X);
-  mod_sub<P>(rr, s2, p.Y);
-  if (u256_iszero(h)) {
-    if (u256_iszero(rr)) {
+  f29 z1z1, u2, s2, h, hh, i, j, rr, v, t, x3, y3, z3;
+  f29_sqr<F>(z1z1, p.Z);
+  f29_mul<F>(u2, x2, z1z1);
+  f29_mul<F>(t, y2, p.Z);
+  f29_mul<F>(s2, t, z1z1);
+  f29_sub<F>(t, u2, p.X);
+  f29_red<F>(h, t);
+  f29_sub<F>(t, s2, p.Y);
+  f29_red<F>(rr, t);
+  if (f29_iszero<F>(h)) {
+    if (f29_iszero<F>(rr)) {
       jdbl<C>(r, p);
     } else {
       r.inf = true;
     }
     return;
   }
-  mont_sqr<P>(hh, h);
-  mod_add<P>(i, hh, hh);
-  mod_add<P>(i, i, i);
-  mont_mul<P>(j, h, i);
-  mod_add<P>(rr, rr, rr);
-  mont_mul<P>(v, p.X, i);
-  mont_sqr<P>(x3, rr);
-  mod_sub<P>(x3, x3, j);
-  mod_sub<P>(x3, x3, v);
-  mod_sub<P>(x3, x3, v);
-  mod_sub<P>(t, v, x3);
-  mont_mul<P>(y3, rr, t);
-  mont_mul<P>(t, p.Y, j);
-  mod_add<P>(t, t, t);
-  mod_sub<P>(y3, y3, t);
-  mod_add<P>(t, p.Z, h);
-  mont_sqr<P>(t, t);
-  mod_sub<P>(t, t, z1z1);
-  mod_sub<P>(z3, t, hh);
+  f29_sqr<F>(hh, h);
+  f29_add(i, hh, hh);
+  f29_add(i, i, i);             // I = 4 HH, < 8p
+  f29_mul<F>(j, h, i);
+  f29_add(rr, rr, rr);
+  f29_mul<F>(v, p.X, i);
+  f29_sqr<F>(x3, rr);
+  f29_sub<F>(x3, x3, j);
+  f29_sub<F>(x3, x3, v);
+  f29_sub<F>(t, x3, v);
+  f29_red<F>(x3, t);
+  f29_sub<F>(t, v, x3);
+  f29_mul<F>(y3, rr, t);
+  f29_mul<F>(t, p.Y, j);
+  f29_sub<F>(y3, y3, t);
+  f29_sub<F>(y3, y3, t);
+  f29_red<F>(y3, y3);
+  f29_add(t, p.Z, h);
+  f29_sqr<F>(t, t);
+  f29_sub<F>(t, t, z1z1);
+  f29_sub<F>(t, t, hh);
+  f29_red<F>(z3, t);
   r.X = x3;
   r.Y = y3;
   r.Z = z3;
   r.inf = false;
 }
 
-// ---- G tables: entry k (1..128) = [k]G affine (Montgomery x, y), 16 u32 ------
+// ---- G tables: entry k (0..128) = [k]G affine (Montgomery, canonical) ------
+// tables [0, 129) = [k]G and, for secp256k1, [129, 258) = [k](lambda G) = (beta x, y)
 static constexpr int kGEntries = 129;
-static constexpr int kGEntryWords = 16;
+static constexpr int kGEntryWords = 20;  // x[9], y[9], 2 pad: five 16-B loads
+static constexpr int kGTables = 2;
 
 template <class C>
 __global__ void __launch_bounds__(64) ecdsa_gtable_kernel(uint32_t* __restrict__ tab) {
-  using P = typename C::P;
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= kGEntries) return;
-  uint32_t* o = tab + k * kGEntryWords;
-  if (k == 0) {
+  using F = typename C::F;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= kGTables * kGEntries) return;
+  const int k = g % kGEntries;
+  uint32_t* o = tab + g * kGEntryWords;
+  if (k == 0 || (g >= kGEntries && !C::kGlv)) {
     for (int i = 0; i < kGEntryWords; i++) o[i] = 0;
     return;
   }
   jpt G, R;
-  G.X = limbs_of<typename C::Gx>();
-  G.Y = limbs_of<typename C::Gy>();
-  u256 one;
-#pragma unroll
-  for (int i = 0; i < 8; i++) one.v[i] = i == 0;
-  to_mont<P>(G.Z, one);
+  for (int i = 0; i < 9; i++) {
+    G.X.v[i] = F::gxm(i);
+    G.Y.v[i] = F::gym(i);
+  }
+  f29_const_one<F>(G.Z);
   G.inf = false;
   R.inf = true;
   for (int bit = 7; bit >= 0; bit--) {
     jdbl<C>(R, R);
     if ((k >> bit) & 1) jadd<C>(R, R, G);
   }
-  u256 zi, zi2, x, y;
-  mont_pow_const<P, typename C::Pm2>(zi, R.Z);
-  mont_sqr<P>(zi2, zi);
-  mont_mul<P>(x, R.X, zi2);
-  mont_mul<P>(zi2, zi2, zi);
-  mont_mul<P>(y, R.Y, zi2);
-  for (int i = 0; i < 8; i++) {
-    o[i] = x.v[i];
-    o[8 + i] = y.v[i];
+  f29 zi, zi2, x, y;
+  f29_pow_const<F, typename C::Pm2>(zi, R.Z);
+  f29_sqr<F>(zi2, zi);
+  f29_mul<F>(x, R.X, zi2);
+  f29_mul<F>(zi2, zi2, zi);
+  f29_mul<F>(y, R.Y, zi2);
+  if (g >= kGEntries) {
+    f29 b;
+    for (int i = 0; i < 9; i++) b.v[i] = F::betam(i);
+    f29_mul<F>(x, x, b);
   }
+  f29_canon<F>(x, x);
+  f29_canon<F>(y, y);
+  for (int i = 0; i < 9; i++) {
+    o[i] = x.v[i];
+    o[9 + i] = y.v[i];
+  }
+  o[18] = 0;
+  o[19] = 0;
 }
 
-CDEV void load_g(u256& x, u256& y, const uint32_t* __restrict__ tab, int idx) {
+CDEV void load_g(f29& x, f29& y, const uint32_t* __restrict__ tab, int idx) {
   const uint4* e = reinterpret_cast<const uint4*>(tab + idx * kGEntryWords);
-  const uint4 a = e[0], b = e[1], c = e[2], d = e[3];
-  x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
-  x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
-  y.v[0] = c.x; y.v[1] = c.y; y.v[2] = c.z; y.v[3] = c.w;
-  y.v[4] = d.x; y.v[5] = d.y; y.v[6] = d.z; y.v[7] = d.w;
+  uint32_t w[20];
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    const uint4 v = e[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    x.v[i] = w[i];
+    y.v[i] = w[9 + i];
+  }
 }
 
 // SEC1 point decode + validation (BC ECCurve.decodePoint); Montgomery form
 template <class C>
 CDEV bool decode_key(jpt& Q, const uint8_t* __restrict__ key, uint32_t len) {
   using P = typename C::P;
+  using F = typename C::F;
   const u256 pm = mod_m<P>();
-  u256 x, y, xm, ym, rhs, t;
   const bool unc = (len == 65 && key[0] == 4);
   const bool cmp = (len == 33 && (key[0] == 2 || key[0] == 3));
   if (!unc && !cmp) return false;
+  u256 x, y;
   u256_from_be_bytes(x, key + 1);
   if (u256_geq(x, pm)) return false;
-  to_mont<P>(xm, x);
+  f29 xm, rhs, t, ym;
+  f29_from_words(t, x.v);
+  f29_to_mont<F>(xm, t);
   // rhs = x^3 + a x + b
-  mont_sqr<P>(rhs, xm);
-  mont_mul<P>(rhs, rhs, xm);
-  if (C::kAm3) {
-    mod_sub<P>(rhs, rhs, xm);
-    mod_sub<P>(rhs, rhs, xm);
-    mod_sub<P>(rhs, rhs, xm);
+  f29_sqr<F>(rhs, xm);
+  f29_mul<F>(rhs, rhs, xm);
+  if constexpr (C::kAm3) {
+    f29_add(t, xm, xm);
+    f29_add(t, t, xm);
+    f29_red<F>(t, t);
+    f29_sub<F>(rhs, rhs, t);
   }
-  mod_add<P>(rhs, rhs, limbs_of<typename C::B>());
+#pragma unroll
+  for (int i = 0; i < 9; i++) t.v[i] = F::bm(i);
+  f29_add(rhs, rhs, t);
+  f29_red<F>(rhs, rhs);
   if (unc) {
     u256_from_be_bytes(y, key + 33);
     if (u256_geq(y, pm)) return false;
-    to_mont<P>(ym, y);
+    f29_from_words(t, y.v);
+    f29_to_mont<F>(ym, t);
   } else {
-    mont_pow_const<P, typename C::Sqrt>(ym, rhs);
-    u256 yp;
-    from_mont<P>(yp, ym);
-    if ((yp.v[0] & 1) != (uint32_t)(key[0] & 1)) mod_neg<P>(ym, ym);
+    f29_pow_const<F, typename C::Sqrt>(ym, rhs);
+    f29 yp;
+    f29_from_mont<F>(yp, ym);
+    f29_cneg<F>(ym, (yp.v[0] & 1) != (uint32_t)(key[0] & 1));
   }
-  mont_sqr<P>(t, ym);
-  if (!u256_eq(t, rhs)) return false;
+  f29_sqr<F>(t, ym);
+  if (!f29_eq<F>(t, rhs)) return false;
   Q.X = xm;
   Q.Y = ym;
-  u256 one;
-#pragma unroll
-  for (int i = 0; i < 8; i++) one.v[i] = i == 0;
-  to_mont<P>(Q.Z, one);
+  f29_const_one<F>(Q.Z);
   Q.inf = false;
   return true;
 }
@@ -405,92 +438,299 @@ CDEV void split_sign(u256& out, bool& neg, const u256& k) {
   for (int i = 0; i < 8; i++) out.v[i] = neg ? t.v[i] : k.v[i];
 }
 
+// round(k g / 2^384) for k, g < 2^256 (bits 384.. of the product, rounded at bit 383)
+CDEV void mul_shift_384(u256& c, const u256& k, const u256& g) {
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint64_t t = (uint64_t)k.v[i] * g.v[j] + x[i + j] + carry;
+      x[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    x[i + 8] = (uint32_t)carry;
+  }
+  uint64_t s = (uint64_t)x[12] + (x[11] >> 31);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (i) s += x[12 + i];
+    c.v[i] = (uint32_t)s;
+    s >>= 32;
+  }
+  c.v[4] = (uint32_t)s;
+  c.v[5] = c.v[6] = c.v[7] = 0;
+}
+
+// secp256k1 GLV split: k == k1 + k2 lambda (mod n), returned as magnitudes
+// < 2^129 with signs (split_sign convention). Basis, rounding constants and
+// the bound: tools/gen_fp29_consts.py (Gallant-Lambert-Vanstone 2001).
+CDEV void glv_split(u256& k1, bool& neg1, u256& k2, bool& neg2, const u256& k) {
+  using N = K1N;
+  u256 c1, c2, t1, t2, r1, r2;
+  mul_shift_384(c1, k, limbs_of<K1G1>());
+  mul_shift_384(c2, k, limbs_of<K1G2>());
+  mont_mul<N>(t1, c1, limbs_of<K1MB1M>());   // c1 (-b1) mod n
+  mont_mul<N>(t2, c2, limbs_of<K1MB2M>());   // c2 (-b2) mod n
+  mod_add<N>(r2, t1, t2);
+  mont_mul<N>(t1, r2, limbs_of<K1MLamM>());  // -lambda r2
+  mod_add<N>(r1, t1, k);
+  split_sign<N>(k1, neg1, r1);
+  split_sign<N>(k2, neg2, r2);
+}
+
+// ---- per-lane workspace record (split path) and its layout ------------------
+// Slots are the curve-partitioned order (perm), processed in chunks of
+// ws_slots; each slot owns a 1 KiB record in HBM.
+static constexpr int kEcPtWords = 28;           // X, Y, Z (9 limbs each) + 1 pad: seven 16-B accesses
+static constexpr int kEcTab = 0;                // [k]Q, k = 1..8, Jacobian
+static constexpr int kEcS = 8 * kEcPtWords;     // s, Montgomery form mod n (batch-inversion input)
+static constexpr int kEcW = kEcS + 8;           // prefix products, then w = s^-1 (Montgomery form mod n)
+static constexpr int kEcE = kEcW + 8;           // e = SHA-256(msg) mod n
+static constexpr int kEcR = kEcE + 8;           // r
+static constexpr int kEcWords = kEcR + 8;       // 256 words = 1 KiB
+static constexpr int kEcInvBatch = 16;          // signatures per thread in the batch inversion
+static constexpr uint8_t kEcPending = 0xff;     // slot whose verdict the ladder decides
+
+CDEV void st256(uint32_t* __restrict__ o, const u256& v) {
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+  o4[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+  o4[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+}
+CDEV void ld256(u256& v, const uint32_t* __restrict__ p) {
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);
+  const uint4 a = p4[0], b = p4[1];
+  v.v[0] = a.x; v.v[1] = a.y; v.v[2] = a.z; v.v[3] = a.w;
+  v.v[4] = b.x; v.v[5] = b.y; v.v[6] = b.z; v.v[7] = b.w;
+}
+CDEV void st_jpt(uint32_t* __restrict__ o, const jpt& p) {
+  uint32_t w[28];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    w[i] = p.X.v[i];
+    w[9 + i] = p.Y.v[i];
+    w[18 + i] = p.Z.v[i];
+  }
+  w[27] = 0;
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+#pragma unroll
+  for (int q = 0; q < 7; q++) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+CDEV void ld_jpt(jpt& p, const uint32_t* __restrict__ o) {
+  const uint4* o4 = reinterpret_cast<const uint4*>(o);
+  uint32_t w[28];
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    const uint4 v = o4[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    p.X.v[i] = w[i];
+    p.Y.v[i] = w[9 + i];
+    p.Z.v[i] = w[18 + i];
+  }
+  p.inf = false;
+}
+
+// x(P) mod n == r  <=>  X == r Z^2  or (r < p - n and X == (r + n) Z^2)
+template <class C>
+CDEV uint8_t x_check(const jpt& acc, const u256& r) {
+  using F = typename C::F;
+  if (acc.inf) return kStatusBadSig;
+  f29 z2, rm, t;
+  f29_sqr<F>(z2, acc.Z);
+  f29_from_words(t, r.v);
+  f29_to_mont<F>(rm, t);
+  f29_mul<F>(t, rm, z2);
+  const bool eq0 = f29_eq<F>(t, acc.X);
+  u256 rn;
+  u256_add(rn, r, mod_m<typename C::N>());
+  const bool alt = !u256_geq(r, limbs_of<typename C::PmN>());
+  f29_from_words(t, rn.v);
+  f29_to_mont<F>(rm, t);
+  f29_mul<F>(t, rm, z2);
+  const bool eq1 = f29_eq<F>(t, acc.X);
+  return (eq0 || (alt && eq1)) ? kStatusOk : kStatusBadSig;
+}
+
+// Everything before the scalar multiplication, in the reference's order (key
+// decode, Crypto.doVerify's require()s, DER, range checks), then e, s, r and
+// the [k]Q table go to the slot's record. Decided lanes store s = 1 so the
+// batch product stays invertible.
+template <class C>
+CDEV uint8_t ecdsa_prep_lane(const uint8_t* __restrict__ key, uint32_t key_len, const uint8_t* __restrict__ sig,
+                             uint32_t sig_len, const uint8_t* __restrict__ msg, uint64_t msg_len, uint8_t pre_status,
+                             uint32_t* __restrict__ rec) {
+  using N = typename C::N;
+  u256 sm;
+  {
+    u256 one;
+#pragma unroll
+    for (int q = 0; q < 8; q++) one.v[q] = q == 0;
+    to_mont<N>(sm, one);
+  }
+  jpt Q;
+  uint8_t st = kEcPending;
+  u256 r, s;
+  if (!decode_key<C>(Q, key, key_len)) {
+    st = kStatusBadKey;  // key built before verify
+  } else if (pre_status != kStatusOk) {
+    st = pre_status;
+  } else if (sig_len == 0 || msg_len == 0) {
+    st = kStatusEmpty;  // Crypto.kt:475-476
+  } else {
+    DerInt dr, ds;
+    if (!der_decode_sig(sig, sig_len, dr, ds)) {
+      st = kStatusMalformedSig;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        r.v[q] = dr.v[q];
+        s.v[q] = ds.v[q];
+      }
+      const u256 nm = mod_m<N>();
+      if (dr.neg || dr.big || ds.neg || ds.big || u256_iszero(r) || u256_iszero(s) || u256_geq(r, nm) ||
+          u256_geq(s, nm))
+        st = kStatusBadSig;
+    }
+  }
+  if (st == kEcPending) {
+    uint32_t hw[8];
+    sha256_bytes(hw, msg, msg_len);
+    u256 e, t;
+#pragma unroll
+    for (int q = 0; q < 8; q++) e.v[q] = hw[7 - q];
+    if (!u256_sub(t, e, mod_m<N>())) e = t;
+    to_mont<N>(sm, s);
+    st256(rec + kEcE, e);
+    st256(rec + kEcR, r);
+    st_jpt(rec + kEcTab, Q);
+    jpt T;
+    jdbl<C>(T, Q);
+    st_jpt(rec + kEcTab + kEcPtWords, T);
+    for (int k = 3; k <= 8; k++) {
+      jmadd<C>(T, T, Q.X, Q.Y);  // Q has Z = 1
+      st_jpt(rec + kEcTab + kEcPtWords * (k - 1), T);
+    }
+  }
+  st256(rec + kEcS, sm);
+  return st;
+}
+
+// P = u1 G + u2 Q with w = s^-1 from the record; x(P) mod n == r
+template <class C>
+CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ gtab) {
+  using F = typename C::F;
+  using N = typename C::N;
+  u256 w, e, r, u1, u2;
+  ld256(w, rec + kEcW);
+  ld256(e, rec + kEcE);
+  ld256(r, rec + kEcR);
+  mont_mul<N>(u1, e, w);  // plain e * s^-1 (one Montgomery factor cancels)
+  mont_mul<N>(u2, r, w);
+  const uint32_t* tab = rec + kEcTab;
+  jpt acc;
+  acc.inf = true;
+  if constexpr (C::kGlv) {
+    // u1 G = [a1]G + [a2](lambda G), u2 Q = [b1]Q + [b2]phi(Q): 33 windows of 4 bits
+    u256 a1, a2, b1, b2;
+    bool na1, na2, nb1, nb2;
+    glv_split(a1, na1, a2, na2, u1);
+    glv_split(b1, nb1, b2, nb2, u2);
+    f29 beta;
+#pragma unroll
+    for (int i = 0; i < 9; i++) beta.v[i] = F::betam(i);
+    const uint32_t* gtab2 = gtab + kGEntries * kGEntryWords;
+    for (int j = 32; j >= 0; j--) {
+      const int d1 = booth_digit<4>(b1.v, j), d2 = booth_digit<4>(b2.v, j);
+      const int e1 = d1 < 0 ? -d1 : d1, e2 = d2 < 0 ? -d2 : d2;
+      jpt T1, T2;  // issued before the doublings, consumed after them
+      ld_jpt(T1, tab + kEcPtWords * (e1 > 0 ? e1 - 1 : 0));
+      ld_jpt(T2, tab + kEcPtWords * (e2 > 0 ? e2 - 1 : 0));
+      if (j != 32) {
+        jdbl<C>(acc, acc);
+        jdbl<C>(acc, acc);
+        jdbl<C>(acc, acc);
+        jdbl<C>(acc, acc);
+      }
+      if (e1) {
+        f29_cneg<F>(T1.Y, (d1 < 0) != nb1);
+        jadd<C>(acc, acc, T1);
+      }
+      if (e2) {
+        f29_mul<F>(T2.X, T2.X, beta);  // phi([e2]Q)
+        f29_cneg<F>(T2.Y, (d2 < 0) != nb2);
+        jadd<C>(acc, acc, T2);
+      }
+      if ((j & 1) == 0) {
+        const int g1 = booth_digit<8>(a1.v, j >> 1), g2 = booth_digit<8>(a2.v, j >> 1);
+        f29 gx, gy;
+        if (g1) {
+          load_g(gx, gy, gtab, g1 < 0 ? -g1 : g1);
+          f29_cneg<F>(gy, (g1 < 0) != na1);
+          jmadd<C>(acc, acc, gx, gy);
+        }
+        if (g2) {
+          load_g(gx, gy, gtab2, g2 < 0 ? -g2 : g2);
+          f29_cneg<F>(gy, (g2 < 0) != na2);
+          jmadd<C>(acc, acc, gx, gy);
+        }
+      }
+    }
+  } else {
+    bool neg1, neg2;
+    split_sign<N>(u1, neg1, u1);
+    split_sign<N>(u2, neg2, u2);
+    for (int j = 63; j >= 0; j--) {
+      const int dq = booth_digit<4>(u2.v, j);
+      const int aq = dq < 0 ? -dq : dq;
+      jpt T;  // issued before the doublings, consumed after them
+      ld_jpt(T, tab + kEcPtWords * (aq > 0 ? aq - 1 : 0));
+      if (j != 63) {
+        jdbl<C>(acc, acc);
+        jdbl<C>(acc, acc);
+        jdbl<C>(acc, acc);
+        jdbl<C>(acc, acc);
+      }
+      if (aq) {
+        f29_cneg<F>(T.Y, (dq < 0) != neg2);
+        jadd<C>(acc, acc, T);
+      }
+      if ((j & 1) == 0) {
+        const int dg = booth_digit<8>(u1.v, j >> 1);
+        if (dg) {
+          f29 gx, gy;
+          load_g(gx, gy, gtab, dg < 0 ? -dg : dg);
+          f29_cneg<F>(gy, (dg < 0) != neg1);
+          jmadd<C>(acc, acc, gx, gy);
+        }
+      }
+    }
+  }
+  return x_check<C>(acc, r);
+}
+
+// Fused single-kernel lane (A/B baseline, CORDAHIP_ECDSA=fused): the split
+// path's prep and ladder over a private record, with a per-lane Fermat inversion.
 template <class C>
 CDEV uint8_t ecdsa_verify_lane(const uint8_t* __restrict__ key, uint32_t key_len, const uint8_t* __restrict__ sig,
                                uint32_t sig_len, const uint8_t* __restrict__ msg, uint64_t msg_len,
                                const uint32_t* __restrict__ gtab, uint8_t pre_status) {
-  using P = typename C::P;
-  using N = typename C::N;
-  jpt Q;
-  if (!decode_key<C>(Q, key, key_len)) return kStatusBadKey;  // key built before verify
-  if (pre_status != kStatusOk) return pre_status;
-  if (sig_len == 0 || msg_len == 0) return kStatusEmpty;      // Crypto.kt:475-476
-  DerInt dr, ds;
-  if (!der_decode_sig(sig, sig_len, dr, ds)) return kStatusMalformedSig;
-  u256 r, s;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    r.v[i] = dr.v[i];
-    s.v[i] = ds.v[i];
-  }
-  const u256 nm = mod_m<N>();
-  if (dr.neg || dr.big || ds.neg || ds.big || u256_iszero(r) || u256_iszero(s) || u256_geq(r, nm) ||
-      u256_geq(s, nm))
-    return kStatusBadSig;
-  // e = SHA-256(msg) as a big-endian integer, reduced below n
-  uint32_t hw[8];
-  sha256_bytes(hw, msg, msg_len);
-  u256 e;
-#pragma unroll
-  for (int i = 0; i < 8; i++) e.v[i] = hw[7 - i];
-  {
-    u256 t;
-    if (!u256_sub(t, e, nm)) e = t;
-  }
-  // w = s^-1 (Montgomery), u1 = e w, u2 = r w (plain: one Montgomery factor cancels)
-  u256 sm, w, u1, u2;
-  to_mont<N>(sm, s);
-  mont_pow_const<N, typename C::Nm2>(w, sm);
-  mont_mul<N>(u1, e, w);
-  mont_mul<N>(u2, r, w);
-  bool neg1, neg2;
-  split_sign<N>(u1, neg1, u1);
-  split_sign<N>(u2, neg2, u2);
-  // per-lane table: [k]Q, k = 1..8
-  jpt qt[8];
-  qt[0] = Q;
-  jdbl<C>(qt[1], Q);
-  for (int k = 2; k < 8; k++) jadd<C>(qt[k], qt[k - 1], Q);
-  jpt acc;
-  acc.inf = true;
-  for (int j = 63; j >= 0; j--) {
-    if (j != 63) {
-      jdbl<C>(acc, acc);
-      jdbl<C>(acc, acc);
-      jdbl<C>(acc, acc);
-      jdbl<C>(acc, acc);
-    }
-    const int dq = booth_digit<4>(u2.v, j);
-    if (dq != 0) {
-      jpt T = qt[(dq < 0 ? -dq : dq) - 1];
-      if ((dq < 0) != neg2) mod_neg<P>(T.Y, T.Y);
-      jadd<C>(acc, acc, T);
-    }
-    if ((j & 1) == 0) {
-      const int dg = booth_digit<8>(u1.v, j >> 1);
-      if (dg != 0) {
-        u256 gx, gy;
-        load_g(gx, gy, gtab, dg < 0 ? -dg : dg);
-        if ((dg < 0) != neg1) mod_neg<P>(gy, gy);
-        jmadd<C>(acc, acc, gx, gy);
-      }
-    }
-  }
-  if (acc.inf) return kStatusBadSig;
-  // x(P) mod n == r  <=>  X == r Z^2  or (r < p - n and X == (r + n) Z^2)
-  u256 z2, rm, t;
-  mont_sqr<P>(z2, acc.Z);
-  to_mont<P>(rm, r);
-  mont_mul<P>(t, rm, z2);
-  if (u256_eq(t, acc.X)) return kStatusOk;
-  if (!u256_geq(r, limbs_of<typename C::PmN>())) {
-    u256 rn;
-    u256_add(rn, r, nm);
-    to_mont<P>(rm, rn);
-    mont_mul<P>(t, rm, z2);
-    if (u256_eq(t, acc.X)) return kStatusOk;
-  }
-  return kStatusBadSig;
+  __attribute__((aligned(16))) uint32_t rec[kEcWords];
+  const uint8_t st = ecdsa_prep_lane<C>(key, key_len, sig, sig_len, msg, msg_len, pre_status, rec);
+  if (st != kEcPending) return st;
+  u256 sm, w;
+  ld256(sm, rec + kEcS);
+  mont_pow_const<typename C::N, typename C::Nm2>(w, sm);
+  st256(rec + kEcW, w);
+  return ecdsa_ladder_lane<C>(rec, gtab);
 }
 
 // ---- signing (corpus generation for the C3 / C5 benchmarks) -----------------
@@ -498,6 +738,7 @@ CDEV uint8_t ecdsa_verify_lane(const uint8_t* __restrict__ key, uint32_t key_len
 // synthetic nonces: this is test-data generation, not a production signer).
 template <class C>
 CDEV void fixed_base_g(jpt& acc, const u256& k, const uint32_t* __restrict__ gtab) {
+  using F = typename C::F;
   u256 kk;
   bool neg;
   split_sign<typename C::N>(kk, neg, k);
@@ -507,25 +748,27 @@ CDEV void fixed_base_g(jpt& acc, const u256& k, const uint32_t* __restrict__ gta
       for (int t = 0; t < 8; t++) jdbl<C>(acc, acc);
     const int d = booth_digit<8>(kk.v, j);
     if (d != 0) {
-      u256 gx, gy;
+      f29 gx, gy;
       load_g(gx, gy, gtab, d < 0 ? -d : d);
-      if ((d < 0) != neg) mod_neg<typename C::P>(gy, gy);
+      f29_cneg<F>(gy, (d < 0) != neg);
       jmadd<C>(acc, acc, gx, gy);
     }
   }
 }
 
 template <class C>
-CDEV void to_affine(u256& x, u256& y, const jpt& p) {  // plain (non-Montgomery) coordinates
-  using P = typename C::P;
-  u256 zi, zi2;
-  mont_pow_const<P, typename C::Pm2>(zi, p.Z);
-  mont_sqr<P>(zi2, zi);
-  mont_mul<P>(x, p.X, zi2);
-  mont_mul<P>(zi2, zi2, zi);
-  mont_mul<P>(y, p.Y, zi2);
-  from_mont<P>(x, x);
-  from_mont<P>(y, y);
+CDEV void to_affine(u256& x, u256& y, const jpt& p) {  // plain coordinates
+  using F = typename C::F;
+  f29 zi, zi2, X, Y;
+  f29_pow_const<F, typename C::Pm2>(zi, p.Z);
+  f29_sqr<F>(zi2, zi);
+  f29_mul<F>(X, p.X, zi2);
+  f29_mul<F>(zi2, zi2, zi);
+  f29_mul<F>(Y, p.Y, zi2);
+  f29_from_mont<F>(X, X);
+  f29_from_mont<F>(Y, Y);
+  f29_to_words(x.v, X);
+  f29_to_words(y.v, Y);
 }
 
 CDEV void put_be32(uint8_t* o, const u256& v) {
@@ -702,104 +945,6 @@ __global__ void __launch_bounds__(256) verdict_kernel(const uint8_t* __restrict_
 }
 
 // ---- split verification (default): prep -> batch inversion -> ladder --------
-// Slots are the curve-partitioned order (perm), processed in chunks of
-// ws_slots; each slot owns a 896-B workspace record in HBM.
-static constexpr int kEcTab = 0;             // [k]Q, k = 1..8: Jacobian X, Y, Z (Montgomery), 24 words each
-static constexpr int kEcS = 8 * 24;          // s, Montgomery form mod n (batch-inversion input)
-static constexpr int kEcW = kEcS + 8;        // prefix products, then w = s^-1 (Montgomery form mod n)
-static constexpr int kEcE = kEcW + 8;        // e = SHA-256(msg) mod n
-static constexpr int kEcR = kEcE + 8;        // r
-static constexpr int kEcWords = kEcR + 8;    // 224 words = 896 B
-static constexpr int kEcInvBatch = 16;       // signatures per thread in the batch inversion
-static constexpr uint8_t kEcPending = 0xff;  // slot whose verdict the ladder decides
-
-CDEV void st256(uint32_t* __restrict__ o, const u256& v) {
-  uint4* o4 = reinterpret_cast<uint4*>(o);
-  o4[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
-  o4[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
-}
-CDEV void ld256(u256& v, const uint32_t* __restrict__ p) {
-  const uint4* p4 = reinterpret_cast<const uint4*>(p);
-  const uint4 a = p4[0], b = p4[1];
-  v.v[0] = a.x; v.v[1] = a.y; v.v[2] = a.z; v.v[3] = a.w;
-  v.v[4] = b.x; v.v[5] = b.y; v.v[6] = b.z; v.v[7] = b.w;
-}
-CDEV void st_jpt(uint32_t* __restrict__ o, const jpt& p) {
-  st256(o, p.X);
-  st256(o + 8, p.Y);
-  st256(o + 16, p.Z);
-}
-CDEV void ld_jpt(jpt& p, const uint32_t* __restrict__ o) {
-  ld256(p.X, o);
-  ld256(p.Y, o + 8);
-  ld256(p.Z, o + 16);
-  p.inf = false;
-}
-
-// Everything before the scalar multiplication, in the reference's order (key
-// decode, Crypto.doVerify's require()s, DER, range checks), then e, s, r and
-// the [k]Q table go to the slot's record. Decided lanes store s = 1 so the
-// batch product stays invertible.
-template <class C>
-CDEV uint8_t ecdsa_prep_lane(const uint8_t* __restrict__ key, uint32_t key_len, const uint8_t* __restrict__ sig,
-                             uint32_t sig_len, const uint8_t* __restrict__ msg, uint64_t msg_len, uint8_t pre_status,
-                             uint32_t* __restrict__ rec) {
-  using N = typename C::N;
-  u256 sm;
-  {
-    u256 one;
-#pragma unroll
-    for (int q = 0; q < 8; q++) one.v[q] = q == 0;
-    to_mont<N>(sm, one);
-  }
-  jpt Q;
-  uint8_t st = kEcPending;
-  u256 r, s;
-  if (!decode_key<C>(Q, key, key_len)) {
-    st = kStatusBadKey;  // key built before verify
-  } else if (pre_status != kStatusOk) {
-    st = pre_status;
-  } else if (sig_len == 0 || msg_len == 0) {
-    st = kStatusEmpty;  // Crypto.kt:475-476
-  } else {
-    DerInt dr, ds;
-    if (!der_decode_sig(sig, sig_len, dr, ds)) {
-      st = kStatusMalformedSig;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        r.v[q] = dr.v[q];
-        s.v[q] = ds.v[q];
-      }
-      const u256 nm = mod_m<N>();
-      if (dr.neg || dr.big || ds.neg || ds.big || u256_iszero(r) || u256_iszero(s) || u256_geq(r, nm) ||
-          u256_geq(s, nm))
-        st = kStatusBadSig;
-    }
-  }
-  if (st == kEcPending) {
-    uint32_t hw[8];
-    sha256_bytes(hw, msg, msg_len);
-    u256 e, t;
-#pragma unroll
-    for (int q = 0; q < 8; q++) e.v[q] = hw[7 - q];
-    if (!u256_sub(t, e, mod_m<N>())) e = t;
-    to_mont<N>(sm, s);
-    st256(rec + kEcE, e);
-    st256(rec + kEcR, r);
-    st_jpt(rec + kEcTab, Q);
-    jpt T;
-    jdbl<C>(T, Q);
-    st_jpt(rec + kEcTab + 24, T);
-    for (int k = 3; k <= 8; k++) {
-      jadd<C>(T, T, Q);
-      st_jpt(rec + kEcTab + 24 * (k - 1), T);
-    }
-  }
-  st256(rec + kEcS, sm);
-  return st;
-}
-
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ecdsa_prep_kernel(
     const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, const uint8_t* __restrict__ keys,
     const uint8_t* __restrict__ key_len, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ sig_len,
@@ -875,65 +1020,6 @@ __global__ void __launch_bounds__(256) ecdsa_inv_kernel(uint64_t base, uint64_t 
   }
 }
 
-// P = u1 G + u2 Q with w = s^-1 from the batch inversion; x(P) mod n == r
-template <class C>
-CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ gtab) {
-  using P = typename C::P;
-  using N = typename C::N;
-  u256 w, e, r, u1, u2;
-  ld256(w, rec + kEcW);
-  ld256(e, rec + kEcE);
-  ld256(r, rec + kEcR);
-  mont_mul<N>(u1, e, w);  // plain e * s^-1 (one Montgomery factor cancels)
-  mont_mul<N>(u2, r, w);
-  bool neg1, neg2;
-  split_sign<N>(u1, neg1, u1);
-  split_sign<N>(u2, neg2, u2);
-  jpt acc;
-  acc.inf = true;
-  for (int j = 63; j >= 0; j--) {
-    const int dq = booth_digit<4>(u2.v, j);
-    const int aq = dq < 0 ? -dq : dq;
-    jpt T;  // issued before the doublings, consumed after them
-    ld_jpt(T, rec + kEcTab + 24 * (aq > 0 ? aq - 1 : 0));
-    if (j != 63) {
-      jdbl<C>(acc, acc);
-      jdbl<C>(acc, acc);
-      jdbl<C>(acc, acc);
-      jdbl<C>(acc, acc);
-    }
-    if (dq != 0) {
-      if ((dq < 0) != neg2) mod_neg<P>(T.Y, T.Y);
-      jadd<C>(acc, acc, T);
-    }
-    if ((j & 1) == 0) {
-      const int dg = booth_digit<8>(u1.v, j >> 1);
-      if (dg != 0) {
-        u256 gx, gy;
-        load_g(gx, gy, gtab, dg < 0 ? -dg : dg);
-        if ((dg < 0) != neg1) mod_neg<P>(gy, gy);
-        jmadd<C>(acc, acc, gx, gy);
-      }
-    }
-  }
-  if (acc.inf) return kStatusBadSig;
-  // x(P) mod n == r  <=>  X == r Z^2  or (r < p - n and X == (r + n) Z^2)
-  const u256 nm = mod_m<N>();
-  u256 z2, rm, t;
-  mont_sqr<P>(z2, acc.Z);
-  to_mont<P>(rm, r);
-  mont_mul<P>(t, rm, z2);
-  if (u256_eq(t, acc.X)) return kStatusOk;
-  if (!u256_geq(r, limbs_of<typename C::PmN>())) {
-    u256 rn;
-    u256_add(rn, r, nm);
-    to_mont<P>(rm, rn);
-    mont_mul<P>(t, rm, z2);
-    if (u256_eq(t, acc.X)) return kStatusOk;
-  }
-  return kStatusBadSig;
-}
-
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ecdsa_ladder_kernel(
     const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, uint64_t base, uint64_t m,
     const uint32_t* __restrict__ gtab_k1, const uint32_t* __restrict__ gtab_r1, const uint32_t* __restrict__ ws,
@@ -948,7 +1034,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
 }
 
 // ---------------------------------------------------------------------------
-size_t ecdsa_gtable_bytes() { return (size_t)kGEntries * kGEntryWords * sizeof(uint32_t); }
+size_t ecdsa_gtable_bytes() { return (size_t)kGTables * kGEntries * kGEntryWords * sizeof(uint32_t); }
 size_t ecdsa_ws_slot_bytes() { return kEcWords * sizeof(uint32_t); }
 
 hipError_t launch_ecdsa_sign(const uint8_t* scheme, const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len,
@@ -961,8 +1047,9 @@ hipError_t launch_ecdsa_sign(const uint8_t* scheme, const uint8_t* seeds, const 
 }
 
 hipError_t launch_ecdsa_gtables(uint32_t* k1, uint32_t* r1, hipStream_t s) {
-  hipLaunchKernelGGL(ecdsa_gtable_kernel<Curve<2>>, dim3((kGEntries + 63) / 64), dim3(64), 0, s, k1);
-  hipLaunchKernelGGL(ecdsa_gtable_kernel<Curve<3>>, dim3((kGEntries + 63) / 64), dim3(64), 0, s, r1);
+  const dim3 g((kGTables * kGEntries + 63) / 64);
+  hipLaunchKernelGGL(ecdsa_gtable_kernel<Curve<2>>, g, dim3(64), 0, s, k1);
+  hipLaunchKernelGGL(ecdsa_gtable_kernel<Curve<3>>, g, dim3(64), 0, s, r1);
   return hipGetLastError();
 }
 

@@ -1,0 +1,298 @@
+// Base-field arithmetic of the two ECDSA curves (secp256k1, P-256) for
+// gfx950 lanes: kernel K2's ladder, point tables and key decode.
+//
+// Representation: 9 unsigned 32-bit limbs in radix 2^29 (261 bits),
+// Montgomery form with R = 2^261. Why this shape on CDNA4: a 32x32->64
+// v_mad_u64_u32 issues at the same rate as an add (profiles/r01_int_rates.jsonl),
+// so a field product costs its instruction count. With 29-bit limbs every
+// column of the product AND of the Montgomery reduction (<= 9 + 9 terms of
+// < 2^60) stays below 2^64: each partial product is ONE v_mad_u64_u32 into a
+// 64-bit column accumulator, no carry instruction, and the column carry rides
+// in the next column's addend. The saturated 8 x 32-bit Montgomery product
+// (mp256.hpp, still used for the scalar field mod n) needs a v_addc_co_u32
+// per partial product: ~1.5-2x the instructions.
+//
+// Lazy reduction (all bounds exact; modelled limb for limb, with assertions,
+// by tests/test_fp29_model.py):
+//   "norm"  limbs 0..7 < 2^29 (limbs 0, 1 may exceed it by < 2^15 after
+//           f29_red), value < 2p. Outputs of f29_mul / f29_sqr / f29_red.
+//   f29_mul(a, b): needs a * b < 2^261 p (e.g. a, b < 4p, or 2p x 16p) and
+//           limb products <= 2^60.5 (both limbs <= 2^30.25, or one <= 2^29 and
+//           the other <= 2^31.5). Output norm, < 2p.
+//   f29_add: limb-wise, no carry (values and limb bounds add).
+//   f29_sub(a, b) = a + 2p - b with one carry pass: b norm (value <= 2p),
+//           a limbs < 2^31; output limbs normalised, value < a + 2p.
+//   f29_red(a): limbs < 2^31.5, value < 2^260 -> norm (< 2p), by folding the
+//           bits above 2^256 with 2^256 == 2^256 - p (mod p).
+//   f29_canon: norm input -> the canonical residue in [0, p).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef CDEV
+#define CDEV __device__ __forceinline__
+#endif
+
+namespace cordahip {
+
+static constexpr uint32_t kMask29 = (1u << 29) - 1;
+
+struct f29 {
+  uint32_t v[9];
+};
+
+// A compile-time constant moved into an SGPR behind an empty asm: q * m then
+// stays one v_mad_u64_u32 per limb (with the constant visible, InstCombine
+// rewrites q * (2^29 - 1) as a 64-bit shift-subtract and factors equal
+// constants out of a column's sum).
+CDEV uint32_t sconst(uint32_t x) {
+  asm("" : "+s"(x));
+  return x;
+}
+
+// r = a b R^-1 mod p (norm, < 2p). Product scanning (FIPS): column k
+// accumulates a_j b_{k-j} and q_j m_{k-j}; for k < 9 the column then picks q_k
+// so that its low 29 bits vanish.
+template <class F>
+CDEV void f29_mul(f29& r, const f29& a, const f29& b) {
+  uint32_t q[9], mk[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) mk[i] = F::m(i) ? sconst(F::m(i)) : 0u;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      acc += (uint64_t)a.v[j] * b.v[k - j];
+      if (F::m(k - j)) acc += (uint64_t)q[j] * mk[k - j];
+    }
+    acc += (uint64_t)a.v[k] * b.v[0];
+    q[k] = (F::kMinvOne ? (uint32_t)acc : (uint32_t)acc * F::kMinv) & kMask29;
+    acc += (uint64_t)q[k] * mk[0];
+    acc >>= 29;
+  }
+  f29 t;
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+#pragma unroll
+    for (int j = k - 8; j < 9; j++) {
+      acc += (uint64_t)a.v[j] * b.v[k - j];
+      if (F::m(k - j)) acc += (uint64_t)q[j] * mk[k - j];
+    }
+    t.v[k - 9] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+  }
+  t.v[8] = (uint32_t)acc;
+  r = t;  // r may alias a or b
+}
+
+// r = a^2 R^-1 mod p: 45 distinct limb products (off-diagonal ones doubled)
+template <class F>
+CDEV void f29_sqr(f29& r, const f29& a) {
+  uint32_t q[9], mk[9], a2[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    mk[i] = F::m(i) ? sconst(F::m(i)) : 0u;
+    a2[i] = a.v[i] << 1;
+  }
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+#pragma unroll
+    for (int j = 0; 2 * j < k; j++) acc += (uint64_t)a2[j] * a.v[k - j];
+    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+#pragma unroll
+    for (int j = 0; j < k; j++)
+      if (F::m(k - j)) acc += (uint64_t)q[j] * mk[k - j];
+    q[k] = (F::kMinvOne ? (uint32_t)acc : (uint32_t)acc * F::kMinv) & kMask29;
+    acc += (uint64_t)q[k] * mk[0];
+    acc >>= 29;
+  }
+  f29 t;
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+#pragma unroll
+    for (int j = k - 8; 2 * j < k; j++) acc += (uint64_t)a2[j] * a.v[k - j];
+    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+#pragma unroll
+    for (int j = k - 8; j < 9; j++)
+      if (F::m(k - j)) acc += (uint64_t)q[j] * mk[k - j];
+    t.v[k - 9] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+  }
+  t.v[8] = (uint32_t)acc;
+  r = t;
+}
+
+CDEV void f29_add(f29& r, const f29& a, const f29& b) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = a.v[i] + b.v[i];
+}
+
+// r = a + 2p - b, one carry pass. F::sub2p is 2p written with limbs 0..7 >=
+// 2^29 - 1 (each borrowed from the limb above), so no limb goes negative for a
+// norm b; the top limb may wrap transiently, the total stays >= 0.
+template <class F>
+CDEV void f29_sub(f29& r, const f29& a, const f29& b) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a.v[i] + F::sub2p(i) - b.v[i] + c;
+    r.v[i] = t & kMask29;
+    c = t >> 29;
+  }
+  r.v[8] = a.v[8] + F::sub2p(8) - b.v[8] + c;
+}
+
+// conditional negation (2p - a for a norm a), branch-free
+template <class F>
+CDEV void f29_cneg(f29& r, bool neg) {
+  f29 z, n;
+#pragma unroll
+  for (int i = 0; i < 9; i++) z.v[i] = 0;
+  f29_sub<F>(n, z, r);
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = neg ? n.v[i] : r.v[i];
+}
+
+// limbs < 2^31.5, value < 2^260  ->  norm, value < 2p
+template <class F>
+CDEV void f29_red(f29& r, const f29& a) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a.v[i] + c;
+    r.v[i] = t & kMask29;
+    c = t >> 29;
+  }
+  const uint32_t top = a.v[8] + c;
+  const uint32_t q = top >> 24;  // the value's bits >= 2^256 (q < 16)
+  r.v[8] = top & 0xffffffu;
+  if (F::kRed == 1) {
+    // secp256k1: 2^256 == 2^32 + 977 (mod p); 2^32 = 2^29 * 8
+    r.v[0] += q * 977u;
+    r.v[1] += q << 3;
+  } else {
+    // P-256: 2^256 == 2^224 - 2^192 - 2^96 + 1 (mod p); bit 96 is limb 3 bit 9,
+    // bit 192 limb 6 bit 18, bit 224 limb 7 bit 21. Limbs 3 and 6 may go
+    // negative: one signed carry pass over limbs 3..7 (the total is >= 0).
+    r.v[0] += q;
+    r.v[3] -= q << 9;
+    r.v[6] -= q << 18;
+    r.v[7] += q << 21;
+#pragma unroll
+    for (int i = 3; i < 8; i++) {
+      const int32_t cs = (int32_t)r.v[i] >> 29;
+      r.v[i] &= kMask29;
+      r.v[i + 1] += (uint32_t)cs;
+    }
+  }
+}
+
+// canonical residue in [0, p), limbs fully normalised
+template <class F>
+CDEV void f29_canon(f29& r, const f29& a) {
+  f29 t;
+  f29_red<F>(t, a);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t s = t.v[i] + c;
+    t.v[i] = s & kMask29;
+    c = s >> 29;
+  }
+  t.v[8] += c;
+  f29 d;  // t - p, kept when there is no borrow
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint32_t s = t.v[i] - F::m(i) - br;
+    d.v[i] = s & kMask29;
+    br = s >> 31;
+  }
+  const bool ge = br == 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = ge ? d.v[i] : t.v[i];
+}
+
+template <class F>
+CDEV bool f29_iszero(const f29& a) {
+  f29 c;
+  f29_canon<F>(c, a);
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) x |= c.v[i];
+  return x == 0;
+}
+
+template <class F>
+CDEV bool f29_eq(const f29& a, const f29& b) {
+  f29 x, y;
+  f29_canon<F>(x, a);
+  f29_canon<F>(y, b);
+  uint32_t d = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) d |= x.v[i] ^ y.v[i];
+  return d == 0;
+}
+
+// 8 little-endian 32-bit words (value < 2^256) <-> 29-bit limbs
+CDEV void f29_from_words(f29& r, const uint32_t w[8]) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int lo = 29 * i, wi = lo >> 5, sh = lo & 31;
+    const uint64_t x = (uint64_t)w[wi] | (wi + 1 < 8 ? (uint64_t)w[wi + 1] << 32 : 0ull);
+    r.v[i] = (uint32_t)(x >> sh) & kMask29;
+  }
+}
+// a: canonical (fully normalised limbs, value < 2^256)
+CDEV void f29_to_words(uint32_t w[8], const f29& a) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int lo = 32 * k, li = lo / 29, sh = lo % 29;
+    uint64_t x = (uint64_t)a.v[li] >> sh;
+    x |= (uint64_t)a.v[li + 1] << (29 - sh);
+    if (li + 2 < 9 && 58 - sh < 32) x |= (uint64_t)a.v[li + 2] << (58 - sh);
+    w[k] = (uint32_t)x;
+  }
+}
+
+template <class F>
+CDEV void f29_const_one(f29& r) {  // R mod p: 1 in Montgomery form
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = F::one(i);
+}
+
+// plain x < 2^256  ->  Montgomery form x R mod p (norm)
+template <class F>
+CDEV void f29_to_mont(f29& r, const f29& x) {
+  f29 r2;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r2.v[i] = F::r2(i);
+  f29_mul<F>(r, x, r2);
+}
+// Montgomery form -> canonical plain residue
+template <class F>
+CDEV void f29_from_mont(f29& r, const f29& a) {
+  f29 one;
+#pragma unroll
+  for (int i = 0; i < 9; i++) one.v[i] = i == 0;
+  f29_mul<F>(r, a, one);
+  f29_canon<F>(r, r);
+}
+
+// a^e for a compile-time exponent E (8 x 32-bit limbs)
+template <class F, class E>
+CDEV void f29_pow_const(f29& r, const f29& a) {
+  f29 acc = a;
+  int top = 255;
+  while (top > 0 && !((E::limb(top >> 5) >> (top & 31)) & 1)) top--;
+#pragma unroll 1
+  for (int i = top - 1; i >= 0; i--) {
+    f29_sqr<F>(acc, acc);
+    if ((E::limb(i >> 5) >> (i & 31)) & 1) f29_mul<F>(acc, acc, a);
+  }
+  r = acc;
+}
+
+}  // namespace cordahip

@@ -138,16 +138,15 @@ __global__ void __launch_bounds__(256) tx_reduce_kernel(const uint8_t* __restric
                                                        int64_t* __restrict__ first_bad, uint8_t* __restrict__ tx_status) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntx) return;
-  if (tx_status[t] != kStatusOk) {  // no leaves: the id itself could not be computed
-    first_bad[t] = -1;
-    return;
-  }
   const uint64_t lo = tx_sig_off[t], hi = tx_sig_off[t + 1];
+  first_bad[t] = -1;
+  // require(sigs.isNotEmpty()) runs in the constructor (SignedTransaction.kt:37-39),
+  // before the lazy tx.id can throw MerkleTreeException
   if (lo == hi) {
-    first_bad[t] = -1;
     tx_status[t] = kTxNoSignatures;
     return;
   }
+  if (tx_status[t] != kStatusOk) return;  // no leaves: the id itself could not be computed
   int64_t fb = -1;
   uint8_t st = kStatusOk;
   for (uint64_t s = lo; s < hi; s++) {

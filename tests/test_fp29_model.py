@@ -1,0 +1,316 @@
+"""Limb-level model of fp29.hpp (kernel K2's base-field arithmetic) and of
+ecdsa.hip's point formulas, run on the CPU.
+
+Each operation mirrors the device code step for step on Python ints and
+asserts what the device relies on: every 64-bit column accumulator of
+f29_mul / f29_sqr stays below 2^64, every 32-bit limb below 2^32, every
+Montgomery column clears its low 29 bits, and every result is the right
+residue inside its documented value bound (fp29.hpp header). The point
+formulas (jdbl for a = -3 and a = 0, jadd, jmadd, including their exceptional
+branches) run on random Jacobian representatives pushed to the top of the
+allowed range and are compared with the BouncyCastle restatement's affine
+arithmetic (oracle/bc_ecdsa.py, the checker). The constants come from
+tools/gen_fp29_consts.py; the committed header must match its output.
+"""
+import os
+import random
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import bc_ecdsa as ec  # noqa: E402  (oracle: checker only)
+import gen_fp29_consts as gen  # noqa: E402
+
+U32, U64 = 1 << 32, 1 << 64
+M29 = (1 << 29) - 1
+R = 1 << 261
+
+
+class Fp29:
+    def __init__(self, p, kred):
+        self.p, self.kred = p, kred
+        self.m = gen.limbs29(p)
+        self.minv = gen.minv29(p)
+        self.s2p = gen.sub2p(p)
+        self.r2 = gen.limbs29(R * R % p)
+        self.one = gen.limbs29(R % p)
+
+    @staticmethod
+    def val(a):
+        return sum(v << (29 * i) for i, v in enumerate(a))
+
+    def mul(self, a, b):
+        assert all(0 <= x < U32 for x in a + b)
+        va, vb = self.val(a), self.val(b)
+        assert va * vb < R * self.p, "Montgomery input bound a b < R p"
+        q, t, acc = [0] * 9, [0] * 9, 0
+        for k in range(17):
+            acc += sum(a[j] * b[k - j] for j in range(max(0, k - 8), min(k, 8) + 1))
+            acc += sum(q[j] * self.m[k - j] for j in range(max(0, k - 8), min(k, 9)))
+            if k < 9:
+                q[k] = ((acc % U32) * self.minv % U32) & M29
+                acc += q[k] * self.m[0]
+                assert acc & M29 == 0
+            else:
+                t[k - 9] = acc & M29
+            assert acc < U64, "column %d overflows" % k
+            acc >>= 29
+        t[8] = acc
+        assert t[8] < U32
+        assert self.val(t) % self.p == va * vb * pow(R, -1, self.p) % self.p
+        assert self.val(t) < 2 * self.p
+        return t
+
+    def sqr(self, a):
+        assert all(2 * x < U32 for x in a)  # the doubled operand a2[j] = a[j] << 1
+        return self.mul(a, a)               # same column sums as the symmetric schedule
+
+    @staticmethod
+    def add(a, b):
+        r = [x + y for x, y in zip(a, b)]
+        assert all(x < U32 for x in r)
+        return r
+
+    def sub(self, a, b):
+        assert self.val(b) <= 2 * self.p
+        r, c = [0] * 9, 0
+        for i in range(8):
+            t = a[i] + self.s2p[i] - b[i] + c
+            assert 0 <= t < U32
+            r[i], c = t & M29, t >> 29
+        r[8] = a[8] + self.s2p[8] - b[8] + c
+        assert 0 <= r[8] < U32
+        assert self.val(r) == self.val(a) + 2 * self.p - self.val(b)
+        return r
+
+    def red(self, a):
+        assert all(0 <= x < U32 for x in a) and self.val(a) < 1 << 260
+        r, c = [0] * 9, 0
+        for i in range(8):
+            t = a[i] + c
+            assert t < U32
+            r[i], c = t & M29, t >> 29
+        top = a[8] + c
+        assert top < U32
+        q = top >> 24
+        r[8] = top & 0xFFFFFF
+        if self.kred == 1:
+            r[0] += q * 977
+            r[1] += q << 3
+        else:
+            r[0] += q
+            r[3] -= q << 9
+            r[6] -= q << 18
+            r[7] += q << 21
+            for i in range(3, 8):
+                assert -(1 << 31) <= r[i] < 1 << 31
+                cs = r[i] >> 29          # arithmetic shift, as (int32_t) >> 29
+                r[i] &= M29
+                r[i + 1] += cs
+        assert all(0 <= x < U32 for x in r)
+        assert all(x < (1 << 29) + (1 << 15) for x in r[:8])
+        assert self.val(r) % self.p == self.val(a) % self.p and self.val(r) < 2 * self.p
+        return r
+
+    def canon(self, a):
+        t = self.red(a)
+        c = 0
+        for i in range(8):
+            s = t[i] + c
+            t[i], c = s & M29, s >> 29
+        t[8] += c
+        d, br = [0] * 9, 0
+        for i in range(9):
+            s = (t[i] - self.m[i] - br) % U32
+            d[i], br = s & M29, s >> 31
+        r = d if br == 0 else t
+        assert self.val(r) == self.val(a) % self.p
+        return r
+
+    def iszero(self, a):
+        return not any(self.canon(a))
+
+    def neg(self, a):
+        return self.sub([0] * 9, a)
+
+    def to_mont(self, x):
+        return self.mul(gen.limbs29(x), self.r2)
+
+    def from_mont(self, a):
+        return self.val(self.canon(self.mul(a, [1] + [0] * 8)))
+
+
+FIELDS = {2: Fp29(gen.P_K1, 1), 3: Fp29(gen.P_R1, 2)}
+AM3 = {2: False, 3: True}
+
+
+# ---- ecdsa.hip's point formulas, op for op -----------------------------------
+def jdbl(F, am3, P):
+    if P is None:
+        return None
+    X, Y, Z = P
+    if am3:
+        delta, gamma = F.sqr(Z), F.sqr(Y)
+        beta = F.mul(X, gamma)
+        t, u = F.sub(X, delta), F.add(X, delta)
+        a3 = F.mul(t, u)
+        a3 = F.red(F.add(F.add(a3, a3), a3))
+        x3 = F.sqr(a3)
+        t = F.add(beta, beta)
+        b4 = F.red(F.add(t, t))
+        x3 = F.red(F.sub(F.sub(x3, b4), b4))
+        t = F.sqr(F.add(Y, Z))
+        z3 = F.red(F.sub(F.sub(t, gamma), delta))
+        y3 = F.mul(a3, F.sub(b4, x3))
+        u = F.sqr(F.add(gamma, gamma))
+        y3 = F.red(F.sub(F.sub(y3, u), u))
+    else:
+        A, B = F.sqr(X), F.sqr(Y)
+        C = F.sqr(B)
+        t = F.sub(F.sub(F.sqr(F.add(X, B)), A), C)
+        D = F.red(F.add(t, t))
+        E = F.red(F.add(F.add(A, A), A))
+        x3 = F.red(F.sub(F.sub(F.sqr(E), D), D))
+        y3 = F.mul(E, F.sub(D, x3))
+        t = F.add(C, C)
+        u = F.red(F.add(t, t))
+        y3 = F.red(F.sub(F.sub(y3, u), u))
+        z3 = F.mul(F.add(Y, Y), Z)
+    return (x3, y3, z3)
+
+
+def jadd(F, am3, P, Q):
+    if P is None:
+        return Q
+    if Q is None:
+        return P
+    (X1, Y1, Z1), (X2, Y2, Z2) = P, Q
+    z1z1, z2z2 = F.sqr(Z1), F.sqr(Z2)
+    u1, u2 = F.mul(X1, z2z2), F.mul(X2, z1z1)
+    s1 = F.mul(F.mul(Y1, Z2), z2z2)
+    s2 = F.mul(F.mul(Y2, Z1), z1z1)
+    h, rr = F.red(F.sub(u2, u1)), F.red(F.sub(s2, s1))
+    if F.iszero(h):
+        return jdbl(F, am3, P) if F.iszero(rr) else None
+    i = F.sqr(F.add(h, h))
+    j = F.mul(h, i)
+    rr = F.add(rr, rr)
+    v = F.mul(u1, i)
+    x3 = F.red(F.sub(F.sub(F.sub(F.sqr(rr), j), v), v))
+    y3 = F.mul(rr, F.sub(v, x3))
+    t = F.mul(s1, j)
+    y3 = F.red(F.sub(F.sub(y3, t), t))
+    t = F.sub(F.sub(F.sqr(F.add(Z1, Z2)), z1z1), z2z2)
+    return (x3, y3, F.mul(t, h))
+
+
+def jmadd(F, am3, P, x2, y2):
+    if P is None:
+        return (x2, y2, list(F.one))
+    X1, Y1, Z1 = P
+    z1z1 = F.sqr(Z1)
+    u2 = F.mul(x2, z1z1)
+    s2 = F.mul(F.mul(y2, Z1), z1z1)
+    h, rr = F.red(F.sub(u2, X1)), F.red(F.sub(s2, Y1))
+    if F.iszero(h):
+        return jdbl(F, am3, P) if F.iszero(rr) else None
+    hh = F.sqr(h)
+    i = F.add(hh, hh)
+    i = F.add(i, i)
+    j = F.mul(h, i)
+    rr = F.add(rr, rr)
+    v = F.mul(X1, i)
+    x3 = F.red(F.sub(F.sub(F.sub(F.sqr(rr), j), v), v))
+    y3 = F.mul(rr, F.sub(v, x3))
+    t = F.mul(Y1, j)
+    y3 = F.red(F.sub(F.sub(y3, t), t))
+    t = F.sub(F.sub(F.sqr(F.add(Z1, h)), z1z1), hh)
+    return (x3, y3, F.red(t))
+
+
+def affine(F, P):
+    if P is None:
+        return None
+    X, Y, Z = (F.from_mont(c) for c in P)
+    zi = pow(Z, -1, F.p)
+    return (X * zi * zi % F.p, Y * zi * zi * zi % F.p)
+
+
+def high(F, x, rng):
+    """Montgomery form of x as a norm value, pushed to [p, 2p) half the time."""
+    v = F.val(F.canon(F.to_mont(x)))
+    if rng.random() < 0.5 and v + F.p < 2 * F.p:
+        v += F.p
+    return gen.limbs29(v)
+
+
+def jacobian(F, pt, rng):
+    z = rng.randrange(1, F.p)
+    x, y = pt
+    return (high(F, x * z * z % F.p, rng), high(F, y * z * z * z % F.p, rng), high(F, z, rng))
+
+
+def rand_point(c, rng):
+    return ec._mul(c, rng.randrange(1, c.n), c.G)
+
+
+def test_header_matches_generator():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_fp29_consts.py"), "--check"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("scheme", [2, 3])
+def test_field_ops_extremes(scheme):
+    F = FIELDS[scheme]
+    rng = random.Random(scheme)
+    p = F.p
+    edge = [0, 1, p - 1, p, p + 1, 2 * p - 1, (1 << 256) - 1 if (1 << 256) - 1 < 2 * p else 2 * p - 2]
+    vals = edge + [rng.randrange(2 * p) for _ in range(200)]
+    for a in vals:
+        la = gen.limbs29(a)
+        for b in rng.sample(vals, 4):
+            lb = gen.limbs29(b)
+            F.mul(la, lb)
+            F.mul(F.add(la, la), F.add(lb, lb))           # 4p x 4p
+            F.sub(la, lb)
+            F.red(F.add(F.add(la, la), F.add(la, la)))    # 8p, limbs < 2^31
+        F.sqr(F.add(la, la))
+        assert F.val(F.canon(la)) == a % p
+        assert F.from_mont(F.to_mont(a % p)) == a % p
+
+
+@pytest.mark.parametrize("scheme", [2, 3])
+def test_point_formulas_vs_affine(scheme):
+    F, c, am3 = FIELDS[scheme], ec.CURVES[scheme], AM3[scheme]
+    rng = random.Random(10 + scheme)
+    for _ in range(25):
+        P, Q = rand_point(c, rng), rand_point(c, rng)
+        JP, JQ = jacobian(F, P, rng), jacobian(F, Q, rng)
+        assert affine(F, jdbl(F, am3, JP)) == ec._add(c, P, P)
+        assert affine(F, jadd(F, am3, JP, JQ)) == ec._add(c, P, Q)
+        xq, yq = high(F, Q[0], rng), high(F, Q[1], rng)
+        assert affine(F, jmadd(F, am3, JP, xq, yq)) == ec._add(c, P, Q)
+        # chained: outputs feed further ops (the ladder's shape)
+        S = jdbl(F, am3, jdbl(F, am3, jadd(F, am3, JP, JQ)))
+        assert affine(F, jmadd(F, am3, S, xq, yq)) == ec._add(c, ec._mul(c, 4, ec._add(c, P, Q)), Q)
+
+
+@pytest.mark.parametrize("scheme", [2, 3])
+def test_exceptional_additions(scheme):
+    F, c, am3 = FIELDS[scheme], ec.CURVES[scheme], AM3[scheme]
+    rng = random.Random(20 + scheme)
+    P = rand_point(c, rng)
+    JP, JP2 = jacobian(F, P, rng), jacobian(F, P, rng)
+    assert affine(F, jadd(F, am3, JP, JP2)) == ec._add(c, P, P)            # P + P -> doubling
+    negP = (P[0], (-P[1]) % F.p)
+    assert jadd(F, am3, JP, jacobian(F, negP, rng)) is None                 # P - P -> infinity
+    assert affine(F, jmadd(F, am3, JP, high(F, P[0], rng), high(F, P[1], rng))) == ec._add(c, P, P)
+    assert jmadd(F, am3, JP, high(F, P[0], rng), F.neg(high(F, P[1], rng))) is None
+
+
+def test_glv_split_bound():
+    assert gen.check() <= 129

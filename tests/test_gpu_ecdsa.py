@@ -120,6 +120,45 @@ def test_device_signer_matches_oracle(engine):
     assert (st.cpu().numpy() == 0).all()
 
 
+def _x_vector(ec, scheme, x_start, r_is_x, rng, tag):
+    """A valid signature whose R = u1 G + u2 Q has x(R) >= x_start (key solved for)."""
+    c = ec.CURVES[scheme]
+    n, xr = c.n, x_start
+    while True:
+        rhs = (xr ** 3 + c.a * xr + c.b) % c.p
+        yr = pow(rhs, (c.p + 1) // 4, c.p)
+        if yr * yr % c.p == rhs:
+            break
+        xr += 1
+    r = xr if r_is_x else xr - n
+    m = hashlib.sha256(b"xcheck-%d" % tag).digest()
+    e = int.from_bytes(hashlib.sha256(m).digest(), "big")
+    s = rng.randrange(1, n)
+    w = pow(s, n - 2, n)
+    u1, u2 = e * w % n, r * w % n
+    Q = ec._mul(c, pow(u2, n - 2, n), ec._add(c, (xr, yr), ec._mul(c, n - u1, c.G)))
+    pub = b"\x04" + Q[0].to_bytes(32, "big") + Q[1].to_bytes(32, "big")
+    return scheme, pub, ec.der_encode(r, s), m
+
+
+def test_x_coordinate_check_ranges(engine):
+    """The inversion-free x(P) mod n == r check on both of its branches: x(P) < n
+    (X == r Z^2) and x(P) in [n, p) (X == (r + n) Z^2), with x near n, near p and
+    at 2^255, on both curves, against the oracle."""
+    import bc_ecdsa as ec
+    rng = random.Random(33)
+    rows = []
+    for scheme in (2, 3):
+        c = ec.CURVES[scheme]
+        for start, r_is_x in ((c.n + 1, False), (c.n - 2**20, True), (c.p - 2**40, False), (2**255, True),
+                              (c.n + 2**100, False), (c.n + 2**100, True)):
+            rows.append(_x_vector(ec, scheme, start, r_is_x, rng, len(rows)))
+    st, _ = engine.verify_batch(*zip(*rows))
+    want = [ec.verify_status(*r) for r in rows]
+    assert [int(x) for x in st] == want
+    assert want.count(0) == 10  # the two r = x(P) >= n rows are range-rejected
+
+
 def test_batch_inversion_boundaries(engine, ec_vectors):
     """The split path inverts s in runs of 16 slots per thread (Montgomery's
     trick) over the curve-partitioned order: odd batch sizes, runs that straddle

@@ -66,12 +66,15 @@ def test_signed_tx_semantics(engine, oracle):
     sigs[2][0] = good[3][0]
     # tx3: one component byte changed -> the recomputed id no longer matches every signature
     txs[3][2] = bytes([txs[3][2][0] ^ 1]) + txs[3][2][1:]
-    # tx4: no signatures; tx5: no components
+    # tx4: no signatures; tx5: no components; tx6: neither (the constructor's
+    # require(sigs.isNotEmpty()), SignedTransaction.kt:37-39, fires before tx.id)
     sigs[4] = []
     txs[5] = []
+    txs.append([])
+    sigs.append([])
     got_ids, tx_st, first_bad, sig_st = engine.signed_tx_verify(txs, sigs)
-    assert list(tx_st) == [0, 1, 1, 1, 7, 6]
-    assert list(first_bad) == [-1, 1, 0, 0, -1, -1]
+    assert list(tx_st) == [0, 1, 1, 1, 7, 6, 7]
+    assert list(first_bad) == [-1, 1, 0, 0, -1, -1, -1]
     assert got_ids[0].tobytes() == ids[0].tobytes()
     flat = [x for per in sigs for x in per]
     assert len(sig_st) == len(flat)
