@@ -139,6 +139,28 @@ CDEV uint32_t mul19(uint32_t x) {
   return r;
 }
 
+// acc + a * b as ONE v_mad_u64_u32 the compiler cannot re-associate. With
+// plain C++ LLVM starts every column at 0 (for ILP) and adds the incoming
+// carry at the end with a separate 64-bit add -- one extra VALU op per column.
+// Opaque MACs keep the carry as the chain's initial addend; the independent
+// multiplications of a group operation supply the ILP instead.
+#ifndef FE_ASM_MAC
+#define FE_ASM_MAC 0  // 1 measured: microbench +2-6%, full C2 -4% (192.2 vs 184.9 ms); kept for A/B
+#endif
+CDEV uint64_t mac64(uint32_t a, uint32_t b, uint64_t acc) {
+#if FE_ASM_MAC == 2
+  uint64_t r;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(acc) : "vcc");
+  return r;
+#elif FE_ASM_MAC == 1
+  uint64_t r = acc + (uint64_t)a * b;
+  asm("" : "+v"(r));  // empty: only pins the association order
+  return r;
+#else
+  return acc + (uint64_t)a * b;
+#endif
+}
+
 CDEV void fe_fold_top(fe& r, uint64_t c) {
   const uint64_t t = (uint64_t)r.v[0] + c * 19u;
   r.v[0] = (uint32_t)t & M26;
@@ -167,7 +189,7 @@ CDEV void fe_mul(fe& r, const fe& f, const fe& g) {
       const bool oo = (i & 1) && (j & 1);
       const uint32_t a = oo ? f2[i] : f.v[i];
       const uint32_t b = wrap ? g19[j] : g.v[j];
-      acc += (uint64_t)a * b;
+      acc = mac64(a, b, acc);
     }
     o.v[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
     c = acc >> limb_bits(k);
@@ -224,7 +246,7 @@ CDEV void fe_sq(fe& r, const fe& f) {
       const int mult = (i < j ? 2 : 1) * (oo ? 2 : 1);  // 1, 2 or 4
       const uint32_t a = mult == 1 ? f.v[i] : (mult == 2 ? f2[i] : f4[i]);
       const uint32_t b = wrap ? f19[j] : f.v[j];
-      acc += (uint64_t)a * b;
+      acc = mac64(a, b, acc);
     }
     o.v[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
     c = acc >> limb_bits(k);
