@@ -109,6 +109,70 @@ class C2:
                 "single_thread_value": one / dt1, "wall_s": dt, "gpu_vs_port_mismatches_on_sample": mism}
 
 
+# ---- C1: the CPU reference path's own workload, all valid ------------------------
+class C1(C2):
+    """2^20 tuples, seed_i = SHA-256("C1" || u64 i), msg_i =
+    SHA-256("C1msg" || u64 i), key/sig by RFC 8032 (signed on the GPU). The GPU
+    line verifies the same 2^20 tuples; cpu_baseline times the C restatement at 1
+    thread and at `cores` threads, and OpenSSL 3 EVP_DigestVerify (an independent
+    CPU Ed25519, raw-key decode included per call like Crypto.doVerify's key
+    handling) on a sample, all on the same tuples."""
+
+    def __init__(self, eng, device, stream, rank, args):
+        import hashlib
+        import numpy as np
+        import torch
+        self.torch, self.eng, self.device, self.stream = torch, eng, device, stream
+        self.n = n = 1 << args.batch_log2
+        base = rank * n
+        seeds = np.frombuffer(b"".join(hashlib.sha256(b"C1" + (base + i).to_bytes(8, "little")).digest()
+                                       for i in range(n)), np.uint8).reshape(n, 32)
+        msgs = np.frombuffer(b"".join(hashlib.sha256(b"C1msg" + (base + i).to_bytes(8, "little")).digest()
+                                      for i in range(n)), np.uint8).reshape(n, 32)
+        sd = torch.from_numpy(seeds.copy()).to(device)
+        self.msgs = torch.from_numpy(msgs.copy()).to(device)
+        self.pubs = torch.empty((n, 32), dtype=torch.uint8, device=device)
+        self.sigs = torch.empty((n, 64), dtype=torch.uint8, device=device)
+        eng.ed25519_sign_device(sd, self.msgs, self.pubs, self.sigs, device=0, stream=stream)
+        torch.cuda.synchronize(device)
+        self.expected = torch.zeros(n, dtype=torch.int16, device=device)
+        self.status = torch.empty(n, dtype=torch.uint8, device=device)
+        self.verdict = torch.empty((n + 63) // 64, dtype=torch.int64, device=device)
+        self.units = n
+        self.macs = LIMB_MACS["ed25519"]
+        self.workload = "C1: Crypto.doVerify EDDSA_ED25519_SHA512 over 2^%d valid (key, sig, 32-byte txId) tuples" \
+                        % args.batch_log2
+        self.data = "synthetic: SURVEY §8(d) C1 seeds/messages, RFC 8032 keys and signatures made on the GPU"
+        self.config = {"batch_per_gpu": n, "msg_len": 32, "corrupt_frac": 0.0}
+
+    def cpu_baseline(self, sample):
+        out = C2.cpu_baseline(self, sample)
+        out["sample"] = out["sample"].replace("C2 batch (same corpus, 1% corrupted)", "C1 set (all valid)")
+        # OpenSSL 3 (libcrypto.so.3, present on the box) as an independent CPU reference
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+            import openssl_ed25519 as ossl
+            from concurrent.futures import ThreadPoolExecutor
+            ns = min(sample, 1 << 15)
+            k = self.pubs[:ns].cpu().numpy()
+            s = self.sigs[:ns].cpu().numpy()
+            m = self.msgs[:ns].cpu().numpy()
+            cores = _cores()
+
+            def run(lo):
+                return sum(bool(ossl.verify(bytes(k[i]), bytes(s[i]), bytes(m[i]))) for i in range(lo, ns, cores))
+
+            t0 = time.perf_counter()
+            with ThreadPoolExecutor(cores) as ex:
+                ok = sum(ex.map(run, range(cores)))
+            dt = time.perf_counter() - t0
+            out["openssl"] = {"value": ns / dt, "cores": cores, "sample": ns, "accepted": ok,
+                              "note": "EVP_PKEY_new_raw_public_key + EVP_DigestVerify per tuple via ctypes"}
+        except Exception as e:  # noqa: BLE001 - the independent reference is optional on a box without libcrypto
+            out["openssl"] = {"error": "%s: %s" % (type(e).__name__, e)}
+        return out
+
+
 # ---- C3: mixed secp256k1 / P-256 ECDSA ----------------------------------------
 class C3:
     kernel = "ecdsa_verify_kernel"
@@ -353,7 +417,7 @@ class C5:
                 "wall_s": t_ed + t_ec, "gpu_vs_port_mismatches_on_sample": mism}
 
 
-WORKLOADS = {"c2": C2, "c3": C3, "c4": C4, "c5": C5}
+WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c4": C4, "c5": C5}
 
 
 def main():
@@ -362,11 +426,13 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
-    ap.add_argument("--batch-log2", type=int, default=24)
+    ap.add_argument("--batch-log2", type=int, default=None, help="lanes per GPU (default 2^20 for c1, 2^24 otherwise)")
     ap.add_argument("--c4-txs", type=int, default=10_000_000 // 8)
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.batch_log2 is None:
+        args.batch_log2 = 20 if args.workload == "c1" else 24
 
     import torch
     import torch.distributed as dist
@@ -461,7 +527,7 @@ def main():
             "corpus_gen_s": t_gen,
         }
         if world == 1 and not args.no_cpu_baseline:
-            sample = args.cpu_sample or {"c2": 1 << 17, "c3": 1 << 16, "c4": 1 << 16, "c5": 1 << 16}[args.workload]
+            sample = args.cpu_sample or {"c1": 1 << 20, "c2": 1 << 17, "c3": 1 << 16, "c4": 1 << 16, "c5": 1 << 16}[args.workload]
             out["cpu_baseline"] = wl.cpu_baseline(min(sample, wl.units))
         print(json.dumps(out), flush=True)
     eng.close()
