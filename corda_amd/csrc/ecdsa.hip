@@ -491,7 +491,9 @@ static constexpr int kEcS = 8 * kEcPtWords;     // s, Montgomery form mod n (bat
 static constexpr int kEcW = kEcS + 8;           // prefix products, then w = s^-1 (Montgomery form mod n)
 static constexpr int kEcE = kEcW + 8;           // e = SHA-256(msg) mod n
 static constexpr int kEcR = kEcE + 8;           // r
-static constexpr int kEcWords = kEcR + 8;       // 256 words = 1 KiB
+static constexpr int kEcZ = kEcR + 8;           // prod of the table's Z (k = 2..8), Montgomery mod p (12 words)
+static constexpr int kEcZW = kEcZ + 12;         // prefix products, then that product's inverse (12 words)
+static constexpr int kEcWords = kEcZW + 12;     // 280 words = 1120 B
 static constexpr int kEcInvBatch = 16;          // signatures per thread in the batch inversion
 static constexpr uint8_t kEcPending = 0xff;     // slot whose verdict the ladder decides
 
@@ -506,6 +508,42 @@ CDEV void ld256(u256& v, const uint32_t* __restrict__ p) {
   v.v[0] = a.x; v.v[1] = a.y; v.v[2] = a.z; v.v[3] = a.w;
   v.v[4] = b.x; v.v[5] = b.y; v.v[6] = b.z; v.v[7] = b.w;
 }
+CDEV void st_f29(uint32_t* __restrict__ o, const f29& a) {
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+  o4[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  o4[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+  o4[2] = make_uint4(a.v[8], 0u, 0u, 0u);
+}
+CDEV void ld_f29(f29& a, const uint32_t* __restrict__ o) {
+  const uint4* o4 = reinterpret_cast<const uint4*>(o);
+  const uint4 x = o4[0], y = o4[1], z = o4[2];
+  a.v[0] = x.x; a.v[1] = x.y; a.v[2] = x.z; a.v[3] = x.w;
+  a.v[4] = y.x; a.v[5] = y.y; a.v[6] = y.z; a.v[7] = y.w; a.v[8] = z.x;
+}
+// Z of a Jacobian table slot (words 18..26: not 16-B aligned, dword loads)
+CDEV void ld_slot_z(f29& z, const uint32_t* __restrict__ slot) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) z.v[i] = slot[18 + i];
+}
+// affine table entry: X, Y in the first 18 words of a kEcPtWords slot (five 16-B loads)
+CDEV void ld_aff(f29& x, f29& y, const uint32_t* __restrict__ o) {
+  const uint4* o4 = reinterpret_cast<const uint4*>(o);
+  uint32_t w[20];
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    const uint4 v = o4[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    x.v[i] = w[i];
+    y.v[i] = w[9 + i];
+  }
+}
+
 CDEV void st_jpt(uint32_t* __restrict__ o, const jpt& p) {
   uint32_t w[28];
 #pragma unroll
@@ -569,6 +607,9 @@ CDEV uint8_t ecdsa_prep_lane(const uint8_t* __restrict__ key, uint32_t key_len, 
                              uint32_t sig_len, const uint8_t* __restrict__ msg, uint64_t msg_len, uint8_t pre_status,
                              uint32_t* __restrict__ rec) {
   using N = typename C::N;
+  using F = typename C::F;
+  f29 zprod;
+  f29_const_one<F>(zprod);
   u256 sm;
   {
     u256 one;
@@ -615,12 +656,15 @@ CDEV uint8_t ecdsa_prep_lane(const uint8_t* __restrict__ key, uint32_t key_len, 
     jpt T;
     jdbl<C>(T, Q);
     st_jpt(rec + kEcTab + kEcPtWords, T);
+    zprod = T.Z;
     for (int k = 3; k <= 8; k++) {
       jmadd<C>(T, T, Q.X, Q.Y);  // Q has Z = 1
       st_jpt(rec + kEcTab + kEcPtWords * (k - 1), T);
+      f29_mul<F>(zprod, zprod, T.Z);
     }
   }
   st256(rec + kEcS, sm);
+  st_f29(rec + kEcZ, zprod);  // decided lanes: 1, so the batch product stays invertible
   return st;
 }
 
@@ -651,9 +695,9 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
     for (int j = 32; j >= 0; j--) {
       const int d1 = booth_digit<4>(b1.v, j), d2 = booth_digit<4>(b2.v, j);
       const int e1 = d1 < 0 ? -d1 : d1, e2 = d2 < 0 ? -d2 : d2;
-      jpt T1, T2;  // issued before the doublings, consumed after them
-      ld_jpt(T1, tab + kEcPtWords * (e1 > 0 ? e1 - 1 : 0));
-      ld_jpt(T2, tab + kEcPtWords * (e2 > 0 ? e2 - 1 : 0));
+      f29 x1, y1, x2, y2;  // affine [k]Q; issued before the doublings, consumed after them
+      ld_aff(x1, y1, tab + kEcPtWords * (e1 > 0 ? e1 - 1 : 0));
+      ld_aff(x2, y2, tab + kEcPtWords * (e2 > 0 ? e2 - 1 : 0));
       if (j != 32) {
         jdbl<C>(acc, acc);
         jdbl<C>(acc, acc);
@@ -661,13 +705,13 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
         jdbl<C>(acc, acc);
       }
       if (e1) {
-        f29_cneg<F>(T1.Y, (d1 < 0) != nb1);
-        jadd<C>(acc, acc, T1);
+        f29_cneg<F>(y1, (d1 < 0) != nb1);
+        jmadd<C>(acc, acc, x1, y1);
       }
       if (e2) {
-        f29_mul<F>(T2.X, T2.X, beta);  // phi([e2]Q)
-        f29_cneg<F>(T2.Y, (d2 < 0) != nb2);
-        jadd<C>(acc, acc, T2);
+        f29_mul<F>(x2, x2, beta);  // phi([e2]Q)
+        f29_cneg<F>(y2, (d2 < 0) != nb2);
+        jmadd<C>(acc, acc, x2, y2);
       }
       if ((j & 1) == 0) {
         const int g1 = booth_digit<8>(a1.v, j >> 1), g2 = booth_digit<8>(a2.v, j >> 1);
@@ -691,8 +735,8 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
     for (int j = 63; j >= 0; j--) {
       const int dq = booth_digit<4>(u2.v, j);
       const int aq = dq < 0 ? -dq : dq;
-      jpt T;  // issued before the doublings, consumed after them
-      ld_jpt(T, tab + kEcPtWords * (aq > 0 ? aq - 1 : 0));
+      f29 tx, ty;  // affine [aq]Q; issued before the doublings, consumed after them
+      ld_aff(tx, ty, tab + kEcPtWords * (aq > 0 ? aq - 1 : 0));
       if (j != 63) {
         jdbl<C>(acc, acc);
         jdbl<C>(acc, acc);
@@ -700,8 +744,8 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
         jdbl<C>(acc, acc);
       }
       if (aq) {
-        f29_cneg<F>(T.Y, (dq < 0) != neg2);
-        jadd<C>(acc, acc, T);
+        f29_cneg<F>(ty, (dq < 0) != neg2);
+        jmadd<C>(acc, acc, tx, ty);
       }
       if ((j & 1) == 0) {
         const int dg = booth_digit<8>(u1.v, j >> 1);
@@ -1035,6 +1079,31 @@ CDEV void ecdsa_inv_run(uint32_t* __restrict__ ws, uint64_t a, uint64_t b) {
   st256(ws + a * kEcWords + kEcW, inv);
 }
 
+// The same trick mod p over the slots' table-Z products (kEcZ -> kEcZW).
+template <class C>
+CDEV void ecdsa_zinv_run(uint32_t* __restrict__ ws, uint64_t a, uint64_t b) {
+  using F = typename C::F;
+  f29 acc, x;
+  ld_f29(acc, ws + a * kEcWords + kEcZ);
+  st_f29(ws + a * kEcWords + kEcZW, acc);
+  for (uint64_t j = a + 1; j < b; j++) {
+    ld_f29(x, ws + j * kEcWords + kEcZ);
+    f29_mul<F>(acc, acc, x);
+    st_f29(ws + j * kEcWords + kEcZW, acc);
+  }
+  f29 inv;
+  f29_pow_const<F, typename C::Pm2>(inv, acc);
+  for (uint64_t j = b - 1; j > a; j--) {
+    ld_f29(x, ws + (j - 1) * kEcWords + kEcZW);
+    f29 wj;
+    f29_mul<F>(wj, inv, x);
+    st_f29(ws + j * kEcWords + kEcZW, wj);
+    ld_f29(x, ws + j * kEcWords + kEcZ);
+    f29_mul<F>(inv, inv, x);
+  }
+  st_f29(ws + a * kEcWords + kEcZW, inv);
+}
+
 // kEcInvBatch consecutive slots per thread; curve runs from the partition
 // counts (slots [0, c1) secp256k1, [c1, c1 + c2) P-256, the rest unsupported)
 __global__ void __launch_bounds__(256) ecdsa_inv_kernel(uint64_t base, uint64_t m,
@@ -1049,12 +1118,81 @@ __global__ void __launch_bounds__(256) ecdsa_inv_kernel(uint64_t base, uint64_t 
   const uint64_t r1_end = c2 > base ? (c2 - base < m ? c2 - base : m) : 0;
   {
     const uint64_t a = lo, b = hi < k1_end ? hi : k1_end;
-    if (a < b) ecdsa_inv_run<Curve<2>>(ws, a, b);
+    if (a < b) {
+      ecdsa_inv_run<Curve<2>>(ws, a, b);
+      ecdsa_zinv_run<Curve<2>>(ws, a, b);
+    }
   }
   {
     const uint64_t a = lo > k1_end ? lo : k1_end, b = hi < r1_end ? hi : r1_end;
-    if (a < b) ecdsa_inv_run<Curve<3>>(ws, a, b);
+    if (a < b) {
+      ecdsa_inv_run<Curve<3>>(ws, a, b);
+      ecdsa_zinv_run<Curve<3>>(ws, a, b);
+    }
   }
+}
+
+// Table [k]Q, k = 2..8, to affine with the inverse of their Z product from
+// ecdsa_inv_kernel: per-entry Z^-1 by back-substitution (2M each), then
+// x = X Z^-2, y = Y Z^-3 written over X, Y. The ladder then adds Q-multiples
+// with jmadd (7M + 4S) instead of jadd (11M + 5S).
+template <class C>
+CDEV void ecdsa_affine_lane(uint32_t* __restrict__ rec) {
+  using F = typename C::F;
+  uint32_t* tab = rec + kEcTab;
+  f29 pre[7];  // pre[k - 2] = Z_2 ... Z_k
+  ld_slot_z(pre[0], tab + kEcPtWords * 1);
+#pragma unroll
+  for (int k = 3; k <= 8; k++) {
+    f29 z;
+    ld_slot_z(z, tab + kEcPtWords * (k - 1));
+    f29_mul<F>(pre[k - 2], pre[k - 3], z);
+  }
+  f29 inv;
+  ld_f29(inv, rec + kEcZW);  // (Z_2 ... Z_8)^-1
+#pragma unroll
+  for (int k = 8; k >= 2; k--) {
+    f29 zi, z;
+    if (k > 2) {
+      f29_mul<F>(zi, inv, pre[k - 3]);  // Z_k^-1
+      ld_slot_z(z, tab + kEcPtWords * (k - 1));
+      f29_mul<F>(inv, inv, z);          // (Z_2 ... Z_{k-1})^-1
+    } else {
+      zi = inv;
+    }
+    f29 z2, z3, x, y;
+    ld_aff(x, y, tab + kEcPtWords * (k - 1));
+    f29_sqr<F>(z2, zi);
+    f29_mul<F>(z3, z2, zi);
+    f29_mul<F>(x, x, z2);
+    f29_mul<F>(y, y, z3);
+    uint32_t w[20];
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      w[q] = x.v[q];
+      w[9 + q] = y.v[q];
+    }
+    w[18] = w[19] = 0;
+    uint4* o4 = reinterpret_cast<uint4*>(tab + kEcPtWords * (k - 1));
+#pragma unroll
+    for (int q = 0; q < 5; q++) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
+}
+
+__global__ void __launch_bounds__(256) ecdsa_affine_kernel(const unsigned int* __restrict__ perm,
+                                                          const uint8_t* __restrict__ scheme, uint64_t base,
+                                                          uint64_t m, const uint8_t* __restrict__ status,
+                                                          uint32_t* __restrict__ ws) {
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= m) return;
+  const uint64_t slot = base + li;
+  const uint64_t i = perm ? perm[slot] : slot;
+  if (status[i] != kEcPending) return;
+  uint32_t* rec = ws + li * kEcWords;
+  if (scheme[i] == 2)
+    ecdsa_affine_lane<Curve<2>>(rec);
+  else
+    ecdsa_affine_lane<Curve<3>>(rec);
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ecdsa_ladder_kernel(
@@ -1123,6 +1261,7 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
       const uint64_t nt = (m + kEcInvBatch - 1) / kEcInvBatch;
       hipLaunchKernelGGL(ecdsa_inv_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, s, base, m, counters6,
                          ws);
+      hipLaunchKernelGGL(ecdsa_affine_kernel, g, dim3(256), 0, s, perm, scheme, base, m, status, ws);
       hipLaunchKernelGGL(ecdsa_ladder_kernel, g, dim3(256), 0, s, perm, scheme, base, m, gk1, gr1, ws, status);
       e = hipGetLastError();
       if (e != hipSuccess) return e;
