@@ -1,0 +1,147 @@
+"""North-star agreement sweep: >= 1e9 mixed valid/invalid signatures on one MI355X.
+
+BASELINE.json north_star asks for "100% verdict agreement with the reference on
+>= 1e9 mixed valid/invalid signatures". This runs ED x 2^LOG2 Ed25519 lanes
+(C2 corpora: 1% corrupted / non-canonical / off-curve / small-order / S + kL)
+and EC x 2^LOG2 ECDSA lanes (C3 corpora: 50/50 secp256k1 / P-256, DER
+malformations, r/s out of range, off-curve and compressed keys, high-S) through
+the product kernels, each batch from a fresh seed, and checks EVERY lane's
+status byte:
+  * against the corpus construction where it fixes the exact status
+    (valid lanes, and every corruption whose status is determined);
+  * against the CPU oracle (oracle/c, the i2p 0.2.0 / BC 1.57 restatement)
+    for every lane the construction leaves open (slide()-dependent S >= 2^255
+    cases, "any rejection" ECDSA corruptions) and for a contiguous sample of
+    2^SAMPLE lanes per batch (valid and corrupted alike).
+Test infrastructure: the oracle is the checker here, never the thing measured.
+Usage (GPU box): python tools/agree_1e9.py --out gpurun_out/agree.json
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def ecdsa_csr(sc, K, KL, S, SL, M):
+    kl = KL.astype(np.uint64)
+    sl = SL.astype(np.uint64)
+    kb = np.ascontiguousarray(np.concatenate([K[i, :kl[i]] for i in range(len(sc))])) if len(sc) else np.zeros(1, np.uint8)
+    sb = np.ascontiguousarray(np.concatenate([S[i, :sl[i]] for i in range(len(sc))])) if len(sc) else np.zeros(1, np.uint8)
+    ko = np.zeros(len(sc) + 1, np.uint64)
+    so = np.zeros(len(sc) + 1, np.uint64)
+    ko[1:] = np.cumsum(kl)
+    so[1:] = np.cumsum(sl)
+    mo = np.arange(len(sc) + 1, dtype=np.uint64) * M.shape[1]
+    return kb, ko, sb, so, np.ascontiguousarray(M), mo
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ed", type=int, default=48, help="Ed25519 batches")
+    ap.add_argument("--ec", type=int, default=12, help="ECDSA batches")
+    ap.add_argument("--log2", type=int, default=24)
+    ap.add_argument("--sample-log2", type=int, default=15)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    import torch
+
+    from conftest import load_oracle
+    from corda_amd.corpus import REJECT_ANY, make_c2_corpus, make_c3_corpus
+    from corda_amd.engine import Engine
+
+    orc = load_oracle()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    n = 1 << args.log2
+    smp = 1 << args.sample_log2
+    tot = {"ed25519": dict(lanes=0, construction_checked=0, oracle_checked=0, mismatches=0, rejected=0),
+           "ecdsa": dict(lanes=0, construction_checked=0, oracle_checked=0, mismatches=0, rejected=0)}
+    t0 = time.time()
+    gpu_s = 0.0
+    with Engine(1) as eng:
+        for b in range(args.ed):
+            pubs, sigs, msgs, exp, _ = make_c2_corpus(eng, n, 0xA9EE0000 + b, dev, stream=stream)
+            st = torch.empty(n, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize(dev)
+            t1 = time.time()
+            eng.ed25519_verify_device(pubs, sigs, msgs, st, None, stream=stream)
+            torch.cuda.synchronize(dev)
+            gpu_s += time.time() - t1
+            known = exp >= 0
+            mism = int((st[known].to(torch.int16) != exp[known]).sum())
+            # oracle: every open lane plus the first `smp` lanes
+            idx = torch.nonzero(~known).flatten()
+            idx = torch.unique(torch.cat([idx, torch.arange(smp, device=dev)]))
+            k = pubs[idx].cpu().numpy().copy()
+            s = sigs[idx].cpu().numpy().copy()
+            m = msgs[idx].cpu().numpy().copy()
+            want = np.zeros(len(idx), np.uint8)
+            orc.oracle_ed25519_verify_batch(len(idx), k.ctypes.data, s.ctypes.data, m.ctypes.data, 32,
+                                            want.ctypes.data, args.threads)
+            mism_o = int((st[idx].cpu().numpy() != want).sum())
+            r = tot["ed25519"]
+            r["lanes"] += n
+            r["construction_checked"] += int(known.sum())
+            r["oracle_checked"] += len(idx)
+            r["mismatches"] += mism + mism_o
+            r["rejected"] += int((st != 0).sum())
+            print("ed25519 batch %d/%d: %d lanes, construction mism %d, oracle-checked %d mism %d (%.0f s)"
+                  % (b + 1, args.ed, n, mism, len(idx), mism_o, time.time() - t0), flush=True)
+            del pubs, sigs, msgs, exp, st
+        for b in range(args.ec):
+            sc, K, KL, S, SL, M, exp, _ = make_c3_corpus(eng, n, 0xA9EC0000 + b, dev, stream=stream)
+            st = torch.empty(n, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize(dev)
+            t1 = time.time()
+            eng.ecdsa_verify_device(sc, K, KL, S, SL, M, st, None, stream=stream)
+            torch.cuda.synchronize(dev)
+            gpu_s += time.time() - t1
+            exact = exp >= 0
+            anyrej = exp == REJECT_ANY
+            mism = int((st[exact].to(torch.int16) != exp[exact]).sum()) + int((st[anyrej] == 0).sum())
+            idx = torch.nonzero(~exact).flatten()
+            idx = torch.unique(torch.cat([idx, torch.arange(smp, device=dev)]))
+            csr = ecdsa_csr(sc[idx].cpu().numpy(), K[idx].cpu().numpy(), KL[idx].cpu().numpy(),
+                            S[idx].cpu().numpy(), SL[idx].cpu().numpy(), M[idx].cpu().numpy())
+            sch = np.ascontiguousarray(sc[idx].cpu().numpy())
+            kb, ko, sb, so, Mc, mo = csr
+            want = np.zeros(len(idx), np.uint8)
+            orc.oracle_ecdsa_verify_batch(len(idx), sch.ctypes.data, kb.ctypes.data, ko.ctypes.data, sb.ctypes.data,
+                                          so.ctypes.data, Mc.ctypes.data, mo.ctypes.data, want.ctypes.data,
+                                          args.threads)
+            mism_o = int((st[idx].cpu().numpy() != want).sum())
+            r = tot["ecdsa"]
+            r["lanes"] += n
+            r["construction_checked"] += int(exact.sum() + anyrej.sum())
+            r["oracle_checked"] += len(idx)
+            r["mismatches"] += mism + mism_o
+            r["rejected"] += int((st != 0).sum())
+            print("ecdsa batch %d/%d: %d lanes, construction mism %d, oracle-checked %d mism %d (%.0f s)"
+                  % (b + 1, args.ec, n, mism, len(idx), mism_o, time.time() - t0), flush=True)
+            del sc, K, KL, S, SL, M, exp, st
+    lanes = tot["ed25519"]["lanes"] + tot["ecdsa"]["lanes"]
+    out = {"lanes": lanes, "mismatches": tot["ed25519"]["mismatches"] + tot["ecdsa"]["mismatches"],
+           "per_scheme": tot, "gpu_verify_s": gpu_s, "wall_s": time.time() - t0,
+           "batch": n, "oracle_sample_per_batch": smp,
+           "note": "every lane's status vs the corpus construction where it fixes the status; every open lane "
+                   "(slide()-dependent S, any-rejection ECDSA corruptions) plus a 2^%d-lane sample per batch vs "
+                   "the C oracle" % args.sample_log2}
+    print(json.dumps(out), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(out, f, indent=1)
+    return 0 if out["mismatches"] == 0 else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
