@@ -113,3 +113,20 @@ def test_signed_tx_device_path(engine, oracle):
     want_bad = [(nsig[t] - 1 if t % 10 == 3 else -1) for t in range(ntx)]
     assert list(fb.cpu().numpy()) == want_bad
     assert list(tst.cpu().numpy()) == [1 if t % 10 == 3 else 0 for t in range(ntx)]
+
+
+@pytest.mark.gpu
+def test_leaf_sha256_every_length_and_alignment(engine):
+    """K3's aligned-dword loader: single-leaf transactions (root = the leaf hash,
+    MerkleTree.kt:51-52) of every length 0..300 packed back to back, so every
+    length meets every byte alignment; checked against hashlib."""
+    import hashlib
+    rng = random.Random(21)
+    txs = []
+    for shift in range(4):
+        txs.append([bytes(rng.getrandbits(8) for _ in range(shift + 1))])  # vary the running offset
+        txs += [[bytes(rng.getrandbits(8) for _ in range(n))] for n in range(301)]
+    ids, st = engine.tx_ids(txs)
+    assert (st == 0).all()
+    for t, tx in enumerate(txs):
+        assert bytes(ids[t]) == hashlib.sha256(tx[0]).digest(), (t, len(tx[0]))
