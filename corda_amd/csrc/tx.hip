@@ -42,11 +42,37 @@ CDEV void sha256_node(uint32_t out[8], const uint32_t a[8], const uint32_t b[8])
   sha256_block(out, w);
 }
 
-// K3: one lane per leaf
+// K3: one lane per leaf. A wave runs as many SHA-256 blocks as its longest
+// leaf, and a transaction's components differ widely in length (C4: 8, 3, 3, 1
+// and 1 blocks), so each 256-leaf tile is first counting-sorted in LDS by block
+// count (buckets 1..7, 8+): waves then hold leaves of similar length
+// (C4: ~15 instead of 32 wave-blocks per tile). Hashes are written by leaf index.
 __global__ void __launch_bounds__(256) sha256_leaves_kernel(const uint8_t* __restrict__ bytes,
                                                            const uint64_t* __restrict__ off, uint64_t nleaves,
                                                            uint32_t* __restrict__ hashes /* [nleaves][8] BE words */) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ unsigned int cnt[9], order[256];
+  const uint64_t mine = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (threadIdx.x < 9) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  int key = 8;  // past the end: last bucket, never hashed
+  if (mine < nleaves) {
+    const uint64_t nb = (off[mine + 1] - off[mine] + 9 + 63) / 64;
+    key = nb >= 8 ? 7 : (int)nb - 1;
+  }
+  atomicAdd(&cnt[key], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // exclusive prefix over the 9 buckets -> cursors
+    unsigned int run = 0;
+    for (int k = 0; k < 9; k++) {
+      const unsigned int c = cnt[k];
+      cnt[k] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  order[atomicAdd(&cnt[key], 1u)] = threadIdx.x;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + order[threadIdx.x];
   if (i >= nleaves) return;
   uint32_t h[8];
   const uint64_t lo = off[i], hi = off[i + 1];
