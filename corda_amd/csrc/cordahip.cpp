@@ -498,9 +498,28 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
   const uint64_t ne = e1 - e0, nc = c1 - c0;
   uint64_t chunk = kStreamChunk;  // CORDAHIP_STREAM_CHUNK: smaller chunks for tests of the pipeline itself
   if (const char* v = getenv("CORDAHIP_STREAM_CHUNK")) chunk = std::max<uint64_t>(64, strtoull(v, nullptr, 10));
-  const uint64_t nchunks = std::max<uint64_t>(1, (ne + nc + chunk - 1) / chunk);
-  const uint64_t ce = ((ne + nchunks - 1) / nchunks + 63) / 64 * 64;
-  const uint64_t cc = ((nc + nchunks - 1) / nchunks + 63) / 64 * 64;
+  // Chunk boundaries over the combined lane count T = ne + nc, each section cut
+  // at the same fraction of its length (64-aligned). The first chunks ramp up
+  // (chunk/16, chunk/4, then chunk): the GPU starts after a short first copy
+  // instead of a full chunk's H2D (~0.6 GB for C5), and PCIe (~4x faster than
+  // the kernels per lane) stays ahead while the sizes grow.
+  const uint64_t T = ne + nc;
+  std::vector<uint64_t> bound(1, 0);  // cumulative combined lanes at chunk ends
+  for (int k = 0; bound.back() < T; k++) {
+    const uint64_t sz = std::max<uint64_t>(64, k == 0 ? chunk / 16 : k == 1 ? chunk / 4 : chunk);
+    bound.push_back(std::min(T, bound.back() + sz));
+  }
+  const uint64_t nchunks = std::max<size_t>(1, bound.size() - 1);
+  auto cut = [&](uint64_t n, uint64_t k) -> uint64_t {  // section offset at the end of chunk k-1
+    if (k >= nchunks) return n;
+    const uint64_t v = (uint64_t)((__uint128_t)n * bound[k] / (T ? T : 1));
+    return std::min(n, v / 64 * 64);
+  };
+  uint64_t ce = 0, cc = 0;  // largest per-chunk section sizes: the stage buffers
+  for (uint64_t k = 0; k < nchunks; k++) {
+    ce = std::max(ce, cut(ne, k + 1) - cut(ne, k));
+    cc = std::max(cc, cut(nc, k + 1) - cut(nc, k));
+  }
   const uint64_t eml = b->ed_msg_len, cml = b->ec_msg_len;
   for (StreamStage& st : d.sstage) {
     if (!st.stream && hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)
@@ -517,8 +536,8 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
     StreamStage& st = d.sstage[k % kStreamStages];
     hipStream_t s = st.stream;
     if (k >= (uint64_t)kStreamStages && hipStreamSynchronize(s) != hipSuccess) return CORDAHIP_ERR_HIP;
-    const uint64_t a = std::min(e1, e0 + k * ce), ma = std::min(e1, a + ce) - a;
-    const uint64_t c = std::min(c1, c0 + k * cc), mc = std::min(c1, c + cc) - c;
+    const uint64_t a = e0 + cut(ne, k), ma = cut(ne, k + 1) - cut(ne, k);
+    const uint64_t c = c0 + cut(nc, k), mc = cut(nc, k + 1) - cut(nc, k);
     hipError_t e = hipSuccess;
     if (ma) {
       e = e ? e : hipMemcpyAsync(st.ed_keys.p, b->ed_keys + a * 32, ma * 32, h2d, s);

@@ -170,3 +170,31 @@ def test_batch_inversion_boundaries(engine, ec_vectors):
         st, _ = engine.verify_batch([v["scheme"] for v in vs], [v["pub"] for v in vs], [v["sig"] for v in vs],
                                     [v["msg"] for v in vs])
         assert [int(x) for x in st] == [v["status"] for v in vs], n
+
+
+def test_message_lengths_and_alignments(engine, oracle):
+    """e = SHA-256(clear data) for every length 0..140 (and 200, 1000) at every
+    byte alignment of the CSR blob (Crypto.doVerify takes any clearData; the
+    reference only ever passes 32-byte ids, so this pins the generic path):
+    valid signatures verify, a flipped message bit rejects, empty -> EMPTY."""
+    import bc_ecdsa as bc
+    rng = random.Random(33)
+    schemes, keys, sigs, msgs = [], [], [], []
+    for ln in list(range(141)) + [200, 1000]:
+        sch = 2 + (ln & 1)
+        d = rng.randrange(1, 1 << 250)
+        pub = bc.keypair(sch, d)
+        msg = bytes(rng.getrandbits(8) for _ in range(ln))
+        r, s = bc.sign(sch, d, msg, rng.randrange(1, 1 << 250))
+        sig = bc.der_encode(r, s)
+        if ln % 3 == 2:
+            msg = msg[:-1] + bytes([msg[-1] ^ 0x10])
+        schemes.append(sch)
+        keys.append(pub if ln % 4 else bc.compress(pub))
+        sigs.append(sig)
+        msgs.append(msg)
+    st, _ = engine.verify_batch(schemes, keys, sigs, msgs)
+    for i, (sch, k, g, m) in enumerate(zip(schemes, keys, sigs, msgs)):
+        want = oracle.oracle_ecdsa_verify(sch, k, len(k), g, len(g), m, len(m))
+        assert st[i] == want, (i, len(m), st[i], want)
+        assert want == (5 if not m else 1 if len(m) % 3 == 2 else 0)
