@@ -133,8 +133,20 @@ struct Device {
   StreamStage sstage[kStreamStages];
 };
 
-constexpr uint64_t kEdWsLanes = 1ull << 20;  // 3.1 GB of workspace per device
-constexpr uint64_t kEcWsSlots = 1ull << 20;  // 0.9 GB of ECDSA workspace per device
+// Launch-pair sizes of the split kernels = the largest workspace per device.
+// Bigger launches pay fewer end-of-grid tails (C2, measured: 2^18 91.5, 2^20
+// 93.2, 2^22 96.4, 2^24 97.2 M verifs/s): a 2^24-lane batch runs as ONE
+// prep/ladder pair over 50 GB of HBM (17% of the MI355X's 288 GB). Smaller
+// batches allocate only what they use (grow-only, from 2^18 lanes up).
+constexpr uint64_t kEdWsLanes = 1ull << 24;  // x 2,992 B = 50 GB of Ed25519 workspace at most
+constexpr uint64_t kEcWsSlots = 1ull << 24;  // x 1,120 B = 18.8 GB of ECDSA workspace at most
+constexpr uint64_t kWsMinLanes = 1ull << 18;
+
+uint64_t env_lanes(const char* name, uint64_t dflt) {  // A/B overrides, multiples of 64
+  const char* v = getenv(name);
+  const uint64_t x = v ? strtoull(v, nullptr, 10) : 0;
+  return x >= 64 ? x / 64 * 64 : dflt;
+}
 
 // Enqueue ECDSA verification of n slot-layout lanes on stream s (device current,
 // d.ec_mu held): the shared work buffers are reused only after their previous
@@ -144,11 +156,12 @@ hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* ke
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
                              unsigned long long* verdict, hipStream_t s) {
   EcWork& w = d.ec;
-  const uint64_t slots = std::min<uint64_t>(kEcWsSlots, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
+  static const uint64_t ws_slots = env_lanes("CORDAHIP_ECDSA_WS_SLOTS", kEcWsSlots);
+  const uint64_t slots = std::min<uint64_t>(ws_slots, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
   if (w.ws.cap < slots * ecdsa_ws_slot_bytes() || w.perm.cap < std::max<uint64_t>(n, 1) * 4) {
     hipError_t e = w.ev ? hipEventSynchronize(w.ev) : hipSuccess;  // a smaller buffer may still be in use
     if (e != hipSuccess) return e;
-    if (w.ws.ensure(std::max<uint64_t>(slots, kEcWsSlots / 16) * ecdsa_ws_slot_bytes()) ||
+    if (w.ws.ensure(std::max<uint64_t>(slots, std::min<uint64_t>(ws_slots, kWsMinLanes)) * ecdsa_ws_slot_bytes()) ||
         w.perm.ensure(std::max<uint64_t>(n, 1) * 4))
       return hipErrorOutOfMemory;
   }
@@ -168,12 +181,14 @@ hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
                              unsigned long long* verdict, hipStream_t s) {
   std::lock_guard<std::mutex> g(d.ed_mu);
-  const uint64_t lanes = std::min<uint64_t>(kEdWsLanes, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
+  static const uint64_t ws_lanes = env_lanes("CORDAHIP_ED25519_WS_LANES", kEdWsLanes);
+  const uint64_t lanes = std::min<uint64_t>(ws_lanes, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
   if (d.ed_ws.cap < lanes * ed25519_ws_lane_bytes()) {
     // a smaller buffer may still be in use by an earlier stream
     hipError_t e = d.ed_ev ? hipEventSynchronize(d.ed_ev) : hipSuccess;
     if (e != hipSuccess) return e;
-    e = d.ed_ws.ensure(std::max<uint64_t>(lanes, kEdWsLanes / 8) * ed25519_ws_lane_bytes());
+    e = d.ed_ws.ensure(std::max<uint64_t>(lanes, std::min<uint64_t>(ws_lanes, kWsMinLanes)) *
+                       ed25519_ws_lane_bytes());
     if (e != hipSuccess) return e;
   }
   if (!d.ed_ev && hipEventCreateWithFlags(&d.ed_ev, hipEventDisableTiming) != hipSuccess) return hipErrorUnknown;
