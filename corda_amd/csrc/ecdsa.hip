@@ -918,7 +918,17 @@ __global__ void __launch_bounds__(256) ecdsa_sign_kernel(const uint8_t* __restri
 }
 
 // ---- device-side scheme partition (wave-aggregated atomics) -----------------
-CDEV int scheme_class(uint8_t s) { return s == 2 ? 0 : s == 3 ? 1 : 2; }
+// Partition classes: secp256k1 uncompressed / compressed, P-256 uncompressed /
+// compressed, other. Compressed keys (33-byte SEC1) need a square root in
+// prep (a 256-bit exponentiation, about half of prep's instructions); grouping
+// them keeps that divergent branch inside ~10% of the waves instead of
+// letting one compressed key per wave stall 63 lanes. Curve runs stay
+// contiguous: [0, n0 + n1) secp256k1, then P-256, then the rest.
+static constexpr int kPartClasses = 5;
+CDEV int scheme_class(uint8_t s, uint8_t key_len) {
+  const int comp = key_len == 33 ? 1 : 0;
+  return s == 2 ? comp : s == 3 ? 2 + comp : 4;
+}
 
 // Each 256-thread block owns a tile of kPartTile lanes, visited in kPartIter
 // coalesced strides. Counting: wave ballots -> per-wave totals -> LDS -> ONE
@@ -930,60 +940,62 @@ CDEV int scheme_class(uint8_t s) { return s == 2 ? 0 : s == 3 ? 1 : 2; }
 static constexpr int kPartIter = 16;
 static constexpr int kPartTile = 256 * kPartIter;
 
-__global__ void __launch_bounds__(256) ecdsa_count_kernel(const uint8_t* __restrict__ scheme, uint64_t n,
+__global__ void __launch_bounds__(256) ecdsa_count_kernel(const uint8_t* __restrict__ scheme,
+                                                         const uint8_t* __restrict__ key_len, uint64_t n,
                                                          unsigned int* __restrict__ counts) {
-  __shared__ unsigned int part[3][4];
+  __shared__ unsigned int part[kPartClasses][4];
   const uint64_t tile = (uint64_t)blockIdx.x * kPartTile;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned int tot[3] = {0u, 0u, 0u};
+  unsigned int tot[kPartClasses] = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll 4
   for (int it = 0; it < kPartIter; it++) {
     const uint64_t i = tile + (uint64_t)it * 256 + threadIdx.x;
-    const int c = i < n ? scheme_class(scheme[i]) : -1;
+    const int c = i < n ? scheme_class(scheme[i], key_len[i]) : -1;
 #pragma unroll
-    for (int k = 0; k < 3; k++) tot[k] += (unsigned int)__popcll(__ballot(c == k));
+    for (int k = 0; k < kPartClasses; k++) tot[k] += (unsigned int)__popcll(__ballot(c == k));
   }
   if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < 3; k++) part[k][wave] = tot[k];
+    for (int k = 0; k < kPartClasses; k++) part[k][wave] = tot[k];
   }
   __syncthreads();
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < kPartClasses) {
     const unsigned int t = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] + part[threadIdx.x][3];
     if (t) atomicAdd(&counts[threadIdx.x], t);
   }
 }
 
-__global__ void __launch_bounds__(256) ecdsa_scatter_kernel(const uint8_t* __restrict__ scheme, uint64_t n,
+__global__ void __launch_bounds__(256) ecdsa_scatter_kernel(const uint8_t* __restrict__ scheme,
+                                                           const uint8_t* __restrict__ key_len, uint64_t n,
                                                            const unsigned int* __restrict__ counts,
                                                            unsigned int* __restrict__ cursors,
                                                            unsigned int* __restrict__ perm) {
   const uint64_t tile = (uint64_t)blockIdx.x * kPartTile;
   const int lane = threadIdx.x & 63;
-  unsigned int tot[3] = {0u, 0u, 0u};
+  unsigned int tot[kPartClasses] = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll 4
   for (int it = 0; it < kPartIter; it++) {
     const uint64_t i = tile + (uint64_t)it * 256 + threadIdx.x;
-    const int c = i < n ? scheme_class(scheme[i]) : -1;
+    const int c = i < n ? scheme_class(scheme[i], key_len[i]) : -1;
 #pragma unroll
-    for (int k = 0; k < 3; k++) tot[k] += (unsigned int)__popcll(__ballot(c == k));
+    for (int k = 0; k < kPartClasses; k++) tot[k] += (unsigned int)__popcll(__ballot(c == k));
   }
-  unsigned int start[3];
+  unsigned int start[kPartClasses];
+  unsigned int base = 0;
 #pragma unroll
-  for (int k = 0; k < 3; k++) {
+  for (int k = 0; k < kPartClasses; k++) {
     unsigned int s0 = 0;
     if (lane == 0 && tot[k]) s0 = atomicAdd(&cursors[k], tot[k]);
-    start[k] = __shfl(s0, 0);
+    start[k] = __shfl(s0, 0) + base;
+    base += counts[k];
   }
-  start[1] += counts[0];
-  start[2] += counts[0] + counts[1];
   const unsigned long long below = (1ull << lane) - 1;
 #pragma unroll 4
   for (int it = 0; it < kPartIter; it++) {
     const uint64_t i = tile + (uint64_t)it * 256 + threadIdx.x;
-    const int c = i < n ? scheme_class(scheme[i]) : -1;
+    const int c = i < n ? scheme_class(scheme[i], key_len[i]) : -1;
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < kPartClasses; k++) {
       const unsigned long long m = __ballot(c == k);
       if (c == k) perm[start[k] + __popcll(m & below)] = (unsigned int)i;
       start[k] += (unsigned int)__popcll(m);
@@ -1113,7 +1125,7 @@ __global__ void __launch_bounds__(256) ecdsa_inv_kernel(uint64_t base, uint64_t 
   const uint64_t lo = t * kEcInvBatch;
   if (lo >= m) return;
   const uint64_t hi = lo + kEcInvBatch < m ? lo + kEcInvBatch : m;
-  const uint64_t c1 = counts[0], c2 = c1 + counts[1];
+  const uint64_t c1 = counts[0] + counts[1], c2 = c1 + counts[2] + counts[3];  // secp256k1 | P-256 runs
   const uint64_t k1_end = c1 > base ? (c1 - base < m ? c1 - base : m) : 0;
   const uint64_t r1_end = c2 > base ? (c2 - base < m ? c2 - base : m) : 0;
   {
@@ -1228,7 +1240,7 @@ hipError_t launch_ecdsa_gtables(uint32_t* k1, uint32_t* r1, hipStream_t s) {
   return hipGetLastError();
 }
 
-// partition + verify + verdict; work: counts[3] + cursors[3] (zeroed here) and perm[n].
+// partition + verify + verdict; work: counts[5] + cursors[5] (zeroed here) and perm[n].
 // ws (ws_slots * ecdsa_ws_slot_bytes() of device memory) selects the split
 // path (prep -> batch inversion -> ladder per chunk of ws_slots); without it,
 // or with CORDAHIP_ECDSA=fused, the single fused kernel runs (A/B baseline).
@@ -1244,11 +1256,12 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
     return v && std::string(v) == "fused";
   }();
   const dim3 grid((uint32_t)((n + 255) / 256));
-  hipError_t e = hipMemsetAsync(counters6, 0, 6 * sizeof(unsigned int), s);
+  hipError_t e = hipMemsetAsync(counters6, 0, 2 * kPartClasses * sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
   const dim3 pgrid((uint32_t)((n + kPartTile - 1) / kPartTile));
-  hipLaunchKernelGGL(ecdsa_count_kernel, pgrid, dim3(256), 0, s, scheme, n, counters6);
-  hipLaunchKernelGGL(ecdsa_scatter_kernel, pgrid, dim3(256), 0, s, scheme, n, counters6, counters6 + 3, perm);
+  hipLaunchKernelGGL(ecdsa_count_kernel, pgrid, dim3(256), 0, s, scheme, key_len, n, counters6);
+  hipLaunchKernelGGL(ecdsa_scatter_kernel, pgrid, dim3(256), 0, s, scheme, key_len, n, counters6,
+                     counters6 + kPartClasses, perm);
   if (fused || !ws || ws_slots < 64) {
     hipLaunchKernelGGL(ecdsa_verify_kernel, grid, dim3(256), 0, s, perm, scheme, keys, key_len, sigs, sig_len, msgs,
                        msg_off, msg_len, n, gk1, gr1, pre_status, status);
