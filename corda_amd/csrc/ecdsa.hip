@@ -520,10 +520,14 @@ CDEV void ld_f29(f29& a, const uint32_t* __restrict__ o) {
   a.v[0] = x.x; a.v[1] = x.y; a.v[2] = x.z; a.v[3] = x.w;
   a.v[4] = y.x; a.v[5] = y.y; a.v[6] = y.z; a.v[7] = y.w; a.v[8] = z.x;
 }
-// Z of a Jacobian table slot (words 18..26: not 16-B aligned, dword loads)
+// Z of a Jacobian table slot: words 18..26, read as the three aligned 16-B
+// vectors covering words 16..27 (slots start 16-B aligned)
 CDEV void ld_slot_z(f29& z, const uint32_t* __restrict__ slot) {
-#pragma unroll
-  for (int i = 0; i < 9; i++) z.v[i] = slot[18 + i];
+  const uint4* o4 = reinterpret_cast<const uint4*>(slot + 16);
+  const uint4 a = o4[0], b = o4[1], c = o4[2];
+  z.v[0] = a.z; z.v[1] = a.w;
+  z.v[2] = b.x; z.v[3] = b.y; z.v[4] = b.z; z.v[5] = b.w;
+  z.v[6] = c.x; z.v[7] = c.y; z.v[8] = c.z;
 }
 // affine table entry: X, Y in the first 18 words of a kEcPtWords slot (five 16-B loads)
 CDEV void ld_aff(f29& x, f29& y, const uint32_t* __restrict__ o) {
@@ -1209,15 +1213,24 @@ __global__ void __launch_bounds__(256) ecdsa_affine_kernel(const unsigned int* _
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ecdsa_ladder_kernel(
     const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, uint64_t base, uint64_t m,
-    const uint32_t* __restrict__ gtab_k1, const uint32_t* __restrict__ gtab_r1, const uint32_t* __restrict__ ws,
-    uint8_t* __restrict__ status) {
+    const uint32_t* __restrict__ gtab_k1, const uint32_t* __restrict__ gtab_r1, uint32_t* __restrict__ ws,
+    uint8_t* __restrict__ status, int fuse_affine) {
   const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= m) return;
   const uint64_t slot = base + li;
   const uint64_t i = perm ? perm[slot] : slot;
   if (status[i] != kEcPending) return;
-  const uint32_t* rec = ws + li * kEcWords;
-  status[i] = scheme[i] == 2 ? ecdsa_ladder_lane<Curve<2>>(rec, gtab_k1) : ecdsa_ladder_lane<Curve<3>>(rec, gtab_r1);
+  uint32_t* rec = ws + li * kEcWords;
+  // fused table-to-affine pass: its uncoalesced record traffic overlaps the
+  // VALU-bound ladder of the SIMD's other waves instead of running as a
+  // memory-bound kernel of its own (same thread writes, then reads: ordered)
+  if (scheme[i] == 2) {
+    if (fuse_affine) ecdsa_affine_lane<Curve<2>>(rec);
+    status[i] = ecdsa_ladder_lane<Curve<2>>(rec, gtab_k1);
+  } else {
+    if (fuse_affine) ecdsa_affine_lane<Curve<3>>(rec);
+    status[i] = ecdsa_ladder_lane<Curve<3>>(rec, gtab_r1);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1255,6 +1268,10 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
     const char* v = getenv("CORDAHIP_ECDSA");
     return v && std::string(v) == "fused";
   }();
+  static const bool fuse_affine = [] {  // CORDAHIP_ECDSA_AFFINE=kernel: separate affine pass (A/B)
+    const char* v = getenv("CORDAHIP_ECDSA_AFFINE");
+    return !(v && std::string(v) == "kernel");
+  }();
   const dim3 grid((uint32_t)((n + 255) / 256));
   hipError_t e = hipMemsetAsync(counters6, 0, 2 * kPartClasses * sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
@@ -1274,8 +1291,9 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
       const uint64_t nt = (m + kEcInvBatch - 1) / kEcInvBatch;
       hipLaunchKernelGGL(ecdsa_inv_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, s, base, m, counters6,
                          ws);
-      hipLaunchKernelGGL(ecdsa_affine_kernel, g, dim3(256), 0, s, perm, scheme, base, m, status, ws);
-      hipLaunchKernelGGL(ecdsa_ladder_kernel, g, dim3(256), 0, s, perm, scheme, base, m, gk1, gr1, ws, status);
+      if (!fuse_affine) hipLaunchKernelGGL(ecdsa_affine_kernel, g, dim3(256), 0, s, perm, scheme, base, m, status, ws);
+      hipLaunchKernelGGL(ecdsa_ladder_kernel, g, dim3(256), 0, s, perm, scheme, base, m, gk1, gr1, ws, status,
+                         fuse_affine ? 1 : 0);
       e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
