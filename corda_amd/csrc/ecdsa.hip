@@ -765,7 +765,7 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
   return x_check<C>(acc, r);
 }
 
-// Fused single-kernel lane (A/B baseline, CORDAHIP_ECDSA=fused): the split
+// Retired single-kernel lane (no longer dispatched; predates the affine tables): the split
 // path's prep and ladder over a private record, with a per-lane Fermat inversion.
 template <class C>
 CDEV uint8_t ecdsa_verify_lane(const uint8_t* __restrict__ key, uint32_t key_len, const uint8_t* __restrict__ sig,
@@ -1256,7 +1256,7 @@ hipError_t launch_ecdsa_gtables(uint32_t* k1, uint32_t* r1, hipStream_t s) {
 // partition + verify + verdict; work: counts[5] + cursors[5] (zeroed here) and perm[n].
 // ws (ws_slots * ecdsa_ws_slot_bytes() of device memory) selects the split
 // path (prep -> batch inversion -> ladder per chunk of ws_slots); without it,
-// or with CORDAHIP_ECDSA=fused, the single fused kernel runs (A/B baseline).
+// a missing workspace is an error (the old single-kernel path is retired).
 hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
                                const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs,
                                const uint64_t* msg_off, uint32_t msg_len, uint64_t n, const uint32_t* gk1,
@@ -1264,10 +1264,7 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
                                unsigned long long* verdict, unsigned int* counters6, unsigned int* perm,
                                uint32_t* ws, uint64_t ws_slots, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  static const bool fused = [] {
-    const char* v = getenv("CORDAHIP_ECDSA");
-    return v && std::string(v) == "fused";
-  }();
+  if (!ws || ws_slots < 64) return hipErrorInvalidValue;  // the split path is the only verify path
   static const bool fuse_affine = [] {  // CORDAHIP_ECDSA_AFFINE=kernel: separate affine pass (A/B)
     const char* v = getenv("CORDAHIP_ECDSA_AFFINE");
     return !(v && std::string(v) == "kernel");
@@ -1279,24 +1276,19 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
   hipLaunchKernelGGL(ecdsa_count_kernel, pgrid, dim3(256), 0, s, scheme, key_len, n, counters6);
   hipLaunchKernelGGL(ecdsa_scatter_kernel, pgrid, dim3(256), 0, s, scheme, key_len, n, counters6,
                      counters6 + kPartClasses, perm);
-  if (fused || !ws || ws_slots < 64) {
-    hipLaunchKernelGGL(ecdsa_verify_kernel, grid, dim3(256), 0, s, perm, scheme, keys, key_len, sigs, sig_len, msgs,
-                       msg_off, msg_len, n, gk1, gr1, pre_status, status);
-  } else {
-    for (uint64_t base = 0; base < n; base += ws_slots) {
-      const uint64_t m = n - base < ws_slots ? n - base : ws_slots;
-      const dim3 g((uint32_t)((m + 255) / 256));
-      hipLaunchKernelGGL(ecdsa_prep_kernel, g, dim3(256), 0, s, perm, scheme, keys, key_len, sigs, sig_len, msgs,
-                         msg_off, msg_len, base, m, pre_status, status, ws);
-      const uint64_t nt = (m + kEcInvBatch - 1) / kEcInvBatch;
-      hipLaunchKernelGGL(ecdsa_inv_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, s, base, m, counters6,
-                         ws);
-      if (!fuse_affine) hipLaunchKernelGGL(ecdsa_affine_kernel, g, dim3(256), 0, s, perm, scheme, base, m, status, ws);
-      hipLaunchKernelGGL(ecdsa_ladder_kernel, g, dim3(256), 0, s, perm, scheme, base, m, gk1, gr1, ws, status,
-                         fuse_affine ? 1 : 0);
-      e = hipGetLastError();
-      if (e != hipSuccess) return e;
-    }
+  for (uint64_t base = 0; base < n; base += ws_slots) {
+    const uint64_t m = n - base < ws_slots ? n - base : ws_slots;
+    const dim3 g((uint32_t)((m + 255) / 256));
+    hipLaunchKernelGGL(ecdsa_prep_kernel, g, dim3(256), 0, s, perm, scheme, keys, key_len, sigs, sig_len, msgs,
+                       msg_off, msg_len, base, m, pre_status, status, ws);
+    const uint64_t nt = (m + kEcInvBatch - 1) / kEcInvBatch;
+    hipLaunchKernelGGL(ecdsa_inv_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, s, base, m, counters6,
+                       ws);
+    if (!fuse_affine) hipLaunchKernelGGL(ecdsa_affine_kernel, g, dim3(256), 0, s, perm, scheme, base, m, status, ws);
+    hipLaunchKernelGGL(ecdsa_ladder_kernel, g, dim3(256), 0, s, perm, scheme, base, m, gk1, gr1, ws, status,
+                       fuse_affine ? 1 : 0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
   }
   if (verdict) hipLaunchKernelGGL(verdict_kernel, grid, dim3(256), 0, s, status, n, verdict);
   return hipGetLastError();
