@@ -185,7 +185,7 @@ class C1(C2):
 
 # ---- C3: mixed secp256k1 / P-256 ECDSA ----------------------------------------
 class C3:
-    kernel = "ecdsa_verify_kernel"
+    kernel = "ecdsa_prep_kernel + ecdsa_inv_kernel + ecdsa_ladder_kernel"
     pmc = "r01_pmc_ecdsa_verify.json"
 
     def __init__(self, eng, device, stream, rank, args):
