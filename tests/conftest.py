@@ -65,6 +65,16 @@ def ec_vectors():
 
 
 @pytest.fixture(scope="session")
+def cert_vectors():
+    """ECDSA signatures made by the reference's own BouncyCastle path: the dev
+    certificates it ships (tests/golden/make_cert_vectors.py), plus derived flips."""
+    with open(os.path.join(ROOT, "tests", "golden", "cert_vectors.json")) as f:
+        vs = json.load(f)["vectors"]
+    return [dict(v, pub=bytes.fromhex(v["pub"]), sig=bytes.fromhex(v["sig"]), msg=bytes.fromhex(v["msg"]))
+            for v in vs]
+
+
+@pytest.fixture(scope="session")
 def engine():
     from corda_amd.engine import Engine
     e = Engine(1)  # device 0

@@ -198,3 +198,17 @@ def test_message_lengths_and_alignments(engine, oracle):
         want = oracle.oracle_ecdsa_verify(sch, k, len(k), g, len(g), m, len(m))
         assert st[i] == want, (i, len(m), st[i], want)
         assert want == (5 if not m else 1 if len(m) % 3 == 2 else 0)
+
+
+def test_reference_certificate_signatures(engine, cert_vectors):
+    """K2 against signatures made by the reference's own BouncyCastle path (the
+    ecdsa-with-SHA256 certificates shipped in /root/reference, both curves; 430-510
+    byte TBS messages, so the multi-block SHA-256 path too) and their derived
+    corruptions, through the generic C-ABI batch and the dense device path."""
+    vs = cert_vectors
+    st, verdict = engine.verify_batch([v["scheme"] for v in vs], [v["pub"] for v in vs], [v["sig"] for v in vs],
+                                      [v["msg"] for v in vs])
+    bad = [(v["cat"], v["cert"], int(s), v["status"]) for v, s in zip(vs, st) if s != v["status"]]
+    assert not bad, bad
+    for i, v in enumerate(vs):
+        assert ((int(verdict[i // 64]) >> (i % 64)) & 1) == (v["status"] == 0)

@@ -227,3 +227,23 @@ def test_ecdsa_golden_covers_catalogue(ec_vectors):
     for c in ("r_zero", "s_ge_n", "r_negative"):
         assert (c, 1) in cats
     assert ("key_off_curve", 3) in cats and ("key_x_ge_p", 3) in cats
+
+
+def test_ecdsa_oracles_match_reference_certificates(oracle, cert_vectors):
+    """Parity pin: the reference ships BC-1.57-made ecdsa-with-SHA256 signatures
+    (dev CA / node / sample certificates, both curves). The C and Python
+    restatements must accept every one, and reject the derived corruptions with
+    the statuses BC's rules fix (bit flips BAD_SIG, truncated DER MALFORMED_SIG,
+    off-curve issuer key BAD_KEY)."""
+    import bc_ecdsa as ec
+    schemes = set()
+    for v in cert_vectors:
+        p, s, m = v["pub"], v["sig"], v["msg"]
+        assert oracle.oracle_ecdsa_verify(v["scheme"], p, len(p), s, len(s), m, len(m)) == v["status"], \
+            (v["cat"], v["cert"], v["note"])
+        assert ec.verify_status(v["scheme"], p, s, m) == v["status"], (v["cat"], v["cert"])
+        if v["cat"] == "reference_cert":
+            schemes.add(v["scheme"])
+            assert v["status"] == 0 and len(m) > 300  # multi-block SHA-256 messages (TBSCertificate)
+    assert schemes == {2, 3}
+    assert sum(v["cat"] == "reference_cert" for v in cert_vectors) >= 6
