@@ -30,7 +30,10 @@ EXPORTS = [
     "cordahip_ed25519_verify_host", "cordahip_ed25519_sign_device", "cordahip_ecdsa_sign_device", "cordahip_last_kernel_ms",
     "cordahip_tx_ids", "cordahip_signed_tx_verify", "cordahip_signed_tx_verify_ed25519_device",
     "cordahip_ecdsa_verify_device", "cordahip_stream_verify", "cordahip_filtered_tx_verify",
+    "cordahip_tx_submit", "cordahip_txid_submit", "cordahip_filtered_tx_submit", "cordahip_shard_range",
 ]
+ABI_VERSION = 2
+FLAG_IS_VALID = 1  # CORDAHIP_FLAG_IS_VALID: Crypto.isValid semantics (no emptiness checks)
 TX_NO_LEAVES, TX_NO_SIGNATURES, TX_BAD_TREE = 6, 7, 8
 
 
@@ -53,6 +56,7 @@ class SigBatch(ctypes.Structure):
         ("msg", ctypes.c_void_p), ("msg_off", ctypes.c_void_p),
         ("status", ctypes.c_void_p),
         ("verdict", ctypes.c_void_p),
+        ("flags", ctypes.c_uint32),
     ]
 
 
@@ -142,6 +146,10 @@ def lib() -> ctypes.CDLL:
         "cordahip_ecdsa_sign_device": (i32, [vp, i32, vp, vp, vp, u32, u64, vp, vp, vp, vp, vp]),
         "cordahip_stream_verify": (i32, [vp, ctypes.POINTER(StreamBatch)]),
         "cordahip_filtered_tx_verify": (i32, [vp, ctypes.POINTER(FilteredTxBatch)]),
+        "cordahip_tx_submit": (i32, [vp, ctypes.POINTER(SignedTxBatch), ctypes.POINTER(u64)]),
+        "cordahip_txid_submit": (i32, [vp, ctypes.POINTER(TxidBatch), ctypes.POINTER(u64)]),
+        "cordahip_filtered_tx_submit": (i32, [vp, ctypes.POINTER(FilteredTxBatch), ctypes.POINTER(u64)]),
+        "cordahip_shard_range": (None, [u64, u32, u32, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(l, name)
@@ -149,6 +157,13 @@ def lib() -> ctypes.CDLL:
         f.argtypes = args
     _lib = l
     return l
+
+
+def shard_range(n: int, nshards: int, shard: int, align: int = 64):
+    """The library's in-process partition rule (cordahip_shard_range): [lo, hi)."""
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    lib().cordahip_shard_range(n, nshards, shard, align, ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
 
 
 def strerror(code: int) -> str:

@@ -2,12 +2,15 @@
 // batch partitioning and the C-ABI of include/cordahip.h.
 //
 // MI355X-first shape: one context drives the devices named by its mask; a
-// dense batch is split into contiguous 64-aligned shards, one per device, and
-// each shard streams through two HIP streams in fixed chunks (H2D of chunk
-// k+1 overlaps the kernel of chunk k). Device buffers are grow-only per
-// device and reused across calls; the Ed25519 base-point table is built once
-// per device at init by a kernel. There is no CPU verification fallback:
-// a HIP failure is returned to the caller as CORDAHIP_ERR_HIP.
+// host batch is split into contiguous 64-aligned shards, one per device
+// (Ed25519 and ECDSA lanes alike; transactions whole), and each shard streams
+// through HIP streams in fixed chunks (H2D of chunk k+1 overlaps the kernel of
+// chunk k). Device buffers are grow-only per device and reused across calls;
+// every buffer shared between streams is fenced by an event (the next user's
+// stream waits on the last user's completion). Tickets run on a per-context
+// worker pool. The fixed-base tables are built once per device at init by a
+// kernel. There is no CPU verification fallback: a HIP failure is returned to
+// the caller as CORDAHIP_ERR_HIP.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -16,6 +19,8 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <future>
 #include <map>
 #include <memory>
@@ -33,7 +38,8 @@ hipError_t launch_ed25519_btable(uint32_t* tab, hipStream_t s);
 size_t ed25519_btable_bytes();
 hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
                                  uint64_t n, const uint32_t* btab, const uint8_t* pre_status, uint8_t* status,
-                                 unsigned long long* verdict, uint32_t* ws, uint64_t ws_lanes, hipStream_t s);
+                                 unsigned long long* verdict, uint32_t* ws, uint64_t ws_lanes, uint32_t flags,
+                                 hipStream_t s);
 size_t ed25519_ws_lane_bytes();
 hipError_t launch_ed25519_sign(const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len, uint64_t n,
                                const uint32_t* btab, uint8_t* pubs, uint8_t* sigs, hipStream_t s);
@@ -55,7 +61,7 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
                                const uint64_t* msg_off, uint32_t msg_len, uint64_t n, const uint32_t* gk1,
                                const uint32_t* gr1, const uint8_t* pre_status, uint8_t* status,
                                unsigned long long* verdict, unsigned int* counters6, unsigned int* perm,
-                               uint32_t* ws, uint64_t ws_slots, hipStream_t s);
+                               uint32_t* ws, uint64_t ws_slots, uint32_t flags, hipStream_t s);
 size_t ecdsa_ws_slot_bytes();
 hipError_t launch_ecdsa_sign(const uint8_t* scheme, const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len,
                              uint64_t n, const uint32_t* gk1, const uint32_t* gr1, uint8_t* keys, uint8_t* key_len,
@@ -79,6 +85,11 @@ struct DevBuf {
     hipError_t e = hipMalloc(&p, bytes);
     if (e == hipSuccess) cap = bytes;
     return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
   }
   template <class T>
   T* as() const { return static_cast<T*>(p); }
@@ -109,20 +120,35 @@ struct EcWork {  // device buffers of the ECDSA paths (grow-only)
   hipEvent_t ev = nullptr;   // last enqueued user of counters/perm/ws (cross-stream reuse)
 };
 
+// Per-call timing of the *_device entry points: a ring of event pairs per
+// device, one pair per call, so concurrent callers never share events.
+constexpr int kTimingRing = 64;
+struct TimedCall {
+  hipEvent_t a = nullptr, b = nullptr;
+};
+
+std::atomic<uint64_t> g_device_uid{1};
+
 struct Device {
   int id = 0;
+  uint64_t uid = 0;  // process-unique: keys the per-thread timing slot
   uint32_t* btab = nullptr;
   uint32_t* gtab_k1 = nullptr;  // [k]G tables, k = 0..128, secp256k1 / P-256
   uint32_t* gtab_r1 = nullptr;
   std::mutex ec_mu;
   EcWork ec;
   hipStream_t stream = nullptr;  // context stream (init-time work and host tx paths)
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  double last_ms = -1.0;
+  std::mutex tmu;
+  TimedCall ring[kTimingRing];
+  uint32_t ring_next = 0;
   std::mutex mu;  // serialises host-path use of the stages
   Stage stage[2];
-  std::mutex tx_mu;  // serialises use of tx
+  // tx buffers: tx_mu orders the enqueues of every user (host tx paths, the
+  // device signed-tx path), tx_ev marks the last enqueued user's completion;
+  // each user's stream waits on it before touching the buffers.
+  std::mutex tx_mu;
   TxWork tx;
+  hipEvent_t tx_ev = nullptr;
   // Ed25519 split-kernel workspace, shared by every stream that verifies on
   // this device: ed_mu orders the enqueues, ed_ev makes each user's stream
   // wait for the previous user's kernels before it reuses the buffer.
@@ -133,6 +159,9 @@ struct Device {
   StreamStage sstage[kStreamStages];
 };
 
+// device uid -> ring slot of this thread's most recent timed call
+thread_local std::unordered_map<uint64_t, int> tl_last_call;
+
 // Launch-pair sizes of the split kernels = the largest workspace per device.
 // Bigger launches pay fewer end-of-grid tails (C2, measured: 2^18 91.5, 2^20
 // 93.2, 2^22 96.4, 2^24 97.2 M verifs/s): a 2^24-lane batch runs as ONE
@@ -142,7 +171,9 @@ constexpr uint64_t kEdWsLanes = 1ull << 24;  // x 2,992 B = 50 GB of Ed25519 wor
 constexpr uint64_t kEcWsSlots = 1ull << 24;  // x 1,120 B = 18.8 GB of ECDSA workspace at most
 constexpr uint64_t kWsMinLanes = 1ull << 18;
 
-uint64_t env_lanes(const char* name, uint64_t dflt) {  // A/B overrides, multiples of 64
+// Workspace-size overrides (multiples of 64): tests use them to force the
+// multi-chunk paths (several prep/ladder launch sets per batch) at small sizes.
+uint64_t env_lanes(const char* name, uint64_t dflt) {
   const char* v = getenv(name);
   const uint64_t x = v ? strtoull(v, nullptr, 10) : 0;
   return x >= 64 ? x / 64 * 64 : dflt;
@@ -154,7 +185,7 @@ uint64_t env_lanes(const char* name, uint64_t dflt) {  // A/B overrides, multipl
 hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
                              const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs, const uint64_t* msg_off,
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
-                             unsigned long long* verdict, hipStream_t s) {
+                             unsigned long long* verdict, uint32_t flags, hipStream_t s) {
   EcWork& w = d.ec;
   static const uint64_t ws_slots = env_lanes("CORDAHIP_ECDSA_WS_SLOTS", kEcWsSlots);
   const uint64_t slots = std::min<uint64_t>(ws_slots, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
@@ -171,7 +202,7 @@ hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* ke
   e = e ? e
         : launch_ecdsa_verify(scheme, keys, key_len, sigs, sig_len, msgs, msg_off, msg_len, n, d.gtab_k1, d.gtab_r1,
                               pre, status, verdict, w.counters.as<unsigned int>(), w.perm.as<unsigned int>(),
-                              w.ws.as<uint32_t>(), w.ws.cap / ecdsa_ws_slot_bytes() / 64 * 64, s);
+                              w.ws.as<uint32_t>(), w.ws.cap / ecdsa_ws_slot_bytes() / 64 * 64, flags, s);
   e = e ? e : hipEventRecord(w.ev, s);
   return e;
 }
@@ -179,7 +210,7 @@ hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* ke
 // Enqueue Ed25519 verification of n dense lanes on stream s (device already current).
 hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
-                             unsigned long long* verdict, hipStream_t s) {
+                             unsigned long long* verdict, uint32_t flags, hipStream_t s) {
   std::lock_guard<std::mutex> g(d.ed_mu);
   static const uint64_t ws_lanes = env_lanes("CORDAHIP_ED25519_WS_LANES", kEdWsLanes);
   const uint64_t lanes = std::min<uint64_t>(ws_lanes, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
@@ -195,27 +226,149 @@ hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs
   hipError_t e = hipStreamWaitEvent(s, d.ed_ev, 0);
   e = e ? e
         : launch_ed25519_verify(keys, sigs, msgs, msg_len, n, d.btab, pre, status, verdict, d.ed_ws.as<uint32_t>(),
-                                d.ed_ws.cap / ed25519_ws_lane_bytes() / 64 * 64, s);
+                                d.ed_ws.cap / ed25519_ws_lane_bytes() / 64 * 64, flags, s);
   e = e ? e : hipEventRecord(d.ed_ev, s);
   return e;
 }
 
 int hip_err(hipError_t e) { return e == hipSuccess ? CORDAHIP_SUCCESS : CORDAHIP_ERR_HIP; }
 
+// the in-process partition rule (cordahip_shard_range)
+void shard_range(uint64_t n, uint64_t nshards, uint64_t shard, uint64_t align, uint64_t& lo, uint64_t& hi) {
+  if (nshards == 0 || shard >= nshards) {
+    lo = hi = n;
+    return;
+  }
+  align = align ? align : 1;
+  const uint64_t per = ((n + nshards - 1) / nshards + align - 1) / align * align;
+  lo = std::min(n, shard * per);
+  hi = std::min(n, lo + per);
+}
+
+// Run fn(device, lo, hi) for every non-empty shard of n lanes, one host thread
+// per device; returns the first failure.
+template <class F>
+int for_shards(std::vector<std::unique_ptr<Device>>& devs, uint64_t n, uint64_t align, F fn) {
+  const uint64_t nd = devs.size();
+  std::vector<std::future<int>> fs;
+  for (uint64_t i = 0; i < nd; i++) {
+    uint64_t lo, hi;
+    shard_range(n, nd, i, align, lo, hi);
+    if (lo >= hi) break;
+    Device* d = devs[i].get();
+    if (nd == 1) return fn(*d, lo, hi);
+    fs.push_back(std::async(std::launch::async, [=, &fn] { return fn(*d, lo, hi); }));
+  }
+  int rc = CORDAHIP_SUCCESS;
+  for (auto& f : fs) {
+    const int r = f.get();
+    if (r != CORDAHIP_SUCCESS && rc == CORDAHIP_SUCCESS) rc = r;
+  }
+  return rc;
+}
+
+// ---- ticket pool -------------------------------------------------------------
+struct JobState {
+  std::mutex m;
+  std::condition_variable cv;
+  bool done = false;
+  int rc = CORDAHIP_SUCCESS;
+};
+
+class WorkerPool {
+ public:
+  explicit WorkerPool(int nthreads) {
+    for (int i = 0; i < nthreads; i++) threads_.emplace_back([this] { run(); });
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) t.join();
+  }
+  void push(std::shared_ptr<JobState> st, std::function<int()> fn) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.emplace_back(std::move(st), std::move(fn));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      std::pair<std::shared_ptr<JobState>, std::function<int()>> job;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;  // stop_ and drained: queued jobs always run
+        job = std::move(q_.front());
+        q_.pop_front();
+      }
+      int rc;
+      try {
+        rc = job.second();
+      } catch (...) {
+        rc = CORDAHIP_ERR_OUT_OF_MEMORY;  // std::bad_alloc from host staging vectors
+      }
+      {
+        std::lock_guard<std::mutex> g(job.first->m);
+        job.first->rc = rc;
+        job.first->done = true;
+      }
+      job.first->cv.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::pair<std::shared_ptr<JobState>, std::function<int()>>> q_;
+  std::vector<std::thread> threads_;
+  bool stop_ = false;
+};
+
 }  // namespace
 
 struct cordahip_ctx {
   std::vector<std::unique_ptr<Device>> devs;
-  std::mutex mu;
+  std::mutex mu;  // guards next_ticket and jobs
   uint64_t next_ticket = 1;
-  std::unordered_map<uint64_t, std::shared_future<int>> jobs;
+  std::unordered_map<uint64_t, std::shared_ptr<JobState>> jobs;
+  std::unique_ptr<WorkerPool> pool;
 };
 
 namespace {
 
+uint64_t submit_job(cordahip_ctx* ctx, std::function<int()> fn) {
+  auto st = std::make_shared<JobState>();
+  uint64_t t;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    t = ctx->next_ticket++;
+    ctx->jobs.emplace(t, st);
+  }
+  ctx->pool->push(st, std::move(fn));
+  return t;
+}
+
+// timing slot for one *_device call (records `a` now on stream s)
+TimedCall* timed_begin(Device& d, hipStream_t s) {
+  int idx;
+  {
+    std::lock_guard<std::mutex> g(d.tmu);
+    idx = (int)(d.ring_next++ % kTimingRing);
+  }
+  TimedCall* tc = &d.ring[idx];
+  if (hipEventRecord(tc->a, s) != hipSuccess) return nullptr;
+  tl_last_call[d.uid] = idx;
+  return tc;
+}
+
 // Dense Ed25519 shard on one device: [lo, hi) of the caller's host arrays.
 int verify_shard_host(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
-                      const uint8_t* pre, uint64_t lo, uint64_t hi, uint8_t* status, uint64_t* verdict) {
+                      const uint8_t* pre, uint64_t lo, uint64_t hi, uint8_t* status, uint64_t* verdict,
+                      uint32_t flags) {
   std::lock_guard<std::mutex> g(d.mu);
   if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
   const uint64_t chunk = kChunk;
@@ -229,7 +382,6 @@ int verify_shard_host(Device& d, const uint8_t* keys, const uint8_t* sigs, const
       return CORDAHIP_ERR_OUT_OF_MEMORY;
   }
   int k = 0;
-  std::vector<uint64_t> vtmp;
   for (uint64_t off = lo; off < hi; off += chunk, k ^= 1) {
     Stage& st = d.stage[k];
     const uint64_t c = std::min<uint64_t>(chunk, hi - off);
@@ -243,7 +395,7 @@ int verify_shard_host(Device& d, const uint8_t* keys, const uint8_t* sigs, const
     e = e ? e
           : ed_verify_enqueue(d, st.keys.as<uint8_t>(), st.sigs.as<uint8_t>(), st.msgs.as<uint8_t>(), msg_len, c,
                               pre ? st.pre.as<uint8_t>() : nullptr, st.status.as<uint8_t>(),
-                              st.verdict.as<unsigned long long>(), s);
+                              st.verdict.as<unsigned long long>(), flags, s);
     e = e ? e : hipMemcpyAsync(status + off, st.status.p, c, hipMemcpyDeviceToHost, s);
     if (verdict && aligned)
       e = e ? e : hipMemcpyAsync(verdict + off / 64, st.verdict.p, ((c + 63) / 64) * 8, hipMemcpyDeviceToHost, s);
@@ -266,38 +418,63 @@ void verdict_from_status(const uint8_t* status, uint64_t n, uint64_t* verdict) {
 }
 
 int ed25519_dense_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
-                       uint32_t msg_len, const uint8_t* pre, uint64_t n, uint8_t* status, uint64_t* verdict) {
+                       uint32_t msg_len, const uint8_t* pre, uint64_t n, uint8_t* status, uint64_t* verdict,
+                       uint32_t flags) {
   if (n == 0) return CORDAHIP_SUCCESS;
-  const uint64_t nd = ctx->devs.size();
   // contiguous 64-aligned shards: no cross-device dependency
-  const uint64_t per = ((n + nd - 1) / nd + 63) / 64 * 64;
-  std::vector<std::future<int>> fs;
-  for (uint64_t i = 0; i < nd; i++) {
-    const uint64_t lo = std::min(n, i * per), hi = std::min(n, lo + per);
-    if (lo >= hi) break;
-    Device* d = ctx->devs[i].get();
-    fs.push_back(std::async(std::launch::async, [=] {
-      return verify_shard_host(*d, keys, sigs, msgs, msg_len, pre, lo, hi, status, verdict);
-    }));
-  }
-  int rc = CORDAHIP_SUCCESS;
-  for (auto& f : fs) {
-    const int r = f.get();
-    if (r != CORDAHIP_SUCCESS) rc = r;
-  }
+  const int rc = for_shards(ctx->devs, n, 64, [&](Device& d, uint64_t lo, uint64_t hi) {
+    return verify_shard_host(d, keys, sigs, msgs, msg_len, pre, lo, hi, status, verdict, flags);
+  });
   // chunk boundaries are 64-aligned except possibly a shard tail; recompute
   // the verdict words from status so every word is exact
   if (rc == CORDAHIP_SUCCESS && verdict) verdict_from_status(status, n, verdict);
   return rc;
 }
 
+// One device's shard [lo, hi) of packed ECDSA slot-layout lanes (host arrays).
+int ecdsa_shard_host(Device& d, const uint8_t* sch, const uint8_t* keys, const uint8_t* klen, const uint8_t* sigs,
+                     const uint8_t* slen, const uint8_t* msgs, const uint64_t* moff, const uint8_t* pre, uint64_t lo,
+                     uint64_t hi, uint8_t* st, uint32_t flags) {
+  const uint64_t m = hi - lo;
+  std::vector<uint64_t> off(m + 1);  // message offsets rebased to the shard
+  for (uint64_t j = 0; j <= m; j++) off[j] = moff[lo + j] - moff[lo];
+  const uint64_t mbytes = off[m];
+  std::lock_guard<std::mutex> g(d.ec_mu);
+  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  EcWork& w = d.ec;
+  hipStream_t s = d.stream;
+  if (w.ev && hipEventSynchronize(w.ev) != hipSuccess) return CORDAHIP_ERR_HIP;  // staging buffers below are shared
+  if (w.scheme.ensure(m) || w.keys.ensure(m * 65) || w.key_len.ensure(m) || w.sigs.ensure(m * 72) ||
+      w.sig_len.ensure(m) || w.msgs.ensure(std::max<uint64_t>(mbytes, 16)) || w.msg_off.ensure((m + 1) * 8) ||
+      w.pre.ensure(m) || w.status.ensure(m))
+    return CORDAHIP_ERR_OUT_OF_MEMORY;
+  const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+  hipError_t e = hipMemcpyAsync(w.scheme.p, sch + lo, m, h2d, s);
+  e = e ? e : hipMemcpyAsync(w.keys.p, keys + lo * 65, m * 65, h2d, s);
+  e = e ? e : hipMemcpyAsync(w.key_len.p, klen + lo, m, h2d, s);
+  e = e ? e : hipMemcpyAsync(w.sigs.p, sigs + lo * 72, m * 72, h2d, s);
+  e = e ? e : hipMemcpyAsync(w.sig_len.p, slen + lo, m, h2d, s);
+  if (mbytes) e = e ? e : hipMemcpyAsync(w.msgs.p, msgs + moff[lo], mbytes, h2d, s);
+  e = e ? e : hipMemcpyAsync(w.msg_off.p, off.data(), (m + 1) * 8, h2d, s);
+  e = e ? e : hipMemcpyAsync(w.pre.p, pre + lo, m, h2d, s);
+  e = e ? e
+        : ec_verify_enqueue(d, w.scheme.as<uint8_t>(), w.keys.as<uint8_t>(), w.key_len.as<uint8_t>(),
+                            w.sigs.as<uint8_t>(), w.sig_len.as<uint8_t>(), w.msgs.as<uint8_t>(), w.msg_off.as<uint64_t>(),
+                            0, m, w.pre.as<uint8_t>(), w.status.as<uint8_t>(), nullptr, flags, s);
+  e = e ? e : hipMemcpyAsync(st + lo, w.status.p, m, hipMemcpyDeviceToHost, s);
+  e = e ? e : hipStreamSynchronize(s);
+  return hip_err(e);
+}
+
 // ECDSA lanes of a generic batch: pack into the kernel's slot layout (65-byte
-// keys, 72-byte DER slots, CSR messages) and run K2 on one device. Signatures
-// longer than 72 bytes cannot hold r, s < n (some INTEGER needs > 33 bytes):
-// the host decides them with the same DER rules (der.hpp), the kernel still
-// decodes the key first so key errors keep precedence.
+// keys, 72-byte DER slots, CSR messages) and run K2 on contiguous 64-aligned
+// shards, one per context device. Signatures longer than 72 bytes cannot hold
+// r, s < n (some INTEGER needs > 33 bytes): the host decides them with the same
+// DER rules (der.hpp); the kernel still decodes the key first so key errors
+// keep precedence.
 int ecdsa_host_lanes(cordahip_ctx* ctx, const cordahip_sig_batch* b, const std::vector<uint64_t>& lanes) {
   const uint64_t m = lanes.size();
+  const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
   std::vector<uint8_t> sch(m), keys(m * 65, 0), klen(m), sigs(m * 72, 0), slen(m), pre(m, 0), st(m);
   std::vector<uint64_t> moff(m + 1, 0);
   for (uint64_t j = 0; j < m; j++) moff[j + 1] = moff[j] + (b->msg_off[lanes[j] + 1] - b->msg_off[lanes[j]]);
@@ -315,51 +492,33 @@ int ecdsa_host_lanes(cordahip_ctx* ctx, const cordahip_sig_batch* b, const std::
       slen[j] = (uint8_t)sl;
     } else {
       DerInt r, s;
-      pre[j] = ml == 0 ? CORDAHIP_STATUS_EMPTY
-                       : der_decode_sig(b->sig + b->sig_off[i], (uint32_t)std::min<uint64_t>(sl, 0xffffffffu), r, s)
-                             ? CORDAHIP_STATUS_BAD_SIG
-                             : CORDAHIP_STATUS_MALFORMED_SIG;
+      pre[j] = (ml == 0 && do_verify) ? CORDAHIP_STATUS_EMPTY
+               : der_decode_sig(b->sig + b->sig_off[i], (uint32_t)std::min<uint64_t>(sl, 0xffffffffu), r, s)
+                   ? CORDAHIP_STATUS_BAD_SIG
+                   : CORDAHIP_STATUS_MALFORMED_SIG;
       slen[j] = 72;
     }
     std::memcpy(&msgs[moff[j]], b->msg + b->msg_off[i], ml);
   }
-  Device& d = *ctx->devs[0];
-  std::lock_guard<std::mutex> g(d.ec_mu);
-  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
-  EcWork& w = d.ec;
-  hipStream_t s = d.stream;
-  if (w.ev && hipEventSynchronize(w.ev) != hipSuccess) return CORDAHIP_ERR_HIP;  // staging buffers below are shared
-  if (w.scheme.ensure(m) || w.keys.ensure(m * 65) || w.key_len.ensure(m) || w.sigs.ensure(m * 72) ||
-      w.sig_len.ensure(m) || w.msgs.ensure(msgs.size()) || w.msg_off.ensure((m + 1) * 8) || w.pre.ensure(m) ||
-      w.status.ensure(m))
-    return CORDAHIP_ERR_OUT_OF_MEMORY;
-  hipError_t e = hipMemcpyAsync(w.scheme.p, sch.data(), m, hipMemcpyHostToDevice, s);
-  e = e ? e : hipMemcpyAsync(w.keys.p, keys.data(), m * 65, hipMemcpyHostToDevice, s);
-  e = e ? e : hipMemcpyAsync(w.key_len.p, klen.data(), m, hipMemcpyHostToDevice, s);
-  e = e ? e : hipMemcpyAsync(w.sigs.p, sigs.data(), m * 72, hipMemcpyHostToDevice, s);
-  e = e ? e : hipMemcpyAsync(w.sig_len.p, slen.data(), m, hipMemcpyHostToDevice, s);
-  e = e ? e : hipMemcpyAsync(w.msgs.p, msgs.data(), msgs.size(), hipMemcpyHostToDevice, s);
-  e = e ? e : hipMemcpyAsync(w.msg_off.p, moff.data(), (m + 1) * 8, hipMemcpyHostToDevice, s);
-  e = e ? e : hipMemcpyAsync(w.pre.p, pre.data(), m, hipMemcpyHostToDevice, s);
-  e = e ? e
-        : ec_verify_enqueue(d, w.scheme.as<uint8_t>(), w.keys.as<uint8_t>(), w.key_len.as<uint8_t>(),
-                            w.sigs.as<uint8_t>(), w.sig_len.as<uint8_t>(), w.msgs.as<uint8_t>(), w.msg_off.as<uint64_t>(),
-                            0, m, w.pre.as<uint8_t>(), w.status.as<uint8_t>(), nullptr, s);
-  e = e ? e : hipMemcpyAsync(st.data(), w.status.p, m, hipMemcpyDeviceToHost, s);
-  e = e ? e : hipStreamSynchronize(s);
-  if (e != hipSuccess) return CORDAHIP_ERR_HIP;
+  const int rc = for_shards(ctx->devs, m, 64, [&](Device& d, uint64_t lo, uint64_t hi) {
+    return ecdsa_shard_host(d, sch.data(), keys.data(), klen.data(), sigs.data(), slen.data(), msgs.data(),
+                            moff.data(), pre.data(), lo, hi, st.data(), b->flags);
+  });
+  if (rc != CORDAHIP_SUCCESS) return rc;
   for (uint64_t j = 0; j < m; j++) b->status[lanes[j]] = st[j];
   return CORDAHIP_SUCCESS;
 }
 
 // Generic CSR batch: host-side scheme partition and length checks (the
-// Crypto.doVerify require() checks), then one dense device launch per
-// (scheme, message length) group.
+// Crypto.doVerify require() checks, or none under CORDAHIP_FLAG_IS_VALID), then
+// one dense device launch set per (scheme, message length) group.
 int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
   const uint64_t n = b->n;
   if (n == 0) return CORDAHIP_SUCCESS;
-  if (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off || !b->msg || !b->msg_off || !b->status)
+  if (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off || !b->msg || !b->msg_off || !b->status ||
+      (b->flags & ~CORDAHIP_FLAG_IS_VALID))
     return CORDAHIP_ERR_INVALID_ARG;
+  const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
   std::map<uint64_t, std::vector<uint64_t>> ed_groups;  // msg length -> lanes
   std::vector<uint64_t> ec_lanes;
   for (uint64_t i = 0; i < n; i++) {
@@ -393,13 +552,13 @@ int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
       const uint64_t i = idx[j];
       std::memcpy(&keys[j * 32], b->key + b->key_off[i], 32);
       const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
-      if (sl == 0 || mlen == 0) pre[j] = CORDAHIP_STATUS_EMPTY;          // Crypto.kt:475-476
-      else if (sl != 64) pre[j] = CORDAHIP_STATUS_MALFORMED_SIG;         // EdDSAEngine length check
+      if (do_verify && (sl == 0 || mlen == 0)) pre[j] = CORDAHIP_STATUS_EMPTY;  // Crypto.kt:475-476
+      else if (sl != 64) pre[j] = CORDAHIP_STATUS_MALFORMED_SIG;                // EdDSAEngine length check
       else std::memcpy(&sigs[j * 64], b->sig + b->sig_off[i], 64);
       if (mlen) std::memcpy(&msgs[j * mlen], b->msg + b->msg_off[i], mlen);
     }
     const int rc = ed25519_dense_host(ctx, keys.data(), sigs.data(), msgs.data(), (uint32_t)mlen, pre.data(), m,
-                                      st.data(), nullptr);
+                                      st.data(), nullptr, b->flags);
     if (rc != CORDAHIP_SUCCESS) return rc;
     for (uint64_t j = 0; j < m; j++) b->status[idx[j]] = st[j];
   }
@@ -411,10 +570,18 @@ int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
   return CORDAHIP_SUCCESS;
 }
 
+// Acquire d.tx for a host tx path (tx_mu held): the last device-path user may
+// still be running kernels on its own stream.
+int tx_acquire_host(Device& d) {
+  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  if (hipEventSynchronize(d.tx_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
+  return CORDAHIP_SUCCESS;
+}
+
 // Transaction ids for txs [t0, t1) on one device (offsets rebased to the shard).
 int tx_ids_shard(Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1) {
   std::lock_guard<std::mutex> g(d.tx_mu);
-  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  if (int rc = tx_acquire_host(d)) return rc;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1];
   const uint64_t nleaves = l1 - l0;
@@ -438,34 +605,22 @@ int tx_ids_shard(Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t 
                                  w.tx_status.as<uint8_t>(), s);
   e = e ? e : hipMemcpyAsync(b->txid + t0 * 32, w.txid.p, ntx * 32, hipMemcpyDeviceToHost, s);
   e = e ? e : hipMemcpyAsync(b->tx_status + t0, w.tx_status.p, ntx, hipMemcpyDeviceToHost, s);
+  e = e ? e : hipEventRecord(d.tx_ev, s);
   e = e ? e : hipStreamSynchronize(s);
   return hip_err(e);
 }
 
 int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
-  if (!b->leaf_off || !b->tx_leaf_off || !b->txid || !b->tx_status || (!b->leaf_bytes && b->ntx))
+  if (b->ntx && (!b->leaf_off || !b->tx_leaf_off || !b->txid || !b->tx_status || !b->leaf_bytes))
     return CORDAHIP_ERR_INVALID_ARG;
-  const uint64_t n = b->ntx, nd = ctx->devs.size();
-  if (n == 0) return CORDAHIP_SUCCESS;
-  const uint64_t per = (n + nd - 1) / nd;  // contiguous tx shards, independent trees
-  std::vector<std::future<int>> fs;
-  for (uint64_t i = 0; i < nd; i++) {
-    const uint64_t t0 = std::min(n, i * per), t1 = std::min(n, t0 + per);
-    if (t0 >= t1) break;
-    Device* d = ctx->devs[i].get();
-    fs.push_back(std::async(std::launch::async, [=] { return tx_ids_shard(*d, b, t0, t1); }));
-  }
-  int rc = CORDAHIP_SUCCESS;
-  for (auto& f : fs) {
-    const int r = f.get();
-    if (r != CORDAHIP_SUCCESS) rc = r;
-  }
-  return rc;
+  if (b->ntx == 0) return CORDAHIP_SUCCESS;
+  // contiguous tx shards: a transaction's tree stays on one device
+  return for_shards(ctx->devs, b->ntx, 1, [&](Device& d, uint64_t t0, uint64_t t1) { return tx_ids_shard(d, b, t0, t1); });
 }
 
 int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   const uint64_t ntx = b->tx.ntx;
-  if (!b->tx_sig_off || !b->first_bad_sig || !b->sig_status) return CORDAHIP_ERR_INVALID_ARG;
+  if (ntx && (!b->tx_sig_off || !b->first_bad_sig || !b->sig_status)) return CORDAHIP_ERR_INVALID_ARG;
   int rc = tx_ids_impl(ctx, &b->tx);
   if (rc != CORDAHIP_SUCCESS) return rc;
   const uint64_t nsig = ntx ? b->tx_sig_off[ntx] : 0;
@@ -476,8 +631,9 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
     for (uint64_t s = b->tx_sig_off[t]; s < b->tx_sig_off[t + 1]; s++) std::memcpy(&msgs[s * 32], b->tx.txid + t * 32, 32);
   for (uint64_t s = 0; s <= nsig; s++) moff[s] = s * 32;
   if (nsig) {
+    // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
     cordahip_sig_batch sb{nsig, b->scheme, b->key, b->key_off, b->sig, b->sig_off, msgs.data(), moff.data(),
-                          b->sig_status, nullptr};
+                          b->sig_status, nullptr, 0u};
     rc = sig_verify_impl(ctx, &sb);
     if (rc != CORDAHIP_SUCCESS) return rc;
   }
@@ -570,12 +726,12 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
     if (ma)
       e = e ? e
             : ed_verify_enqueue(d, st.ed_keys.as<uint8_t>(), st.ed_sigs.as<uint8_t>(), st.ed_msgs.as<uint8_t>(),
-                                (uint32_t)eml, ma, nullptr, st.ed_status.as<uint8_t>(), nullptr, s);
+                                (uint32_t)eml, ma, nullptr, st.ed_status.as<uint8_t>(), nullptr, 0u, s);
     if (mc && e == hipSuccess) {
       std::lock_guard<std::mutex> ge(d.ec_mu);
       e = ec_verify_enqueue(d, st.ec_scheme.as<uint8_t>(), st.ec_keys.as<uint8_t>(), st.ec_key_len.as<uint8_t>(),
                             st.ec_sigs.as<uint8_t>(), st.ec_sig_len.as<uint8_t>(), st.ec_msgs.as<uint8_t>(), nullptr,
-                            (uint32_t)cml, mc, nullptr, st.ec_status.as<uint8_t>(), nullptr, s);
+                            (uint32_t)cml, mc, nullptr, st.ec_status.as<uint8_t>(), nullptr, 0u, s);
     }
     if (ma) e = e ? e : hipMemcpyAsync(b->ed_status + a, st.ed_status.p, ma, d2h, s);
     if (mc) e = e ? e : hipMemcpyAsync(b->ec_status + c, st.ec_status.p, mc, d2h, s);
@@ -592,19 +748,19 @@ int stream_verify_impl(cordahip_ctx* ctx, const cordahip_stream_batch* b) {
                    !b->ec_status || (b->ec_msg_len && !b->ec_msgs))))
     return CORDAHIP_ERR_INVALID_ARG;
   const uint64_t nd = ctx->devs.size();
-  const uint64_t pe = ((b->n_ed + nd - 1) / nd + 63) / 64 * 64, pc = ((b->n_ec + nd - 1) / nd + 63) / 64 * 64;
   std::vector<std::future<int>> fs;
   for (uint64_t i = 0; i < nd; i++) {
-    const uint64_t e0 = std::min(b->n_ed, i * pe), e1 = std::min(b->n_ed, e0 + pe);
-    const uint64_t c0 = std::min(b->n_ec, i * pc), c1 = std::min(b->n_ec, c0 + pc);
-    if (e0 >= e1 && c0 >= c1) break;
+    uint64_t e0, e1, c0, c1;
+    shard_range(b->n_ed, nd, i, 64, e0, e1);
+    shard_range(b->n_ec, nd, i, 64, c0, c1);
+    if (e0 >= e1 && c0 >= c1) continue;
     Device* d = ctx->devs[i].get();
     fs.push_back(std::async(std::launch::async, [=] { return stream_shard(*d, b, e0, e1, c0, c1); }));
   }
   int rc = CORDAHIP_SUCCESS;
   for (auto& f : fs) {
     const int r = f.get();
-    if (r != CORDAHIP_SUCCESS) rc = r;
+    if (r != CORDAHIP_SUCCESS && rc == CORDAHIP_SUCCESS) rc = r;
   }
   return rc;
 }
@@ -613,7 +769,7 @@ int stream_verify_impl(cordahip_ctx* ctx, const cordahip_stream_batch* b) {
 // filtered leaves, K6 evaluates each partial tree and compares.
 int filtered_tx_shard(Device& d, const cordahip_filtered_tx_batch* b, uint64_t t0, uint64_t t1) {
   std::lock_guard<std::mutex> g(d.tx_mu);
-  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
+  if (int rc = tx_acquire_host(d)) return rc;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
   const uint64_t b0 = nleaves ? b->leaf_off[l0] : 0, b1 = nleaves ? b->leaf_off[l1] : 0;
@@ -649,35 +805,54 @@ int filtered_tx_shard(Device& d, const cordahip_filtered_tx_batch* b, uint64_t t
                                 w.tok_hash.as<uint8_t>(), w.tx_tok_off.as<uint64_t>(), w.root.as<uint8_t>(), ntx,
                                 w.stack.as<uint32_t>(), w.tx_status.as<uint8_t>(), s);
   e = e ? e : hipMemcpyAsync(b->tx_status + t0, w.tx_status.p, ntx, hipMemcpyDeviceToHost, s);
+  e = e ? e : hipEventRecord(d.tx_ev, s);
   e = e ? e : hipStreamSynchronize(s);
   return hip_err(e);
 }
 
 int filtered_tx_impl(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* b) {
-  const uint64_t n = b->ntx, nd = ctx->devs.size();
+  const uint64_t n = b->ntx;
   if (n == 0) return CORDAHIP_SUCCESS;
   if (!b->leaf_off || !b->tx_leaf_off || !b->tx_tok_off || !b->root || !b->tx_status ||
       (!b->tok && b->tx_tok_off[n]) || (!b->tok_hash && b->tx_tok_off[n]))
     return CORDAHIP_ERR_INVALID_ARG;
-  const uint64_t per = (n + nd - 1) / nd;  // contiguous tx shards, independent trees
-  std::vector<std::future<int>> fs;
-  for (uint64_t i = 0; i < nd; i++) {
-    const uint64_t t0 = std::min(n, i * per), t1 = std::min(n, t0 + per);
-    if (t0 >= t1) break;
-    Device* d = ctx->devs[i].get();
-    fs.push_back(std::async(std::launch::async, [=] { return filtered_tx_shard(*d, b, t0, t1); }));
-  }
-  int rc = CORDAHIP_SUCCESS;
-  for (auto& f : fs) {
-    const int r = f.get();
-    if (r != CORDAHIP_SUCCESS) rc = r;
-  }
-  return rc;
+  return for_shards(ctx->devs, n, 1, [&](Device& d, uint64_t t0, uint64_t t1) { return filtered_tx_shard(d, b, t0, t1); });
 }
 
 Device* dev_at(cordahip_ctx* ctx, int device) {
   if (!ctx || device < 0 || device >= (int)ctx->devs.size()) return nullptr;
   return ctx->devs[device].get();
+}
+
+void free_device(Device& d) {
+  (void)hipSetDevice(d.id);
+  for (auto& st : d.stage) {
+    for (DevBuf* b : {&st.keys, &st.sigs, &st.msgs, &st.pre, &st.status, &st.verdict}) b->release();
+    if (st.stream) (void)hipStreamDestroy(st.stream);
+  }
+  for (auto& st : d.sstage) {
+    for (DevBuf* b : {&st.ed_keys, &st.ed_sigs, &st.ed_msgs, &st.ed_status, &st.ec_scheme, &st.ec_keys,
+                      &st.ec_key_len, &st.ec_sigs, &st.ec_sig_len, &st.ec_msgs, &st.ec_status})
+      b->release();
+    if (st.stream) (void)hipStreamDestroy(st.stream);
+  }
+  for (DevBuf* b : {&d.tx.leaf_bytes, &d.tx.leaf_off, &d.tx.tx_leaf_off, &d.tx.hashes, &d.tx.txid, &d.tx.tx_status,
+                    &d.tx.tx_sig_off, &d.tx.msgs, &d.tx.tok, &d.tx.tok_hash, &d.tx.tx_tok_off, &d.tx.root,
+                    &d.tx.stack})
+    b->release();
+  for (DevBuf* b : {&d.ec.scheme, &d.ec.keys, &d.ec.key_len, &d.ec.sigs, &d.ec.sig_len, &d.ec.msgs, &d.ec.msg_off,
+                    &d.ec.pre, &d.ec.status, &d.ec.counters, &d.ec.perm, &d.ec.ws})
+    b->release();
+  d.ed_ws.release();
+  for (hipEvent_t ev : {d.ec.ev, d.ed_ev, d.tx_ev})
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto& tc : d.ring)
+    for (hipEvent_t ev : {tc.a, tc.b})
+      if (ev) (void)hipEventDestroy(ev);
+  if (d.gtab_k1) (void)hipFree(d.gtab_k1);
+  if (d.gtab_r1) (void)hipFree(d.gtab_r1);
+  if (d.btab) (void)hipFree(d.btab);
+  if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
 }  // namespace
@@ -700,71 +875,63 @@ const char* cordahip_strerror(int code) {
   }
 }
 
+void cordahip_shard_range(uint64_t n, uint32_t nshards, uint32_t shard, uint64_t align, uint64_t* lo, uint64_t* hi) {
+  uint64_t a, b;
+  shard_range(n, nshards, shard, align, a, b);
+  if (lo) *lo = a;
+  if (hi) *hi = b;
+}
+
 int cordahip_init(uint32_t device_mask, cordahip_ctx** out) {
   if (!out) return CORDAHIP_ERR_INVALID_ARG;
   *out = nullptr;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return CORDAHIP_ERR_NO_DEVICE;
   auto ctx = std::make_unique<cordahip_ctx>();
-  for (int d = 0; d < count && d < 32; d++) {
+  int rc = CORDAHIP_SUCCESS;
+  for (int d = 0; d < count && d < 32 && rc == CORDAHIP_SUCCESS; d++) {
     if (device_mask && !((device_mask >> d) & 1u)) continue;
-    auto dev = std::make_unique<Device>();
-    dev->id = d;
-    if (hipSetDevice(d) != hipSuccess) return CORDAHIP_ERR_HIP;
-    if (hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking) != hipSuccess) return CORDAHIP_ERR_HIP;
-    if (hipEventCreate(&dev->ev0) != hipSuccess || hipEventCreate(&dev->ev1) != hipSuccess) return CORDAHIP_ERR_HIP;
-    if (hipMalloc(reinterpret_cast<void**>(&dev->btab), ed25519_btable_bytes()) != hipSuccess)
-      return CORDAHIP_ERR_OUT_OF_MEMORY;
-    if (launch_ed25519_btable(dev->btab, dev->stream) != hipSuccess) return CORDAHIP_ERR_HIP;
-    if (hipMalloc(reinterpret_cast<void**>(&dev->gtab_k1), ecdsa_gtable_bytes()) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&dev->gtab_r1), ecdsa_gtable_bytes()) != hipSuccess)
-      return CORDAHIP_ERR_OUT_OF_MEMORY;
-    if (launch_ecdsa_gtables(dev->gtab_k1, dev->gtab_r1, dev->stream) != hipSuccess) return CORDAHIP_ERR_HIP;
-    if (hipStreamSynchronize(dev->stream) != hipSuccess) return CORDAHIP_ERR_HIP;
-    ctx->devs.push_back(std::move(dev));
+    ctx->devs.push_back(std::make_unique<Device>());
+    Device& dev = *ctx->devs.back();
+    dev.id = d;
+    dev.uid = g_device_uid.fetch_add(1);
+    if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&dev.tx_ev, hipEventDisableTiming) != hipSuccess) {
+      rc = CORDAHIP_ERR_HIP;
+      break;
+    }
+    for (auto& tc : dev.ring)
+      if (hipEventCreate(&tc.a) != hipSuccess || hipEventCreate(&tc.b) != hipSuccess) rc = CORDAHIP_ERR_HIP;
+    if (rc != CORDAHIP_SUCCESS) break;
+    if (hipMalloc(reinterpret_cast<void**>(&dev.btab), ed25519_btable_bytes()) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dev.gtab_k1), ecdsa_gtable_bytes()) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dev.gtab_r1), ecdsa_gtable_bytes()) != hipSuccess) {
+      rc = CORDAHIP_ERR_OUT_OF_MEMORY;
+      break;
+    }
+    if (launch_ed25519_btable(dev.btab, dev.stream) != hipSuccess ||
+        launch_ecdsa_gtables(dev.gtab_k1, dev.gtab_r1, dev.stream) != hipSuccess ||
+        hipEventRecord(dev.tx_ev, dev.stream) != hipSuccess || hipStreamSynchronize(dev.stream) != hipSuccess)
+      rc = CORDAHIP_ERR_HIP;
   }
-  if (ctx->devs.empty()) return CORDAHIP_ERR_NO_DEVICE;
+  if (rc == CORDAHIP_SUCCESS && ctx->devs.empty()) rc = CORDAHIP_ERR_NO_DEVICE;
+  if (rc != CORDAHIP_SUCCESS) {
+    for (auto& d : ctx->devs) free_device(*d);
+    return rc;
+  }
+  ctx->pool = std::make_unique<WorkerPool>((int)std::max<size_t>(2, 2 * ctx->devs.size()));
   *out = ctx.release();
   return CORDAHIP_SUCCESS;
 }
 
 void cordahip_shutdown(cordahip_ctx* ctx) {
   if (!ctx) return;
+  ctx->pool.reset();  // runs every queued job to completion, joins the workers
   {
     std::lock_guard<std::mutex> g(ctx->mu);
-    for (auto& kv : ctx->jobs) kv.second.wait();
     ctx->jobs.clear();
   }
-  for (auto& d : ctx->devs) {
-    (void)hipSetDevice(d->id);
-    for (auto& st : d->stage) {
-      for (DevBuf* b : {&st.keys, &st.sigs, &st.msgs, &st.pre, &st.status, &st.verdict})
-        if (b->p) (void)hipFree(b->p);
-      if (st.stream) (void)hipStreamDestroy(st.stream);
-    }
-    for (auto& st : d->sstage) {
-      for (DevBuf* b : {&st.ed_keys, &st.ed_sigs, &st.ed_msgs, &st.ed_status, &st.ec_scheme, &st.ec_keys,
-                        &st.ec_key_len, &st.ec_sigs, &st.ec_sig_len, &st.ec_msgs, &st.ec_status})
-        if (b->p) (void)hipFree(b->p);
-      if (st.stream) (void)hipStreamDestroy(st.stream);
-    }
-    for (DevBuf* b : {&d->tx.leaf_bytes, &d->tx.leaf_off, &d->tx.tx_leaf_off, &d->tx.hashes, &d->tx.txid,
-                      &d->tx.tx_status, &d->tx.tx_sig_off, &d->tx.msgs, &d->tx.tok, &d->tx.tok_hash,
-                      &d->tx.tx_tok_off, &d->tx.root, &d->tx.stack})
-      if (b->p) (void)hipFree(b->p);
-    for (DevBuf* b : {&d->ec.scheme, &d->ec.keys, &d->ec.key_len, &d->ec.sigs, &d->ec.sig_len, &d->ec.msgs,
-                      &d->ec.msg_off, &d->ec.pre, &d->ec.status, &d->ec.counters, &d->ec.perm, &d->ec.ws})
-      if (b->p) (void)hipFree(b->p);
-    if (d->ec.ev) (void)hipEventDestroy(d->ec.ev);
-    if (d->gtab_k1) (void)hipFree(d->gtab_k1);
-    if (d->gtab_r1) (void)hipFree(d->gtab_r1);
-    if (d->btab) (void)hipFree(d->btab);
-    if (d->ed_ws.p) (void)hipFree(d->ed_ws.p);
-    if (d->ed_ev) (void)hipEventDestroy(d->ed_ev);
-    if (d->ev0) (void)hipEventDestroy(d->ev0);
-    if (d->ev1) (void)hipEventDestroy(d->ev1);
-    if (d->stream) (void)hipStreamDestroy(d->stream);
-  }
+  for (auto& d : ctx->devs) free_device(*d);
   delete ctx;
 }
 
@@ -789,36 +956,64 @@ int cordahip_sig_verify(cordahip_ctx* ctx, const cordahip_sig_batch* batch) {
 int cordahip_sig_submit(cordahip_ctx* ctx, const cordahip_sig_batch* batch, uint64_t* ticket) {
   if (!ctx || !batch || !ticket) return CORDAHIP_ERR_INVALID_ARG;
   const cordahip_sig_batch copy = *batch;  // descriptor by value; buffers stay caller-owned
-  std::shared_future<int> f = std::async(std::launch::async, [ctx, copy] { return sig_verify_impl(ctx, &copy); });
-  std::lock_guard<std::mutex> g(ctx->mu);
-  *ticket = ctx->next_ticket++;
-  ctx->jobs.emplace(*ticket, f);
+  *ticket = submit_job(ctx, [ctx, copy] { return sig_verify_impl(ctx, &copy); });
+  return CORDAHIP_SUCCESS;
+}
+
+int cordahip_tx_submit(cordahip_ctx* ctx, const cordahip_signed_tx_batch* batch, uint64_t* ticket) {
+  if (!ctx || !batch || !ticket) return CORDAHIP_ERR_INVALID_ARG;
+  const cordahip_signed_tx_batch copy = *batch;
+  *ticket = submit_job(ctx, [ctx, copy] { return signed_tx_impl(ctx, &copy); });
+  return CORDAHIP_SUCCESS;
+}
+
+int cordahip_txid_submit(cordahip_ctx* ctx, const cordahip_txid_batch* batch, uint64_t* ticket) {
+  if (!ctx || !batch || !ticket) return CORDAHIP_ERR_INVALID_ARG;
+  const cordahip_txid_batch copy = *batch;
+  *ticket = submit_job(ctx, [ctx, copy] { return tx_ids_impl(ctx, &copy); });
+  return CORDAHIP_SUCCESS;
+}
+
+int cordahip_filtered_tx_submit(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch, uint64_t* ticket) {
+  if (!ctx || !batch || !ticket) return CORDAHIP_ERR_INVALID_ARG;
+  const cordahip_filtered_tx_batch copy = *batch;
+  *ticket = submit_job(ctx, [ctx, copy] { return filtered_tx_impl(ctx, &copy); });
   return CORDAHIP_SUCCESS;
 }
 
 int cordahip_wait(cordahip_ctx* ctx, uint64_t ticket, int64_t timeout_ns) {
   if (!ctx) return CORDAHIP_ERR_INVALID_ARG;
-  std::shared_future<int> f;
+  std::shared_ptr<JobState> st;
   {
     std::lock_guard<std::mutex> g(ctx->mu);
     auto it = ctx->jobs.find(ticket);
     if (it == ctx->jobs.end()) return CORDAHIP_ERR_UNKNOWN_TICKET;
-    f = it->second;
+    st = it->second;
   }
-  if (timeout_ns >= 0 && f.wait_for(std::chrono::nanoseconds(timeout_ns)) != std::future_status::ready)
-    return CORDAHIP_ERR_TIMEOUT;
-  const int rc = f.get();
+  int rc;
+  {
+    std::unique_lock<std::mutex> g(st->m);
+    if (timeout_ns < 0) st->cv.wait(g, [&] { return st->done; });
+    else if (!st->cv.wait_for(g, std::chrono::nanoseconds(timeout_ns), [&] { return st->done; }))
+      return CORDAHIP_ERR_TIMEOUT;
+    rc = st->rc;
+  }
   std::lock_guard<std::mutex> g(ctx->mu);
-  ctx->jobs.erase(ticket);
+  ctx->jobs.erase(ticket);  // released: the ticket is single-use
   return rc;
 }
 
 int cordahip_poll(cordahip_ctx* ctx, uint64_t ticket) {
   if (!ctx) return CORDAHIP_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  auto it = ctx->jobs.find(ticket);
-  if (it == ctx->jobs.end()) return CORDAHIP_ERR_UNKNOWN_TICKET;
-  return it->second.wait_for(std::chrono::seconds(0)) == std::future_status::ready ? 1 : 0;
+  std::shared_ptr<JobState> st;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    auto it = ctx->jobs.find(ticket);
+    if (it == ctx->jobs.end()) return CORDAHIP_ERR_UNKNOWN_TICKET;
+    st = it->second;
+  }
+  std::lock_guard<std::mutex> g(st->m);
+  return st->done ? 1 : 0;
 }
 
 int cordahip_ed25519_verify_device(cordahip_ctx* ctx, int device, const void* d_keys, const void* d_sigs,
@@ -831,12 +1026,12 @@ int cordahip_ed25519_verify_device(cordahip_ctx* ctx, int device, const void* d_
   if (msg_len == 32 && (reinterpret_cast<uintptr_t>(d_msgs) & 15)) return CORDAHIP_ERR_INVALID_ARG;
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);  // NULL = the device's null stream
-  hipError_t e = hipEventRecord(d->ev0, s);
-  e = e ? e
-        : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
-                            static_cast<const uint8_t*>(d_msgs), msg_len, n, nullptr, static_cast<uint8_t*>(d_status),
-                            static_cast<unsigned long long*>(d_verdict), s);
-  e = e ? e : hipEventRecord(d->ev1, s);
+  TimedCall* tc = timed_begin(*d, s);
+  if (!tc) return CORDAHIP_ERR_HIP;
+  hipError_t e = ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
+                                   static_cast<const uint8_t*>(d_msgs), msg_len, n, nullptr,
+                                   static_cast<uint8_t*>(d_status), static_cast<unsigned long long*>(d_verdict), 0u, s);
+  e = e ? e : hipEventRecord(tc->b, s);
   return hip_err(e);
 }
 
@@ -849,30 +1044,33 @@ int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_sc
   std::lock_guard<std::mutex> g(d->ec_mu);
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
-  hipError_t e = hipEventRecord(d->ev0, s);
-  e = e ? e
-        : ec_verify_enqueue(*d, static_cast<const uint8_t*>(d_scheme), static_cast<const uint8_t*>(d_keys),
-                            static_cast<const uint8_t*>(d_key_len), static_cast<const uint8_t*>(d_sigs),
-                            static_cast<const uint8_t*>(d_sig_len), static_cast<const uint8_t*>(d_msgs), nullptr,
-                            msg_len, n, nullptr, static_cast<uint8_t*>(d_status),
-                            static_cast<unsigned long long*>(d_verdict), s);
-  e = e ? e : hipEventRecord(d->ev1, s);
+  TimedCall* tc = timed_begin(*d, s);
+  if (!tc) return CORDAHIP_ERR_HIP;
+  hipError_t e = ec_verify_enqueue(*d, static_cast<const uint8_t*>(d_scheme), static_cast<const uint8_t*>(d_keys),
+                                   static_cast<const uint8_t*>(d_key_len), static_cast<const uint8_t*>(d_sigs),
+                                   static_cast<const uint8_t*>(d_sig_len), static_cast<const uint8_t*>(d_msgs), nullptr,
+                                   msg_len, n, nullptr, static_cast<uint8_t*>(d_status),
+                                   static_cast<unsigned long long*>(d_verdict), 0u, s);
+  e = e ? e : hipEventRecord(tc->b, s);
   return hip_err(e);
 }
 
 double cordahip_last_kernel_ms(cordahip_ctx* ctx, int device) {
   Device* d = dev_at(ctx, device);
   if (!d) return -1.0;
-  if (hipEventSynchronize(d->ev1) != hipSuccess) return -1.0;
+  auto it = tl_last_call.find(d->uid);
+  if (it == tl_last_call.end()) return -1.0;
+  const TimedCall& tc = d->ring[it->second];
+  if (hipEventSynchronize(tc.b) != hipSuccess) return -1.0;
   float ms = -1.f;
-  if (hipEventElapsedTime(&ms, d->ev0, d->ev1) != hipSuccess) return -1.0;
+  if (hipEventElapsedTime(&ms, tc.a, tc.b) != hipSuccess) return -1.0;
   return ms;
 }
 
 int cordahip_ed25519_verify_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                                  uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict) {
   if (!ctx || (n && (!keys || !sigs || !status || (msg_len && !msgs)))) return CORDAHIP_ERR_INVALID_ARG;
-  return ed25519_dense_host(ctx, keys, sigs, msgs, msg_len, nullptr, n, status, verdict);
+  return ed25519_dense_host(ctx, keys, sigs, msgs, msg_len, nullptr, n, status, verdict, 0u);
 }
 
 int cordahip_filtered_tx_verify(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch) {
@@ -931,22 +1129,30 @@ int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, cons
     return CORDAHIP_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(d->tx_mu);
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
-  if (d->tx.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) || d->tx.msgs.ensure(std::max<uint64_t>(nsig, 1) * 32))
-    return CORDAHIP_ERR_OUT_OF_MEMORY;
+  TxWork& w = d->tx;
+  if (w.hashes.cap < std::max<uint64_t>(nleaves, 1) * 32 || w.msgs.cap < std::max<uint64_t>(nsig, 1) * 32) {
+    // growing frees the old buffers: the previous user's kernels must be done
+    if (hipEventSynchronize(d->tx_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) || w.msgs.ensure(std::max<uint64_t>(nsig, 1) * 32))
+      return CORDAHIP_ERR_OUT_OF_MEMORY;
+  }
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
-  hipError_t e = hipEventRecord(d->ev0, s);
+  TimedCall* tc = timed_begin(*d, s);
+  if (!tc) return CORDAHIP_ERR_HIP;
+  hipError_t e = hipStreamWaitEvent(s, d->tx_ev, 0);  // the previous user of w.hashes / w.msgs is done
   e = e ? e : launch_sha256_leaves(static_cast<const uint8_t*>(d_leaf_bytes), static_cast<const uint64_t*>(d_leaf_off),
-                                   nleaves, d->tx.hashes.as<uint32_t>(), s);
-  e = e ? e : launch_merkle_root(d->tx.hashes.as<uint32_t>(), static_cast<const uint64_t*>(d_tx_leaf_off), ntx,
+                                   nleaves, w.hashes.as<uint32_t>(), s);
+  e = e ? e : launch_merkle_root(w.hashes.as<uint32_t>(), static_cast<const uint64_t*>(d_tx_leaf_off), ntx,
                                  static_cast<uint8_t*>(d_txid), static_cast<uint8_t*>(d_tx_status), s);
   e = e ? e : launch_gather_txid(static_cast<const uint8_t*>(d_txid), static_cast<const uint64_t*>(d_tx_sig_off), ntx,
-                                 d->tx.msgs.as<uint8_t>(), s);
+                                 w.msgs.as<uint8_t>(), s);
   e = e ? e : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
-                                d->tx.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status),
-                                nullptr, s);
+                                w.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status), nullptr,
+                                0u, s);
+  e = e ? e : hipEventRecord(d->tx_ev, s);  // fences w.hashes / w.msgs for the next user
   e = e ? e : launch_tx_reduce(static_cast<const uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off),
                                ntx, static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);
-  e = e ? e : hipEventRecord(d->ev1, s);
+  e = e ? e : hipEventRecord(tc->b, s);
   return hip_err(e);
 }
 

@@ -609,7 +609,7 @@ CDEV uint8_t x_check(const jpt& acc, const u256& r) {
 template <class C>
 CDEV uint8_t ecdsa_prep_lane(const uint8_t* __restrict__ key, uint32_t key_len, const uint8_t* __restrict__ sig,
                              uint32_t sig_len, const uint8_t* __restrict__ msg, uint64_t msg_len, uint8_t pre_status,
-                             uint32_t* __restrict__ rec) {
+                             bool empty_is_error, uint32_t* __restrict__ rec) {
   using N = typename C::N;
   using F = typename C::F;
   f29 zprod;
@@ -628,8 +628,8 @@ CDEV uint8_t ecdsa_prep_lane(const uint8_t* __restrict__ key, uint32_t key_len, 
     st = kStatusBadKey;  // key built before verify
   } else if (pre_status != kStatusOk) {
     st = pre_status;
-  } else if (sig_len == 0 || msg_len == 0) {
-    st = kStatusEmpty;  // Crypto.kt:475-476
+  } else if (empty_is_error && (sig_len == 0 || msg_len == 0)) {
+    st = kStatusEmpty;  // doVerify: Crypto.kt:475-476 (isValid: DER decode / hash as usual)
   } else {
     DerInt dr, ds;
     if (!der_decode_sig(sig, sig_len, dr, ds)) {
@@ -763,22 +763,6 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
     }
   }
   return x_check<C>(acc, r);
-}
-
-// Retired single-kernel lane (no longer dispatched; predates the affine tables): the split
-// path's prep and ladder over a private record, with a per-lane Fermat inversion.
-template <class C>
-CDEV uint8_t ecdsa_verify_lane(const uint8_t* __restrict__ key, uint32_t key_len, const uint8_t* __restrict__ sig,
-                               uint32_t sig_len, const uint8_t* __restrict__ msg, uint64_t msg_len,
-                               const uint32_t* __restrict__ gtab, uint8_t pre_status) {
-  __attribute__((aligned(16))) uint32_t rec[kEcWords];
-  const uint8_t st = ecdsa_prep_lane<C>(key, key_len, sig, sig_len, msg, msg_len, pre_status, rec);
-  if (st != kEcPending) return st;
-  u256 sm, w;
-  ld256(sm, rec + kEcS);
-  mont_pow_const<typename C::N, typename C::Nm2>(w, sm);
-  st256(rec + kEcW, w);
-  return ecdsa_ladder_lane<C>(rec, gtab);
 }
 
 // ---- signing (corpus generation for the C3 / C5 benchmarks) -----------------
@@ -1007,33 +991,6 @@ __global__ void __launch_bounds__(256) ecdsa_scatter_kernel(const uint8_t* __res
   }
 }
 
-// keys: 65-byte slots + key_len; sigs: 72-byte slots + sig_len; msgs: CSR
-// (msg_off) or fixed stride msg_len. perm may be null (identity).
-__global__ void __launch_bounds__(256) ecdsa_verify_kernel(
-    const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, const uint8_t* __restrict__ keys,
-    const uint8_t* __restrict__ key_len, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ sig_len,
-    const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ msg_off, uint32_t msg_len, uint64_t n,
-    const uint32_t* __restrict__ gtab_k1, const uint32_t* __restrict__ gtab_r1, const uint8_t* __restrict__ pre_status,
-    uint8_t* __restrict__ status) {
-  const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (slot >= n) return;
-  const uint64_t i = perm ? perm[slot] : slot;
-  const uint8_t sch = scheme[i];
-  const uint8_t* key = keys + i * 65;
-  const uint8_t* sig = sigs + i * 72;
-  const uint8_t* msg = msg_off ? msgs + msg_off[i] : msgs + i * (uint64_t)msg_len;
-  const uint64_t ml = msg_off ? msg_off[i + 1] - msg_off[i] : msg_len;
-  const uint8_t pre = pre_status ? pre_status[i] : kStatusOk;
-  uint8_t st;
-  if (sch == 2)
-    st = ecdsa_verify_lane<Curve<2>>(key, key_len[i], sig, sig_len[i], msg, ml, gtab_k1, pre);
-  else if (sch == 3)
-    st = ecdsa_verify_lane<Curve<3>>(key, key_len[i], sig, sig_len[i], msg, ml, gtab_r1, pre);
-  else
-    st = kStatusUnsupported;
-  status[i] = st;
-}
-
 __global__ void __launch_bounds__(256) verdict_kernel(const uint8_t* __restrict__ status, uint64_t n,
                                                      unsigned long long* __restrict__ verdict) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1046,7 +1003,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
     const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, const uint8_t* __restrict__ keys,
     const uint8_t* __restrict__ key_len, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ sig_len,
     const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ msg_off, uint32_t msg_len, uint64_t base,
-    uint64_t m, const uint8_t* __restrict__ pre_status, uint8_t* __restrict__ status, uint32_t* __restrict__ ws) {
+    uint64_t m, const uint8_t* __restrict__ pre_status, uint8_t* __restrict__ status, uint32_t* __restrict__ ws,
+    uint32_t empty_is_error) {
   const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= m) return;
   const uint64_t slot = base + li;
@@ -1056,13 +1014,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
   const uint8_t* sig = sigs + i * 72;
   const uint8_t* msg = msg_off ? msgs + msg_off[i] : msgs + i * (uint64_t)msg_len;
   const uint64_t ml = msg_off ? msg_off[i + 1] - msg_off[i] : msg_len;
-  const uint8_t pre = pre_status ? pre_status[i] : kStatusOk;
+  uint8_t pre = pre_status ? pre_status[i] : kStatusOk;
+  // a DER signature longer than its 72-byte slot is not representable in the
+  // dense layout (r, s < n always fit 72 bytes, so BC would reject it too): the
+  // lane is decided without reading past the slot. The generic CSR path decodes
+  // such signatures exactly on the host (cordahip.cpp ecdsa_host_lanes).
+  const uint32_t sl = sig_len[i];
+  if (sl > 72 && pre == kStatusOk) pre = (ml == 0 && empty_is_error) ? kStatusEmpty : kStatusMalformedSig;
   uint32_t* rec = ws + li * kEcWords;
   uint8_t st;
   if (sch == 2)
-    st = ecdsa_prep_lane<Curve<2>>(key, key_len[i], sig, sig_len[i], msg, ml, pre, rec);
+    st = ecdsa_prep_lane<Curve<2>>(key, key_len[i], sig, sl > 72 ? 72 : sl, msg, ml, pre, empty_is_error, rec);
   else if (sch == 3)
-    st = ecdsa_prep_lane<Curve<3>>(key, key_len[i], sig, sig_len[i], msg, ml, pre, rec);
+    st = ecdsa_prep_lane<Curve<3>>(key, key_len[i], sig, sl > 72 ? 72 : sl, msg, ml, pre, empty_is_error, rec);
   else
     st = kStatusUnsupported;
   status[i] = st;
@@ -1195,40 +1159,24 @@ CDEV void ecdsa_affine_lane(uint32_t* __restrict__ rec) {
   }
 }
 
-__global__ void __launch_bounds__(256) ecdsa_affine_kernel(const unsigned int* __restrict__ perm,
-                                                          const uint8_t* __restrict__ scheme, uint64_t base,
-                                                          uint64_t m, const uint8_t* __restrict__ status,
-                                                          uint32_t* __restrict__ ws) {
-  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (li >= m) return;
-  const uint64_t slot = base + li;
-  const uint64_t i = perm ? perm[slot] : slot;
-  if (status[i] != kEcPending) return;
-  uint32_t* rec = ws + li * kEcWords;
-  if (scheme[i] == 2)
-    ecdsa_affine_lane<Curve<2>>(rec);
-  else
-    ecdsa_affine_lane<Curve<3>>(rec);
-}
-
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ecdsa_ladder_kernel(
     const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, uint64_t base, uint64_t m,
     const uint32_t* __restrict__ gtab_k1, const uint32_t* __restrict__ gtab_r1, uint32_t* __restrict__ ws,
-    uint8_t* __restrict__ status, int fuse_affine) {
+    uint8_t* __restrict__ status) {
   const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= m) return;
   const uint64_t slot = base + li;
   const uint64_t i = perm ? perm[slot] : slot;
   if (status[i] != kEcPending) return;
   uint32_t* rec = ws + li * kEcWords;
-  // fused table-to-affine pass: its uncoalesced record traffic overlaps the
-  // VALU-bound ladder of the SIMD's other waves instead of running as a
-  // memory-bound kernel of its own (same thread writes, then reads: ordered)
+  // table-to-affine pass fused into the ladder: as a kernel of its own its
+  // uncoalesced record traffic cost 14.8 ms per 2^24 lanes; here it overlaps the
+  // VALU-bound ladder of the SIMD's other waves (same thread writes, then reads)
   if (scheme[i] == 2) {
-    if (fuse_affine) ecdsa_affine_lane<Curve<2>>(rec);
+    ecdsa_affine_lane<Curve<2>>(rec);
     status[i] = ecdsa_ladder_lane<Curve<2>>(rec, gtab_k1);
   } else {
-    if (fuse_affine) ecdsa_affine_lane<Curve<3>>(rec);
+    ecdsa_affine_lane<Curve<3>>(rec);
     status[i] = ecdsa_ladder_lane<Curve<3>>(rec, gtab_r1);
   }
 }
@@ -1262,13 +1210,9 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
                                const uint64_t* msg_off, uint32_t msg_len, uint64_t n, const uint32_t* gk1,
                                const uint32_t* gr1, const uint8_t* pre_status, uint8_t* status,
                                unsigned long long* verdict, unsigned int* counters6, unsigned int* perm,
-                               uint32_t* ws, uint64_t ws_slots, hipStream_t s) {
+                               uint32_t* ws, uint64_t ws_slots, uint32_t flags, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (!ws || ws_slots < 64) return hipErrorInvalidValue;  // the split path is the only verify path
-  static const bool fuse_affine = [] {  // CORDAHIP_ECDSA_AFFINE=kernel: separate affine pass (A/B)
-    const char* v = getenv("CORDAHIP_ECDSA_AFFINE");
-    return !(v && std::string(v) == "kernel");
-  }();
   const dim3 grid((uint32_t)((n + 255) / 256));
   hipError_t e = hipMemsetAsync(counters6, 0, 2 * kPartClasses * sizeof(unsigned int), s);
   if (e != hipSuccess) return e;
@@ -1280,13 +1224,11 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
     const uint64_t m = n - base < ws_slots ? n - base : ws_slots;
     const dim3 g((uint32_t)((m + 255) / 256));
     hipLaunchKernelGGL(ecdsa_prep_kernel, g, dim3(256), 0, s, perm, scheme, keys, key_len, sigs, sig_len, msgs,
-                       msg_off, msg_len, base, m, pre_status, status, ws);
+                       msg_off, msg_len, base, m, pre_status, status, ws, (flags & 1u) ? 0u : 1u);
     const uint64_t nt = (m + kEcInvBatch - 1) / kEcInvBatch;
     hipLaunchKernelGGL(ecdsa_inv_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, s, base, m, counters6,
                        ws);
-    if (!fuse_affine) hipLaunchKernelGGL(ecdsa_affine_kernel, g, dim3(256), 0, s, perm, scheme, base, m, status, ws);
-    hipLaunchKernelGGL(ecdsa_ladder_kernel, g, dim3(256), 0, s, perm, scheme, base, m, gk1, gr1, ws, status,
-                       fuse_affine ? 1 : 0);
+    hipLaunchKernelGGL(ecdsa_ladder_kernel, g, dim3(256), 0, s, perm, scheme, base, m, gk1, gr1, ws, status);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

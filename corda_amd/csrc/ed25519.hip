@@ -1,4 +1,5 @@
-// Ed25519 (EDDSA_ED25519_SHA512) batch verification for gfx950 — kernel K1.
+// Ed25519 (EDDSA_ED25519_SHA512) batch verification for gfx950 — kernel K1,
+// first half (prep) plus the fixed-base table and the corpus signer.
 //
 // Replaces, per lane, the reference's
 //   Crypto.isValid(EDDSA_ED25519_SHA512, key, sig, clear)   Crypto.kt:534-541
@@ -6,32 +7,25 @@
 // with bit-exact verdicts (status byte per lane + 64-bit verdict word per
 // wave via ballot). Oracle: oracle/i2p_ed25519.py, oracle/c/ed25519.c.
 //
-// Per lane: decode A exactly as i2p (y not range checked), hash the
-// canonical re-encoding of A, h = SHA-512(R||Abyte||M) mod L, S_eff from an
-// exact emulation of slide()'s carry drop, then R' = [h](-A) + [S_eff]B with
-// a SIMD-uniform Straus ladder: signed 4-bit windows for -A (9-entry
-// per-lane table), signed 8-bit windows for B (129-entry affine table built
-// once per context), finally encode(R') == R byte-for-byte.
+// Two kernels per batch (layout shared in ed25519_ws.hpp):
+//   ed25519_prep_half_kernel (here): decode A exactly as i2p (y not range
+//     checked), decode R strictly, hash the canonical re-encoding of A,
+//     h = SHA-512(R||Abyte||M) mod L, S_eff from an exact emulation of
+//     slide()'s carry drop, the half-size scalars (c0, c1) and e = c1 S_eff,
+//     and the per-lane tables [0..8](-A), [0..8](-R) -> HBM workspace record;
+//   ed25519_ladder_half_kernel (ed25519_ladder.hip): [e]B + [c0](+-A) + [c1](-R) == O.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
 
-#include <string>
-
-#include "fe25519.hpp"
-#include "ge25519.hpp"
-#include "sc25519.hpp"
+#include "ed25519_ws.hpp"
 #include "sha2_device.hpp"
 #include "status.hpp"
 
 namespace cordahip {
 
 // ---------------------------------------------------------------------------
-// B table: entry k (0..128) = [k]B as affine niels (y+x, y-x, 2d*x*y); 32
-// u32 per entry (30 limbs + 2 pad) so a lane fetches it with 8 dwordx4.
-static constexpr int kBTableEntries = 129;
-static constexpr int kBEntryWords = 32;
-
+// B table (layout: ed25519_ws.hpp), built once per context by a kernel.
 CDEV void ge_base(ge_p3& b) {
   const uint32_t bx[10] = {0x325d51a, 0x18b5823, 0xf6592a, 0x104a92d, 0x1a4b31d,
                            0x1d6dc5c, 0x27118fe, 0x7fd814, 0x13cd6e5, 0x85a4db};
@@ -121,30 +115,6 @@ CDEV void load_niels(ge_niels& n, const uint32_t* __restrict__ tab, int idx) {
   }
 }
 
-// conditional negation of a niels / cached point: swap (y+x, y-x), negate t
-CDEV void niels_cneg(ge_niels& n, bool neg) {
-  fe nt;
-  fe_neg_loose(nt, n.xy2d);  // 2x: only ever the g-operand of fe_mul
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    const uint32_t a = n.ypx.v[i], b = n.ymx.v[i];
-    n.ypx.v[i] = neg ? b : a;
-    n.ymx.v[i] = neg ? a : b;
-    n.xy2d.v[i] = neg ? nt.v[i] : n.xy2d.v[i];
-  }
-}
-CDEV void cached_cneg(ge_cached& c, bool neg) {
-  fe nt;
-  fe_neg_loose(nt, c.T2d);
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    const uint32_t a = c.YpX.v[i], b = c.YmX.v[i];
-    c.YpX.v[i] = neg ? b : a;
-    c.YmX.v[i] = neg ? a : b;
-    c.T2d.v[i] = neg ? nt.v[i] : c.T2d.v[i];
-  }
-}
-
 // ---------------------------------------------------------------------------
 // SHA-512 over  seg0(32 B, registers) || seg1(32 B, registers, optional) || msg
 // (global, msg_len bytes). Fast path: everything fits one block with msg_len
@@ -205,91 +175,7 @@ CDEV void sha512_segments(uint32_t out_le[16], const uint32_t s0[8], const uint3
 }
 
 // ---------------------------------------------------------------------------
-// [h](-A) + [s]B  (h, s < L). Returns R' in extended coordinates (T unset).
-CDEV void straus_vartime_uniform(ge_p3& P, const ge_p3& Aneg, const uint32_t h[8], const uint32_t s[8],
-                                 const uint32_t* __restrict__ btab) {
-  // per-lane table of [k](-A), k = 0..8, cached form
-  ge_cached tab[9];
-  {
-    ge_cached& t0 = tab[0];
-    fe_set(t0.YpX, 1);
-    fe_set(t0.YmX, 1);
-    fe_set(t0.Z, 1);
-    fe_set(t0.T2d, 0);
-    ge_to_cached(tab[1], Aneg);
-    ge_p3 Q;
-    ge_dbl<true>(Q, Aneg);
-    ge_to_cached(tab[2], Q);
-#pragma unroll
-    for (int k = 3; k <= 8; k++) {
-      ge_add<true>(Q, Q, tab[1]);
-      ge_to_cached(tab[k], Q);
-    }
-  }
-  ge_identity(P);
-  for (int j = 63; j >= 0; j--) {
-    if (j != 63) {
-      ge_dbl<false>(P, P);
-      ge_dbl<false>(P, P);
-      ge_dbl<false>(P, P);
-      ge_dbl<true>(P, P);
-    }
-    const int da = booth_digit<4>(h, j);
-    ge_cached ca = tab[da < 0 ? -da : da];
-    cached_cneg(ca, da < 0);
-    if ((j & 1) == 0) {
-      ge_add<true>(P, P, ca);
-      const int db = booth_digit<8>(s, j >> 1);
-      ge_niels nb;
-      load_niels(nb, btab, db < 0 ? -db : db);
-      niels_cneg(nb, db < 0);
-      ge_madd<false>(P, P, nb);
-    } else {
-      ge_add<false>(P, P, ca);
-    }
-  }
-}
-
-// Status precedence follows the reference call chain: the key object is
-// decoded when the transaction is deserialised (Kryo.kt:389-392), i.e.
-// before Crypto.doVerify runs its require checks (Crypto.kt:474-476), which
-// run before the engine's length check and the math.
-CDEV uint8_t ed25519_verify_lane(const uint32_t key[8], const uint32_t sig[16], const uint8_t* __restrict__ msg,
-                                 uint32_t msg_len, const uint32_t* __restrict__ btab, uint8_t pre_status) {
-  ge_p3 A;
-  if (!ge_frombytes_i2p(A, key)) return kStatusBadKey;  // i2p GroupElement(Curve, byte[])
-  if (pre_status != kStatusOk) return pre_status;         // EMPTY / MALFORMED decided by the host
-  if (msg_len == 0) return kStatusEmpty;                  // Crypto.kt:476
-  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical re-encoding (Z == 1)
-  uint32_t abyte[8];
-  fe_tobytes(abyte, A.Y);
-  abyte[7] |= fe_isnegative(A.X) << 31;
-  uint32_t R[8], S[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    R[i] = sig[i];
-    S[i] = sig[8 + i];
-  }
-  uint32_t hd[16], h[8], se[8];
-  sha512_segments(hd, R, abyte, true, msg, msg_len);
-  sc_reduce512(h, hd);
-  const bool dropped = slide_drops_carry(S);
-  sc_effective_S(se, S, dropped);
-  ge_p3 Aneg = A;
-  fe_neg(Aneg.X, A.X);
-  fe_neg(Aneg.T, A.T);
-  ge_p3 P;
-  straus_vartime_uniform(P, Aneg, h, se, btab);
-  uint32_t enc[8];
-  ge_tobytes(enc, P);
-  uint32_t diff = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) diff |= enc[i] ^ R[i];
-  return diff == 0 ? kStatusOk : kStatusBadSig;
-}
-
-// ---------------------------------------------------------------------------
-// Half-size scalars (A/B alternative, CORDAHIP_ED25519_LADDER=half). With R decoded strictly,
+// Half-size scalars. With R decoded strictly,
 //   encode([S]B - [h]A) == R_bytes  <=>  P := [S]B - [h]A - R == O.
 // For any (c0, c1) with c0 == c1*h (mod 8L) and c1 odd, c1 != 0 (mod L):
 //   [c1]P == [c1*S mod L]B - [c0]A - [c1]R,   and   [c1]P == O <=> P == O
@@ -324,12 +210,6 @@ CDEV void mp8_neg(uint32_t a[8]) {
     a[i] = (uint32_t)c;
     c >>= 32;
   }
-}
-CDEV int mp8_bitlen(const uint32_t a[8]) {
-  int n = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) n = a[i] ? 32 * i + 32 - __builtin_clz(a[i]) : n;
-  return n;
 }
 CDEV void mp8_copy(uint32_t d[8], const uint32_t s[8]) {
 #pragma unroll
@@ -486,227 +366,8 @@ CDEV bool ge_strict_ok(const ge_p3& R, const uint32_t w[8]) {
   if (all_ones && w[0] >= 0xffffffedu) return false;  // y >= p
   return !((w[7] >> 31) && fe_iszero(R.X));
 }
-CDEV bool ge_frombytes_strict(ge_p3& R, const uint32_t w[8]) {
-  bool all_ones = (w[7] & 0x7fffffffu) == 0x7fffffffu;
-#pragma unroll
-  for (int i = 1; i < 7; i++) all_ones = all_ones && (w[i] == 0xffffffffu);
-  if (all_ones && w[0] >= 0xffffffedu) return false;  // y >= p
-  if (!ge_frombytes_i2p(R, w)) return false;
-  if ((w[7] >> 31) && fe_iszero(R.X)) return false;
-  return true;
-}
-
-CDEV void cached_table9(ge_cached tab[9], const ge_p3& base) {
-  fe_set(tab[0].YpX, 1);
-  fe_set(tab[0].YmX, 1);
-  fe_set(tab[0].Z, 1);
-  fe_set(tab[0].T2d, 0);
-  ge_to_cached(tab[1], base);
-  ge_p3 Q;
-  ge_dbl<true>(Q, base);
-  ge_to_cached(tab[2], Q);
-  for (int k = 3; k <= 8; k++) {
-    ge_add<true>(Q, Q, tab[1]);
-    ge_to_cached(tab[k], Q);
-  }
-}
 
 CDEV void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8], const uint32_t c[8]);
-
-// [ka]Abase + [kr]Rbase + [e]B, ka, kr < 2^(4W-1), e < L; W wave-uniform
-CDEV void straus_half(ge_p3& P, const ge_p3& Abase, const ge_p3& Rbase, const uint32_t ka[8], const uint32_t kr[8],
-                      const uint32_t e[8], int W, const uint32_t* __restrict__ btab) {
-  ge_cached ta[9], tr[9];
-  cached_table9(ta, Abase);
-  cached_table9(tr, Rbase);
-  const uint32_t* btab128 = btab + kBTableEntries * kBEntryWords;
-  ge_identity(P);
-  for (int j = W - 1; j >= 0; j--) {
-    if (j != W - 1) {
-      ge_dbl<false>(P, P);
-      ge_dbl<false>(P, P);
-      ge_dbl<false>(P, P);
-      ge_dbl<true>(P, P);
-    }
-    const int da = booth_digit<4>(ka, j);
-    ge_cached ca = ta[da < 0 ? -da : da];
-    cached_cneg(ca, da < 0);
-    ge_add<true>(P, P, ca);
-    const int dr = booth_digit<4>(kr, j);
-    ge_cached cr = tr[dr < 0 ? -dr : dr];
-    cached_cneg(cr, dr < 0);
-    if ((j & 1) == 0 && j < 32) {
-      ge_add<true>(P, P, cr);
-      const int d0 = booth_digit<8>(e, j >> 1), d1 = booth_digit<8>(e, (j >> 1) + 16);
-      ge_niels nb;
-      load_niels(nb, btab, d0 < 0 ? -d0 : d0);
-      niels_cneg(nb, d0 < 0);
-      ge_madd<true>(P, P, nb);
-      load_niels(nb, btab128, d1 < 0 ? -d1 : d1);
-      niels_cneg(nb, d1 < 0);
-      ge_madd<false>(P, P, nb);
-    } else {
-      ge_add<false>(P, P, cr);
-    }
-  }
-}
-
-CDEV int wave_max(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-  return v;
-}
-
-CDEV uint8_t ed25519_verify_lane_half(const uint32_t key[8], const uint32_t sig[16], const uint8_t* __restrict__ msg,
-                                      uint32_t msg_len, const uint32_t* __restrict__ btab, uint8_t pre_status,
-                                      bool active) {
-  // every lane of the wave reaches the wave-uniform ladder; inactive or
-  // already-decided lanes run it on dummy scalars and keep their status
-  uint8_t st = kStatusOk;
-  ge_p3 A, R;
-  if (!active) st = kStatusBadSig;
-  else if (!ge_frombytes_i2p(A, key)) st = kStatusBadKey;
-  else if (pre_status != kStatusOk) st = pre_status;
-  else if (msg_len == 0) st = kStatusEmpty;
-  uint32_t Rw[8], S[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    Rw[i] = sig[i];
-    S[i] = sig[8 + i];
-  }
-  if (st == kStatusOk && !ge_frombytes_strict(R, Rw)) st = kStatusBadSig;
-  uint32_t ka[8], kr[8], e[8];
-  bool c0neg = false;
-  if (st == kStatusOk) {
-    uint32_t abyte[8];
-    fe_tobytes(abyte, A.Y);
-    abyte[7] |= fe_isnegative(A.X) << 31;
-    uint32_t hd[16], h[8], se[8], zero[8];
-    sha512_segments(hd, Rw, abyte, true, msg, msg_len);
-    sc_reduce512(h, hd);
-    const bool dropped = slide_drops_carry(S);
-    sc_effective_S(se, S, dropped);
-    half_scalars(ka, c0neg, kr, h);
-#pragma unroll
-    for (int i = 0; i < 8; i++) zero[i] = 0;
-    sc_muladd(e, kr, se, zero);  // e = c1 S_eff mod L
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; i++) ka[i] = kr[i] = e[i] = 0;
-    ge_identity(A);
-    ge_identity(R);
-  }
-  const int bits = max(mp8_bitlen(ka), mp8_bitlen(kr));
-  const int W = wave_max((bits + 1 + 3) / 4);
-  // [e]B + [c0](-A) + [c1](-R): -A when c0 > 0, A when c0 < 0; always -R
-  ge_p3 Ab = A, Rb = R;
-  if (!c0neg) {
-    fe_neg(Ab.X, A.X);
-    fe_neg(Ab.T, A.T);
-  }
-  fe_neg(Rb.X, R.X);
-  fe_neg(Rb.T, R.T);
-  ge_p3 P;
-  straus_half(P, Ab, Rb, ka, kr, e, W > 0 ? W : 1, btab);
-  if (st != kStatusOk) return st;
-  fe d;
-  fe_sub(d, P.Y, P.Z);
-  return (fe_iszero(P.X) && fe_iszero(d)) ? kStatusOk : kStatusBadSig;
-}
-
-// keys n*32 B, sigs n*64 B, msgs n*msg_len B (16-B aligned rows when msg_len == 32)
-template <bool HALF>
-__global__ void __launch_bounds__(256) ed25519_verify_kernel(
-    const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
-    uint32_t msg_len, uint64_t n, const uint32_t* __restrict__ btab, const uint8_t* __restrict__ pre_status,
-    uint8_t* __restrict__ status, unsigned long long* __restrict__ verdict) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint8_t st = kStatusBadSig;
-  const bool active = i < n;
-  const uint64_t ii = active ? i : 0;  // inactive lanes read lane 0's row (n > 0), discard it
-  const uint4* k4 = reinterpret_cast<const uint4*>(keys + ii * 32);
-  const uint4* s4 = reinterpret_cast<const uint4*>(sigs + ii * 64);
-  const uint4 ka = k4[0], kb = k4[1];
-  const uint32_t key[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
-  uint32_t sig[16];
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint4 v = s4[q];
-    sig[4 * q] = v.x;
-    sig[4 * q + 1] = v.y;
-    sig[4 * q + 2] = v.z;
-    sig[4 * q + 3] = v.w;
-  }
-  const uint8_t pre = (pre_status && active) ? pre_status[ii] : kStatusOk;
-  if (HALF) {
-    st = ed25519_verify_lane_half(key, sig, msgs + ii * (uint64_t)msg_len, msg_len, btab, pre, active);
-  } else if (active) {
-    st = ed25519_verify_lane(key, sig, msgs + ii * (uint64_t)msg_len, msg_len, btab, pre);
-  }
-  if (active) status[i] = st;
-  const unsigned long long ok = __ballot(i < n && st == kStatusOk);
-  if ((threadIdx.x & 63) == 0 && i < n && verdict) verdict[i >> 6] = ok;
-}
-
-// ---------------------------------------------------------------------------
-// Split verification (the default): two kernels per chunk of lanes.
-//
-//   prep   : key decode, canonical Abyte, SHA-512, h mod L, S_eff, and the
-//            per-lane table [0..8](-A) in cached form -> per-lane workspace
-//            record in HBM (AoS, 1520 B), early statuses -> status[]
-//   ladder : the 64-window Straus ladder, B table staged in LDS, the next
-//            window's -A entry prefetched from the workspace while the four
-//            doublings run; encode(R') == R; status + verdict ballot.
-//
-// Splitting gives each phase its own register allocation: the fused kernel
-// is pinned at 512 registers (1 wave/SIMD) by SHA-512 / decompression and
-// keeps its dynamically indexed table in scratch; the ladder alone has
-// neither. The workspace traffic (1.5 KB written, 64 x 160 B gathered per
-// lane) is cache-friendly: each lane reads whole 160-B entries.
-static constexpr int kWsTabWords = 9 * 40;                  // [0..8](-A), cached (YpX, YmX, Z, T2d)
-static constexpr int kWsH = kWsTabWords;                     // h (8 words)
-static constexpr int kWsS = kWsTabWords + 8;                 // S_eff (8 words)
-static constexpr int kWsLaneWords = kWsTabWords + 16 + 4;    // 380 words = 1520 B (16-B aligned)
-static constexpr int kLdsBStride = 36;                       // words per B entry in LDS (bank spread)
-static constexpr uint8_t kStatusPending = 0xff;
-
-CDEV void store_cached(uint32_t* __restrict__ o, const ge_cached& c) {
-  uint4* o4 = reinterpret_cast<uint4*>(o);
-  uint32_t w[40];
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    w[i] = c.YpX.v[i];
-    w[10 + i] = c.YmX.v[i];
-    w[20 + i] = c.Z.v[i];
-    w[30 + i] = c.T2d.v[i];
-  }
-#pragma unroll
-  for (int q = 0; q < 10; q++) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-}
-
-CDEV void load_cached(ge_cached& c, const uint32_t* __restrict__ p) {
-  const uint4* p4 = reinterpret_cast<const uint4*>(p);
-  uint32_t w[40];
-#pragma unroll
-  for (int q = 0; q < 10; q++) {
-    const uint4 v = p4[q];
-    w[4 * q] = v.x;
-    w[4 * q + 1] = v.y;
-    w[4 * q + 2] = v.z;
-    w[4 * q + 3] = v.w;
-  }
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    c.YpX.v[i] = w[i];
-    c.YmX.v[i] = w[10 + i];
-    c.Z.v[i] = w[20 + i];
-    c.T2d.v[i] = w[30 + i];
-  }
-}
-
-// stops the machine scheduler from interleaving the phases on either side
-// (independent phases interleaved = both phases' registers live at once)
-#define PHASE_BARRIER() __builtin_amdgcn_sched_barrier(0)
 
 CDEV void store_table9(uint32_t* __restrict__ rec, const ge_p3& base) {
   ge_cached c;
@@ -729,156 +390,11 @@ CDEV void store_table9(uint32_t* __restrict__ rec, const ge_p3& base) {
   }
 }
 
-CDEV void store8(uint32_t* __restrict__ o, const uint32_t v[8]) {
-  uint4* o4 = reinterpret_cast<uint4*>(o);
-  o4[0] = make_uint4(v[0], v[1], v[2], v[3]);
-  o4[1] = make_uint4(v[4], v[5], v[6], v[7]);
-}
-CDEV void load8(uint32_t v[8], const uint32_t* __restrict__ p) {
-  const uint4* p4 = reinterpret_cast<const uint4*>(p);
-  const uint4 a = p4[0], b = p4[1];
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-
-// lanes [base, base + m) of the batch; ws holds m records. Phases (see
-// PHASE_BARRIER): decode A -> table [k](-A) | SHA-512, h, S_eff.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_prep_kernel(
-    const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
-    uint32_t msg_len, uint64_t base, uint64_t m, const uint8_t* __restrict__ pre_status,
-    uint8_t* __restrict__ status, uint32_t* __restrict__ ws) {
-  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (li >= m) return;
-  const uint64_t i = base + li;
-  uint32_t* rec = ws + li * kWsLaneWords;
-  uint8_t st = kStatusPending;
-  uint32_t abyte[8];
-  {
-    uint32_t key[8];
-    load8(key, reinterpret_cast<const uint32_t*>(keys + i * 32));
-    ge_p3 A;
-    if (!ge_frombytes_i2p(A, key)) st = kStatusBadKey;  // i2p GroupElement(Curve, byte[]), before doVerify (Kryo.kt:389-392)
-    else if (pre_status && pre_status[i] != kStatusOk) st = pre_status[i];  // EMPTY / MALFORMED decided by the host
-    else if (msg_len == 0) st = kStatusEmpty;  // Crypto.kt:476
-    fe_tobytes(abyte, A.Y);  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
-    abyte[7] |= fe_isnegative(A.X) << 31;
-    if (st != kStatusPending) ge_identity(A);
-    fe_neg(A.X, A.X);
-    fe_neg(A.T, A.T);
-    store_table9(rec, A);  // [k](-A), k = 0..8
-  }
-  PHASE_BARRIER();
-  uint32_t h[8], se[8];
-  if (st == kStatusPending) {
-    uint32_t R[8], S[8], hd[16];
-    load8(R, reinterpret_cast<const uint32_t*>(sigs + i * 64));
-    load8(S, reinterpret_cast<const uint32_t*>(sigs + i * 64 + 32));
-    sha512_segments(hd, R, abyte, true, msgs + i * (uint64_t)msg_len, msg_len);
-    sc_reduce512(h, hd);
-    sc_effective_S(se, S, slide_drops_carry(S));
-  } else {
-#pragma unroll
-    for (int q = 0; q < 8; q++) h[q] = se[q] = 0;
-  }
-  status[i] = st;
-  store8(rec + kWsH, h);
-  store8(rec + kWsS, se);
-}
-
-CDEV void lds_niels(ge_niels& n, const uint32_t* lds, int idx) {
-  const uint4* e = reinterpret_cast<const uint4*>(lds + idx * kLdsBStride);
-  uint32_t w[32];
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    const uint4 v = e[q];
-    w[4 * q] = v.x;
-    w[4 * q + 1] = v.y;
-    w[4 * q + 2] = v.z;
-    w[4 * q + 3] = v.w;
-  }
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    n.ypx.v[i] = w[i];
-    n.ymx.v[i] = w[10 + i];
-    n.xy2d.v[i] = w[20 + i];
-  }
-}
-
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_ladder_kernel(
-    const uint8_t* __restrict__ sigs, uint64_t base, uint64_t m, const uint32_t* __restrict__ btab,
-    const uint32_t* __restrict__ ws, uint8_t* __restrict__ status, unsigned long long* __restrict__ verdict) {
-  __shared__ __attribute__((aligned(16))) uint32_t bl[kBTableEntries * kLdsBStride];
-  for (int t = threadIdx.x; t < kBTableEntries * 8; t += blockDim.x) {
-    const int e = t >> 3, q = t & 7;
-    reinterpret_cast<uint4*>(bl + e * kLdsBStride)[q] = reinterpret_cast<const uint4*>(btab + e * kBEntryWords)[q];
-  }
-  __syncthreads();
-  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = li < m;
-  const uint64_t lc = active ? li : m - 1;  // inactive lanes replay the last record, discard it
-  const uint32_t* rec = ws + lc * kWsLaneWords;
-  uint32_t h[8], s[8];
-  {
-    const uint4* p4 = reinterpret_cast<const uint4*>(rec + kWsH);
-    const uint4 a = p4[0], b = p4[1], c = p4[2], d = p4[3];
-    h[0] = a.x; h[1] = a.y; h[2] = a.z; h[3] = a.w; h[4] = b.x; h[5] = b.y; h[6] = b.z; h[7] = b.w;
-    s[0] = c.x; s[1] = c.y; s[2] = c.z; s[3] = c.w; s[4] = d.x; s[5] = d.y; s[6] = d.z; s[7] = d.w;
-  }
-  ge_p3 P;
-  ge_identity(P);
-  for (int j = 63; j >= 0; j--) {
-    // issue this window's -A entry load first: the four doublings hide it
-    const int da = booth_digit<4>(h, j);
-    ge_cached cur;
-    load_cached(cur, rec + 40 * (da < 0 ? -da : da));
-    if (j != 63) {
-      ge_dbl<false>(P, P);
-      ge_dbl<false>(P, P);
-      ge_dbl<false>(P, P);
-      ge_dbl<true>(P, P);
-    }
-    cached_cneg(cur, da < 0);
-    if ((j & 1) == 0) {
-      ge_add<true>(P, P, cur);
-      const int db = booth_digit<8>(s, j >> 1);
-      ge_niels nb;
-      lds_niels(nb, bl, db < 0 ? -db : db);
-      niels_cneg(nb, db < 0);
-      ge_madd<false>(P, P, nb);
-    } else {
-      ge_add<false>(P, P, cur);
-    }
-  }
-  uint32_t enc[8];
-  ge_tobytes(enc, P);
-  const uint4* s4 = reinterpret_cast<const uint4*>(sigs + (base + lc) * 64);
-  const uint4 r0 = s4[0], r1 = s4[1];
-  const uint32_t diff = (enc[0] ^ r0.x) | (enc[1] ^ r0.y) | (enc[2] ^ r0.z) | (enc[3] ^ r0.w) | (enc[4] ^ r1.x) |
-                        (enc[5] ^ r1.y) | (enc[6] ^ r1.z) | (enc[7] ^ r1.w);
-  const uint64_t i = base + li;
-  uint8_t st = kStatusBadSig;
-  if (active) {
-    st = status[i];
-    if (st == kStatusPending) {
-      st = diff == 0 ? kStatusOk : kStatusBadSig;
-      status[i] = st;
-    }
-  }
-  const unsigned long long ok = __ballot(active && st == kStatusOk);
-  // base is a multiple of 64 (chunk sizes are), so lane 0 of a wave owns a whole verdict word
-  if ((threadIdx.x & 63) == 0 && active && verdict) verdict[i >> 6] = ok;
-}
-
 // ---------------------------------------------------------------------------
-// Split half-size-scalar verification: same prep/ladder split, ladder over
-// [e]B + [c0](+-A) + [c1](-R) with ~128-bit c0, c1 (see half_scalars): 128
-// doublings instead of 252 and no final inversion (P == O is X == 0, Y == Z).
-static constexpr int kWhTabA = 0;                            // [0..8](-A)
-static constexpr int kWhTabR = 9 * 40;                       // [0..8](-R)
-static constexpr int kWhKa = 18 * 40;                        // |c0|, c1, e (8 words each)
-static constexpr int kWhKr = kWhKa + 8;
-static constexpr int kWhE = kWhKa + 16;
-static constexpr int kWhFlags = kWhKa + 24;                  // bit 0: c0 < 0
-static constexpr int kWhLaneWords = kWhKa + 28;              // 748 words = 2992 B (16-B multiple)
+// Prep of the half-size-scalar verification: the ladder (ed25519_ladder.hip)
+// decides [e]B + [c0](+-A) + [c1](-R) == O with ~128-bit c0, c1 (half_scalars):
+// ~132 doublings instead of 252 and no final inversion (P == O is X == 0, Y == Z).
+// Record layout: ed25519_ws.hpp (kWh*).
 
 // Phases, each finished (and its table written to the workspace) before the
 // next starts: decode A -> table [k](-A) | strict decode R -> table [k](-R) |
@@ -887,7 +403,7 @@ static constexpr int kWhLaneWords = kWhKa + 28;              // 748 words = 2992
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_prep_half_kernel(
     const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
     uint32_t msg_len, uint64_t base, uint64_t m, const uint8_t* __restrict__ pre_status,
-    uint8_t* __restrict__ status, uint32_t* __restrict__ ws) {
+    uint8_t* __restrict__ status, uint32_t* __restrict__ ws, uint32_t empty_is_error) {
   const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= m) return;
   const uint64_t i = base + li;
@@ -908,7 +424,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
     if (pass == 0) {
       if (!ok) st = kStatusBadKey;  // key decode precedes doVerify (Kryo.kt:389-392)
       else if (pre_status && pre_status[i] != kStatusOk) st = pre_status[i];
-      else if (msg_len == 0) st = kStatusEmpty;  // Crypto.kt:476
+      else if (msg_len == 0 && empty_is_error) st = kStatusEmpty;  // doVerify: Crypto.kt:476 (isValid hashes it)
       fe_tobytes(abyte, P.Y);  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
       abyte[7] |= fe_isnegative(P.X) << 31;
     } else if (st == kStatusPending && !(ok && ge_strict_ok(P, w))) {
@@ -941,73 +457,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
   store8(rec + kWhKr, kr);
   store8(rec + kWhE, e);
   reinterpret_cast<uint4*>(rec + kWhFlags)[0] = make_uint4(c0neg ? 1u : 0u, 0u, 0u, 0u);
-}
-
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_ladder_half_kernel(
-    uint64_t base, uint64_t m, const uint32_t* __restrict__ btab, const uint32_t* __restrict__ ws,
-    uint8_t* __restrict__ status, unsigned long long* __restrict__ verdict) {
-  __shared__ __attribute__((aligned(16))) uint32_t bl[2 * kBTableEntries * kLdsBStride];
-  for (int t = threadIdx.x; t < 2 * kBTableEntries * 8; t += blockDim.x) {
-    const int e = t >> 3, q = t & 7;
-    reinterpret_cast<uint4*>(bl + e * kLdsBStride)[q] = reinterpret_cast<const uint4*>(btab + e * kBEntryWords)[q];
-  }
-  __syncthreads();
-  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = li < m;
-  const uint64_t lc = active ? li : m - 1;  // inactive lanes replay the last record, discard it
-  const uint32_t* rec = ws + lc * kWhLaneWords;
-  uint32_t ka[8], kr[8], e[8];
-  load8(ka, rec + kWhKa);
-  load8(kr, rec + kWhKr);
-  load8(e, rec + kWhE);
-  const bool c0neg = rec[kWhFlags] & 1u;  // [c0](-A) with c0 < 0 is [|c0|]A: flip the digit signs
-  const int bits = max(mp8_bitlen(ka), mp8_bitlen(kr));
-  const int W = max(wave_max((bits + 1 + 3) / 4), 1);
-  const uint32_t* bl128 = bl + kBTableEntries * kLdsBStride;
-  ge_p3 P;
-  ge_identity(P);
-  for (int j = W - 1; j >= 0; j--) {
-    const int da = booth_digit<4>(ka, j), dr = booth_digit<4>(kr, j);
-    ge_cached ca, cr;  // issued before the doublings, consumed after them
-    load_cached(ca, rec + kWhTabA + 40 * (da < 0 ? -da : da));
-    load_cached(cr, rec + kWhTabR + 40 * (dr < 0 ? -dr : dr));
-    if (j != W - 1) {
-      ge_dbl<false>(P, P);
-      ge_dbl<false>(P, P);
-      ge_dbl<false>(P, P);
-      ge_dbl<true>(P, P);
-    }
-    cached_cneg(ca, (da < 0) != c0neg);
-    ge_add<true>(P, P, ca);
-    cached_cneg(cr, dr < 0);
-    if ((j & 1) == 0 && j < 32) {
-      ge_add<true>(P, P, cr);
-      const int d0 = booth_digit<8>(e, j >> 1), d1 = booth_digit<8>(e, (j >> 1) + 16);
-      ge_niels nb;
-      lds_niels(nb, bl, d0 < 0 ? -d0 : d0);
-      niels_cneg(nb, d0 < 0);
-      ge_madd<true>(P, P, nb);
-      lds_niels(nb, bl128, d1 < 0 ? -d1 : d1);
-      niels_cneg(nb, d1 < 0);
-      ge_madd<false>(P, P, nb);
-    } else {
-      ge_add<false>(P, P, cr);
-    }
-  }
-  fe d;
-  fe_sub(d, P.Y, P.Z);
-  const bool zero = fe_iszero(P.X) && fe_iszero(d);
-  const uint64_t i = base + li;
-  uint8_t st = kStatusBadSig;
-  if (active) {
-    st = status[i];
-    if (st == kStatusPending) {
-      st = zero ? kStatusOk : kStatusBadSig;
-      status[i] = st;
-    }
-  }
-  const unsigned long long ok = __ballot(active && st == kStatusOk);
-  if ((threadIdx.x & 63) == 0 && active && verdict) verdict[i >> 6] = ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -1124,65 +573,28 @@ hipError_t launch_ed25519_btable(uint32_t* tab, hipStream_t s) {
 }
 size_t ed25519_btable_bytes() { return 2 * (size_t)kBTableEntries * kBEntryWords * sizeof(uint32_t); }
 
-// CORDAHIP_ED25519_LADDER selects the verification kernels (all bit-exact):
-//   split-half (default): prep + ladder kernels over a per-lane HBM workspace,
-//                   half-size-scalar ladder (~132 doublings)
-//   split          : the same split with the full 252-doubling ladder
-//   fused          : one kernel, full 252-doubling ladder (round-1 baseline)
-//   half           : one kernel, half-size-scalar ladder
-// profiles/r01_bench_c2_ab.json holds the A/B measurements.
-enum class Ladder { kSplit, kSplitHalf, kFused, kHalf };
-static Ladder ladder_mode() {
-  static const Ladder m = [] {
-    const char* v = getenv("CORDAHIP_ED25519_LADDER");
-    if (!v) return Ladder::kSplitHalf;
-    const std::string s(v);
-    if (s == "split") return Ladder::kSplit;
-    if (s == "half") return Ladder::kHalf;
-    if (s == "fused") return Ladder::kFused;
-    return Ladder::kSplitHalf;
-  }();
-  return m;
-}
-
-// workspace record size (the larger of the two split layouts)
 size_t ed25519_ws_lane_bytes() { return kWhLaneWords * sizeof(uint32_t); }
 
-// ws: ws_lanes * ed25519_ws_lane_bytes() of device memory (ws_lanes a multiple
-// of 64), used only by the split kernels; the caller serialises its users.
+// Split verification, one prep/ladder launch pair per ws_lanes chunk (ws:
+// ws_lanes * ed25519_ws_lane_bytes() of device memory, ws_lanes a multiple of
+// 64; the caller orders the workspace's users). A missing workspace is an
+// error: this is the only verification path.
 hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
                                  uint64_t n, const uint32_t* btab, const uint8_t* pre_status, uint8_t* status,
-                                 unsigned long long* verdict, uint32_t* ws, uint64_t ws_lanes, hipStream_t s) {
+                                 unsigned long long* verdict, uint32_t* ws, uint64_t ws_lanes, uint32_t flags,
+                                 hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const Ladder mode = (ws && ws_lanes >= 64) ? ladder_mode() : Ladder::kFused;
-  if (mode == Ladder::kSplit || mode == Ladder::kSplitHalf) {
-    for (uint64_t base = 0; base < n; base += ws_lanes) {
-      const uint64_t m = n - base < ws_lanes ? n - base : ws_lanes;
-      const uint32_t blocks = (uint32_t)((m + 255) / 256);
-      if (mode == Ladder::kSplit) {
-        hipLaunchKernelGGL(ed25519_prep_kernel, dim3(blocks), dim3(256), 0, s, keys, sigs, msgs, msg_len, base, m,
-                           pre_status, status, ws);
-        hipLaunchKernelGGL(ed25519_ladder_kernel, dim3(blocks), dim3(256), 0, s, sigs, base, m, btab, ws, status,
-                           verdict);
-      } else {
-        hipLaunchKernelGGL(ed25519_prep_half_kernel, dim3(blocks), dim3(256), 0, s, keys, sigs, msgs, msg_len, base,
-                           m, pre_status, status, ws);
-        hipLaunchKernelGGL(ed25519_ladder_half_kernel, dim3(blocks), dim3(256), 0, s, base, m, btab, ws, status,
-                           verdict);
-      }
-      const hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+  if (!ws || ws_lanes < 64 || ws_lanes % 64) return hipErrorInvalidValue;
+  for (uint64_t base = 0; base < n; base += ws_lanes) {
+    const uint64_t m = n - base < ws_lanes ? n - base : ws_lanes;
+    const uint32_t blocks = (uint32_t)((m + 255) / 256);
+    hipLaunchKernelGGL(ed25519_prep_half_kernel, dim3(blocks), dim3(256), 0, s, keys, sigs, msgs, msg_len, base, m,
+                       pre_status, status, ws, (flags & 1u) ? 0u : 1u);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = launch_ed25519_ladder(base, m, btab, ws, status, verdict, s);
+    if (e != hipSuccess) return e;
   }
-  const uint64_t blocks = (n + 255) / 256;
-  if (mode == Ladder::kHalf)
-    hipLaunchKernelGGL(ed25519_verify_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0, s, keys, sigs, msgs,
-                       msg_len, n, btab, pre_status, status, verdict);
-  else
-    hipLaunchKernelGGL(ed25519_verify_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, s, keys, sigs, msgs,
-                       msg_len, n, btab, pre_status, status, verdict);
-  return hipGetLastError();
+  return hipSuccess;
 }
 
 hipError_t launch_ed25519_sign(const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len, uint64_t n,

@@ -1,0 +1,116 @@
+// Ed25519 verification ladder for gfx950 — second kernel of K1.
+//
+// Per lane (record written by ed25519_prep_half_kernel, ed25519.hip): decide
+//   [e]B + [c0](+-A) + [c1](-R) == O
+// with |c0|, c1 ~ 2^128 (c0 == c1 h mod 8L, c1 odd) and e = c1 S_eff mod L: the
+// i2p 0.2.0 cofactorless check encode([S]B - [h]A) == R rewritten over
+// half-size scalars (T. Pornin, ePrint 2020/454; the equivalence argument is in
+// ed25519.hip above half_scalars). 4-bit Booth windows over the per-lane
+// [0..8](-A), [0..8](-R) tables (gathered from the workspace one window ahead,
+// so the four doublings hide the load), 8-bit Booth windows over B and
+// B' = [2^128]B from LDS. Digit positions are the same in every lane, so the
+// ladder never diverges; P == O is X == 0 and Y == Z (no inversion).
+// Verdict word per wave by ballot.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ed25519_ws.hpp"
+#include "status.hpp"
+
+namespace cordahip {
+
+CDEV void lds_niels(ge_niels& n, const uint32_t* lds, int idx) {
+  const uint4* e = reinterpret_cast<const uint4*>(lds + idx * kLdsBStride);
+  uint32_t w[32];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint4 v = e[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    n.ypx.v[i] = w[i];
+    n.ymx.v[i] = w[10 + i];
+    n.xy2d.v[i] = w[20 + i];
+  }
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_ladder_half_kernel(
+    uint64_t base, uint64_t m, const uint32_t* __restrict__ btab, const uint32_t* __restrict__ ws,
+    uint8_t* __restrict__ status, unsigned long long* __restrict__ verdict) {
+  __shared__ __attribute__((aligned(16))) uint32_t bl[2 * kBTableEntries * kLdsBStride];
+  for (int t = threadIdx.x; t < 2 * kBTableEntries * 8; t += blockDim.x) {
+    const int e = t >> 3, q = t & 7;
+    reinterpret_cast<uint4*>(bl + e * kLdsBStride)[q] = reinterpret_cast<const uint4*>(btab + e * kBEntryWords)[q];
+  }
+  __syncthreads();
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = li < m;
+  const uint64_t lc = active ? li : m - 1;  // inactive lanes replay the last record, discard it
+  const uint32_t* rec = ws + lc * kWhLaneWords;
+  uint32_t ka[8], kr[8], e[8];
+  load8(ka, rec + kWhKa);
+  load8(kr, rec + kWhKr);
+  load8(e, rec + kWhE);
+  const bool c0neg = rec[kWhFlags] & 1u;  // [c0](-A) with c0 < 0 is [|c0|]A: flip the digit signs
+  const int bits = max(mp8_bitlen(ka), mp8_bitlen(kr));
+  const int W = max(wave_max((bits + 1 + 3) / 4), 1);
+  const uint32_t* bl128 = bl + kBTableEntries * kLdsBStride;
+  ge_p3 P;
+  ge_identity(P);
+  for (int j = W - 1; j >= 0; j--) {
+    const int da = booth_digit<4>(ka, j), dr = booth_digit<4>(kr, j);
+    ge_cached ca, cr;  // issued before the doublings, consumed after them
+    load_cached(ca, rec + kWhTabA + 40 * (da < 0 ? -da : da));
+    load_cached(cr, rec + kWhTabR + 40 * (dr < 0 ? -dr : dr));
+    if (j != W - 1) {
+      ge_dbl<false>(P, P);
+      ge_dbl<false>(P, P);
+      ge_dbl<false>(P, P);
+      ge_dbl<true>(P, P);
+    }
+    cached_cneg(ca, (da < 0) != c0neg);
+    ge_add<true>(P, P, ca);
+    cached_cneg(cr, dr < 0);
+    if ((j & 1) == 0 && j < 32) {
+      ge_add<true>(P, P, cr);
+      const int d0 = booth_digit<8>(e, j >> 1), d1 = booth_digit<8>(e, (j >> 1) + 16);
+      ge_niels nb;
+      lds_niels(nb, bl, d0 < 0 ? -d0 : d0);
+      niels_cneg(nb, d0 < 0);
+      ge_madd<true>(P, P, nb);
+      lds_niels(nb, bl128, d1 < 0 ? -d1 : d1);
+      niels_cneg(nb, d1 < 0);
+      ge_madd<false>(P, P, nb);
+    } else {
+      ge_add<false>(P, P, cr);
+    }
+  }
+  fe d;
+  fe_sub(d, P.Y, P.Z);
+  const bool zero = fe_iszero(P.X) && fe_iszero(d);
+  const uint64_t i = base + li;
+  uint8_t st = kStatusBadSig;
+  if (active) {
+    st = status[i];
+    if (st == kStatusPending) {
+      st = zero ? kStatusOk : kStatusBadSig;
+      status[i] = st;
+    }
+  }
+  const unsigned long long ok = __ballot(active && st == kStatusOk);
+  // base is a multiple of 64 (workspace chunks are), so lane 0 of a wave owns a whole verdict word
+  if ((threadIdx.x & 63) == 0 && active && verdict) verdict[i >> 6] = ok;
+}
+
+hipError_t launch_ed25519_ladder(uint64_t base, uint64_t m, const uint32_t* btab, const uint32_t* ws, uint8_t* status,
+                                 unsigned long long* verdict, hipStream_t s) {
+  const uint32_t blocks = (uint32_t)((m + 255) / 256);
+  hipLaunchKernelGGL(ed25519_ladder_half_kernel, dim3(blocks), dim3(256), 0, s, base, m, btab, ws, status, verdict);
+  return hipGetLastError();
+}
+
+}  // namespace cordahip

@@ -1,0 +1,127 @@
+// Shared layout of the Ed25519 split verification (kernel K1): the fixed-base
+// table, the per-lane HBM workspace record prep writes and the ladder reads,
+// and the point helpers both translation units use.
+//
+//   ed25519.hip         prep: i2p decode of A, strict decode of R, SHA-512,
+//                       h mod L, S_eff, lattice reduction -> workspace record
+//   ed25519_ladder.hip  ladder: [e]B + [c0](+-A) + [c1](-R) == O, verdict ballot
+//
+// The two live in separate translation units so each gets the field-multiply
+// instruction shape that suits it (fe25519.hpp FE_ASM_MAC): prep is dominated
+// by the serial square chains of two decompressions (latency-bound: column
+// sums re-associated for ILP), the ladder by independent products of the
+// group formulas (throughput-bound: carries ride in the MAC addend).
+#pragma once
+#include "fe25519.hpp"
+#include "ge25519.hpp"
+#include "sc25519.hpp"
+
+namespace cordahip {
+
+// B table: entry k (0..128) = [k]B as affine niels (y+x, y-x, 2d*x*y); 32
+// u32 per entry (30 limbs + 2 pad); entries [129, 258) = [k]B', B' = [2^128]B.
+static constexpr int kBTableEntries = 129;
+static constexpr int kBEntryWords = 32;
+static constexpr int kLdsBStride = 36;  // words per B entry in LDS (bank spread)
+static constexpr uint8_t kStatusPending = 0xff;
+
+// Per-lane workspace record (2,992 B, 16-B aligned fields):
+static constexpr int kWhTabA = 0;                // [0..8](-A), cached form, 40 words each
+static constexpr int kWhTabR = 9 * 40;           // [0..8](-R)
+static constexpr int kWhKa = 18 * 40;            // |c0|, c1, e (8 words each)
+static constexpr int kWhKr = kWhKa + 8;
+static constexpr int kWhE = kWhKa + 16;
+static constexpr int kWhFlags = kWhKa + 24;      // bit 0: c0 < 0
+static constexpr int kWhLaneWords = kWhKa + 28;  // 748 words
+
+// conditional negation of a niels / cached point: swap (y+x, y-x), negate t
+CDEV void niels_cneg(ge_niels& n, bool neg) {
+  fe nt;
+  fe_neg_loose(nt, n.xy2d);  // 2x: only ever the g-operand of fe_mul
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const uint32_t a = n.ypx.v[i], b = n.ymx.v[i];
+    n.ypx.v[i] = neg ? b : a;
+    n.ymx.v[i] = neg ? a : b;
+    n.xy2d.v[i] = neg ? nt.v[i] : n.xy2d.v[i];
+  }
+}
+CDEV void cached_cneg(ge_cached& c, bool neg) {
+  fe nt;
+  fe_neg_loose(nt, c.T2d);
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const uint32_t a = c.YpX.v[i], b = c.YmX.v[i];
+    c.YpX.v[i] = neg ? b : a;
+    c.YmX.v[i] = neg ? a : b;
+    c.T2d.v[i] = neg ? nt.v[i] : c.T2d.v[i];
+  }
+}
+
+CDEV void store_cached(uint32_t* __restrict__ o, const ge_cached& c) {
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+  uint32_t w[40];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    w[i] = c.YpX.v[i];
+    w[10 + i] = c.YmX.v[i];
+    w[20 + i] = c.Z.v[i];
+    w[30 + i] = c.T2d.v[i];
+  }
+#pragma unroll
+  for (int q = 0; q < 10; q++) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+CDEV void load_cached(ge_cached& c, const uint32_t* __restrict__ p) {
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);
+  uint32_t w[40];
+#pragma unroll
+  for (int q = 0; q < 10; q++) {
+    const uint4 v = p4[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    c.YpX.v[i] = w[i];
+    c.YmX.v[i] = w[10 + i];
+    c.Z.v[i] = w[20 + i];
+    c.T2d.v[i] = w[30 + i];
+  }
+}
+
+CDEV void store8(uint32_t* __restrict__ o, const uint32_t v[8]) {
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+  o4[0] = make_uint4(v[0], v[1], v[2], v[3]);
+  o4[1] = make_uint4(v[4], v[5], v[6], v[7]);
+}
+CDEV void load8(uint32_t v[8], const uint32_t* __restrict__ p) {
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);
+  const uint4 a = p4[0], b = p4[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+CDEV int mp8_bitlen(const uint32_t a[8]) {
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) n = a[i] ? 32 * i + 32 - __builtin_clz(a[i]) : n;
+  return n;
+}
+
+CDEV int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+// stops the machine scheduler from interleaving the phases on either side
+// (independent phases interleaved = both phases' registers live at once)
+#define PHASE_BARRIER() __builtin_amdgcn_sched_barrier(0)
+
+// host-side launcher of the ladder (ed25519_ladder.hip)
+hipError_t launch_ed25519_ladder(uint64_t base, uint64_t m, const uint32_t* btab, const uint32_t* ws, uint8_t* status,
+                                 unsigned long long* verdict, hipStream_t s);
+
+}  // namespace cordahip

@@ -167,10 +167,54 @@ CDEV void fe_fold_top(fe& r, uint64_t c) {
   r.v[1] += (uint32_t)(t >> 26);
 }
 
+// Term-major accumulation (FE_TERM_MAJOR): the ten 64-bit column sums grow
+// side by side, term t of every column before term t+1 of any, so the wave's
+// instruction stream holds ten independent v_mad_u64_u32 chains instead of one
+// dependent chain per column (a dependent v_mad_u64_u32 waits ~12 cycles; an
+// independent one issues every ~4). One sequential carry pass follows: per
+// column an and, a 64-bit shift and a 64-bit add (the same count as the
+// carry-chained form's and + shift + re-associated add).
+#ifndef FE_TERM_MAJOR
+#define FE_TERM_MAJOR 0
+#endif
+CDEV void fe_carry_cols(fe& o, uint64_t h[10]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    const uint64_t a = h[k] + c;
+    o.v[k] = (uint32_t)a & ((k & 1) ? M25 : M26);
+    c = a >> limb_bits(k);
+  }
+  fe_fold_top(o, c);
+}
+
 // h = f * g. Column k collects f_i g_j with i + j == k (mod 10); wrapped
 // terms carry 2^255 == 19, and odd*odd terms carry an extra 2 (radix 2^25.5).
 CDEV void fe_mul(fe& r, const fe& f, const fe& g) {
-#if FE_CARRY_CHAIN
+#if FE_TERM_MAJOR
+  uint32_t g19[10], f2[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    g19[i] = mul19(g.v[i]);
+    f2[i] = f.v[i] << 1;
+  }
+  uint64_t h[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+      const int j = (k - i + 10) % 10;
+      const bool wrap = (i + j) >= 10;
+      const bool oo = (i & 1) && (j & 1);
+      const uint32_t a = oo ? f2[i] : f.v[i];
+      const uint32_t b = wrap ? g19[j] : g.v[j];
+      h[k] = i == 0 ? (uint64_t)a * b : mac64(a, b, h[k]);
+    }
+  }
+  fe o;
+  fe_carry_cols(o, h);
+  r = o;
+#elif FE_CARRY_CHAIN
   uint32_t g19[10], f2[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
@@ -231,7 +275,37 @@ CDEV void fe_sq(fe& r, const fe& f) {
     f4[i] = f.v[i] << 2;
     f19[i] = mul19(f.v[i]);
   }
-#if FE_CARRY_CHAIN
+#if FE_TERM_MAJOR
+  // term-major over the (i, j >= i) pairs of each column: step t adds the t-th
+  // pair of every column that has one (columns hold 5 or 6 pairs)
+  uint64_t h[10];
+  bool started[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) started[k] = false;
+#pragma unroll
+  for (int t = 0; t < 6; t++) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        const int j = (k - i + 10) % 10;
+        if (j < i) continue;
+        if (cnt++ != t) continue;
+        const bool wrap = (i + j) >= 10;
+        const bool oo = (i & 1) && (j & 1);
+        const int mult = (i < j ? 2 : 1) * (oo ? 2 : 1);  // 1, 2 or 4
+        const uint32_t a = mult == 1 ? f.v[i] : (mult == 2 ? f2[i] : f4[i]);
+        const uint32_t b = wrap ? f19[j] : f.v[j];
+        h[k] = started[k] ? mac64(a, b, h[k]) : (uint64_t)a * b;
+        started[k] = true;
+      }
+    }
+  }
+  fe o;
+  fe_carry_cols(o, h);
+  r = o;
+#elif FE_CARRY_CHAIN
   fe o;
   uint64_t c = 0;
 #pragma unroll

@@ -54,8 +54,10 @@ class Engine:
         return np.ascontiguousarray(blob), off
 
     def verify_batch(self, schemes: Sequence[int], keys: Sequence[bytes], sigs: Sequence[bytes],
-                     msgs: Sequence[bytes], async_: bool = False):
-        """Per-lane statuses for (scheme, key, sig, msg) tuples; returns (status, verdict)."""
+                     msgs: Sequence[bytes], async_: bool = False, is_valid: bool = False):
+        """Per-lane statuses for (scheme, key, sig, msg) tuples; returns (status, verdict).
+        is_valid=False: Crypto.doVerify semantics (empty sig / clear data -> EMPTY);
+        is_valid=True: Crypto.isValid semantics (no emptiness checks)."""
         n = len(keys)
         sch = np.ascontiguousarray(np.asarray(schemes, dtype=np.uint8))
         kb, ko = self._csr(list(keys))
@@ -64,12 +66,12 @@ class Engine:
         status = np.zeros(max(n, 1), dtype=np.uint8)
         verdict = np.zeros(max((n + 63) // 64, 1), dtype=np.uint64)
         b = SigBatch(n, _ptr(sch), _ptr(kb), _ptr(ko), _ptr(sb), _ptr(so), _ptr(mb), _ptr(mo),
-                     _ptr(status), _ptr(verdict))
+                     _ptr(status), _ptr(verdict), _lib.FLAG_IS_VALID if is_valid else 0)
         keep = (sch, kb, ko, sb, so, mb, mo, status, verdict, b)
         if async_:
             t = ctypes.c_uint64()
             check(lib().cordahip_sig_submit(self._ctx, ctypes.byref(b), ctypes.byref(t)), "cordahip_sig_submit")
-            return Ticket(self, t.value, status[:n], verdict, keep)
+            return Ticket(self, t.value, lambda: (status[:n], verdict), keep)
         check(lib().cordahip_sig_verify(self._ctx, ctypes.byref(b)), "cordahip_sig_verify")
         return status[:n], verdict
 
@@ -121,14 +123,22 @@ class Engine:
         b = TxidBatch(len(txs), _ptr(lb), _ptr(lo), _ptr(to), _ptr(txid), _ptr(st))
         return b, (lb, lo, to, txid, st)
 
-    def tx_ids(self, txs: Sequence[Sequence[bytes]]):
-        """txs: per transaction, the serialised components (leaf preimages). Returns (ids[ntx,32], status[ntx])."""
+    def tx_ids(self, txs: Sequence[Sequence[bytes]], async_: bool = False):
+        """txs: per transaction, the serialised components (leaf preimages). Returns (ids[ntx,32], status[ntx])
+        (or a Ticket whose wait() returns them)."""
         b, keep = self._tx_arrays(txs)
+        res = lambda: (keep[3][:len(txs)], keep[4][:len(txs)])  # noqa: E731
+        if async_:
+            t = ctypes.c_uint64()
+            check(lib().cordahip_txid_submit(self._ctx, ctypes.byref(b), ctypes.byref(t)), "cordahip_txid_submit")
+            return Ticket(self, t.value, res, (b, keep))
         check(lib().cordahip_tx_ids(self._ctx, ctypes.byref(b)), "cordahip_tx_ids")
-        return keep[3][:len(txs)], keep[4][:len(txs)]
+        return res()
 
-    def signed_tx_verify(self, txs: Sequence[Sequence[bytes]], sigs: Sequence[Sequence[tuple]]):
-        """sigs[t] = [(scheme, key, sig), ...] in list order. Returns (ids, tx_status, first_bad, sig_status)."""
+    def signed_tx_verify(self, txs: Sequence[Sequence[bytes]], sigs: Sequence[Sequence[tuple]],
+                         async_: bool = False):
+        """sigs[t] = [(scheme, key, sig), ...] in list order. Returns (ids, tx_status, first_bad, sig_status)
+        (or, async_, a Ticket from cordahip_tx_submit whose wait() returns them)."""
         b, keep = self._tx_arrays(txs)
         flat = [x for per in sigs for x in per]
         so = np.zeros(len(txs) + 1, dtype=np.uint64)
@@ -140,9 +150,14 @@ class Engine:
         sst = np.zeros(max(len(flat), 1), dtype=np.uint8)
         fb = np.zeros(max(len(txs), 1), dtype=np.int64)
         sbatch = SignedTxBatch(b, _ptr(so), _ptr(sch), _ptr(kb), _ptr(ko), _ptr(sb), _ptr(sgo), _ptr(sst), _ptr(fb))
-        check(lib().cordahip_signed_tx_verify(self._ctx, ctypes.byref(sbatch)), "cordahip_signed_tx_verify")
         n = len(txs)
-        return keep[3][:n], keep[4][:n], fb[:n], sst[:len(flat)]
+        res = lambda: (keep[3][:n], keep[4][:n], fb[:n], sst[:len(flat)])  # noqa: E731
+        if async_:
+            t = ctypes.c_uint64()
+            check(lib().cordahip_tx_submit(self._ctx, ctypes.byref(sbatch), ctypes.byref(t)), "cordahip_tx_submit")
+            return Ticket(self, t.value, res, (keep, so, sch, kb, ko, sb, sgo, sst, fb, sbatch))
+        check(lib().cordahip_signed_tx_verify(self._ctx, ctypes.byref(sbatch)), "cordahip_signed_tx_verify")
+        return res()
 
     def signed_tx_verify_ed25519_device(self, leaf_bytes, leaf_off, tx_leaf_off, tx_sig_off, keys, sigs,
                                         txid, tx_status, first_bad, sig_status, device: int = 0, stream=None):
@@ -163,7 +178,7 @@ class Engine:
             verdict.data_ptr() if verdict is not None else None, s), "cordahip_ecdsa_verify_device")
 
     # ---- FilteredTransaction.verify / PartialMerkleTree.verify ----------------
-    def filtered_tx_verify(self, ftxs):
+    def filtered_tx_verify(self, ftxs, async_: bool = False):
         """ftxs[t] = (leaves: [bytes], tokens: [(tok, hash32 or None)], root: bytes32), tokens being the
         post-order stream of the PartialMerkleTree (oracle/partial_merkle.py tokens()). Returns tx_status."""
         leaves = [leaf for f in ftxs for leaf in f[0]]
@@ -180,6 +195,11 @@ class Engine:
         st = np.zeros(max(len(ftxs), 1), dtype=np.uint8)
         b = FilteredTxBatch(len(ftxs), _ptr(lb), _ptr(lo), _ptr(to), _ptr(tok), _ptr(th), _ptr(ko), _ptr(root),
                             _ptr(st))
+        if async_:
+            t = ctypes.c_uint64()
+            check(lib().cordahip_filtered_tx_submit(self._ctx, ctypes.byref(b), ctypes.byref(t)),
+                  "cordahip_filtered_tx_submit")
+            return Ticket(self, t.value, lambda: st[:len(ftxs)], (lb, lo, to, tok, th, ko, root, st, b))
         check(lib().cordahip_filtered_tx_verify(self._ctx, ctypes.byref(b)), "cordahip_filtered_tx_verify")
         return st[:len(ftxs)]
 
@@ -203,8 +223,11 @@ class Engine:
 
 
 class Ticket:
-    def __init__(self, eng: Engine, ticket: int, status, verdict, keep):
-        self.eng, self.ticket, self.status, self.verdict, self._keep = eng, ticket, status, verdict, keep
+    """A submitted batch (cordahip_*_submit). wait() releases the ticket and returns the
+    batch's results; poll() only reports completion. `keep` pins the host buffers."""
+
+    def __init__(self, eng: Engine, ticket: int, result, keep):
+        self.eng, self.ticket, self._result, self._keep = eng, ticket, result, keep
 
     def poll(self) -> bool:
         r = lib().cordahip_poll(self.eng.ctx, self.ticket)
@@ -214,4 +237,4 @@ class Ticket:
 
     def wait(self, timeout_ns: int = -1):
         check(lib().cordahip_wait(self.eng.ctx, self.ticket, timeout_ns), "cordahip_wait")
-        return self.status, self.verdict
+        return self._result()

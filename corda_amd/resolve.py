@@ -84,6 +84,10 @@ class SignedTx:
     sigs: List[Tuple[int, bytes, bytes]]
     must_sign: List[Union[bytes, CompositeKey]] = field(default_factory=list)
     inputs: List[bytes] = field(default_factory=list)
+    # for getMissingKeyDescriptions (SignedTransaction.kt:114-124): tx.commands as
+    # (command.toString(), signers) and tx.notary?.owningKey
+    commands: List[Tuple[str, List[Union[bytes, CompositeKey]]]] = field(default_factory=list)
+    notary: Optional[Union[bytes, CompositeKey]] = None
 
 
 def _lane_exception(status: int) -> Exception:
@@ -107,6 +111,17 @@ class Outcome:
     id: Optional[bytes]                 # WireTransaction.id (None when it cannot be computed)
     error: Optional[Exception]          # what verifySignatures() throws first, or None
     first_bad_sig: int = -1             # index in stx.sigs of the signature that threw
+
+
+def missing_key_descriptions(stx: SignedTx, missing) -> List[str]:
+    """getMissingKeyDescriptions (SignedTransaction.kt:114-124): every command with a
+    missing signer (command.toString(), in command order), then "notary" if the
+    notary's key is missing."""
+    miss = set(missing)
+    out = [desc for desc, signers in stx.commands if any(k in miss for k in signers)]
+    if stx.notary is not None and stx.notary in miss:
+        out.append("notary")
+    return out
 
 
 def verify_signatures_batch(engine, stxs: Sequence[SignedTx], allowed_to_be_missing=()) -> List[Outcome]:
@@ -134,10 +149,13 @@ def verify_signatures_batch(engine, stxs: Sequence[SignedTx], allowed_to_be_miss
             out.append(Outcome(tid, _lane_exception(st), int(first_bad[t])))
             continue
         sig_keys = {k for _, k, _ in stx.sigs}
-        missing = [k for k in stx.must_sign if not is_fulfilled_by(k, sig_keys)]
+        # getMissingSignatures (:102-108): mustSign.filter { !isFulfilledBy }.toSet() -- a
+        # LinkedHashSet, so duplicates collapse and list order is kept; `missing - allowed`
+        # (:79) keeps that order too
+        missing = dict.fromkeys(k for k in stx.must_sign if not is_fulfilled_by(k, sig_keys))
         needed = [k for k in missing if k not in allowed]
         if needed:
-            out.append(Outcome(tid, SignaturesMissingException(needed, [], tid)))
+            out.append(Outcome(tid, SignaturesMissingException(needed, missing_key_descriptions(stx, needed), tid)))
             continue
         out.append(Outcome(tid, None))
     return out

@@ -18,10 +18,13 @@
  *   cordahip_tx_ids (tx id = Merkle root of component hashes)
  *       -> WireTransaction.id (WireTransaction.kt:48) = MerkleTree.getMerkleTree(
  *          availableComponentHashes).hash (MerkleTree.kt:27-66, MerkleTransaction.kt:69)
- *   cordahip_signed_tx_verify
+ *   cordahip_signed_tx_verify / cordahip_tx_submit
  *       -> SignedTransaction.checkSignaturesAreValid (SignedTransaction.kt:95-100)
  *          + the tx.id recomputation of verifySignatures (:70-85); signer coverage
- *          (getMissingSignatures :102-108) stays with the caller, see INTEGRATION.md
+ *          (getMissingSignatures :102-108) stays with the caller, see INTEGRATION.md.
+ *          The _submit forms return a ticket at once: the caller (a Quasar fiber in
+ *          ResolveTransactionsFlow.call, ResolveTransactionsFlow.kt:97-122, on the
+ *          single Node thread) suspends on it instead of blocking the thread.
  *
  * Result contract: a return value < 0 means the whole call failed (the caller
  * falls back to the JVM path for that batch); per-lane outcomes are DATA in
@@ -43,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CORDAHIP_ABI_VERSION 1u
+#define CORDAHIP_ABI_VERSION 2u
 
 /* ---- per-lane statuses (status[i]) ------------------------------------- */
 #define CORDAHIP_STATUS_OK 0            /* isValid -> true;  doVerify -> true                         */
@@ -87,7 +90,14 @@ int cordahip_free_pinned(cordahip_ctx* ctx, void* host);
  * Variable-length fields are CSR: item i's key is key[key_off[i] .. key_off[i+1]).
  * Key encodings: Ed25519 = the 32-byte A (Kryo wire form, Kryo.kt:386); ECDSA =
  * SEC1 point (the SPKI BIT STRING payload, Crypto.kt:348-355).
- * verdict (optional): bit (i % 64) of word (i / 64) = (status[i] == OK).     */
+ * verdict (optional): bit (i % 64) of word (i / 64) = (status[i] == OK).
+ * flags: 0 = Crypto.doVerify semantics (Crypto.kt:472-483: empty signature or
+ * clear data -> EMPTY); CORDAHIP_FLAG_IS_VALID = Crypto.isValid semantics
+ * (Crypto.kt:534-541: no emptiness checks; an empty clear data is hashed like
+ * any other message and may verify, an empty signature is MALFORMED_SIG at the
+ * engine). Lanes are sharded over every context device (contiguous, 64-aligned
+ * shards of each scheme's lanes; cordahip_shard_range).                      */
+#define CORDAHIP_FLAG_IS_VALID 1u
 typedef struct {
   uint64_t n;
   const uint8_t* scheme; /* [n] CORDAHIP_SCHEME_* */
@@ -99,10 +109,17 @@ typedef struct {
   const uint64_t* msg_off; /* [n+1] */
   uint8_t* status;         /* [n] out */
   uint64_t* verdict;       /* [(n+63)/64] out, may be NULL */
+  uint32_t flags;          /* CORDAHIP_FLAG_* */
 } cordahip_sig_batch;
 
+/* Tickets: every *_submit queues the batch on the context's worker pool and
+ * returns at once. cordahip_wait() returns the batch's result code and RELEASES
+ * the ticket (a second wait gives CORDAHIP_ERR_UNKNOWN_TICKET); cordahip_poll()
+ * only reports progress, so every ticket must be waited on once (shutdown
+ * waits for and releases the rest). The descriptor is copied at submit; the
+ * buffers it points to stay the caller's and must stay untouched until wait. */
 int cordahip_sig_submit(cordahip_ctx* ctx, const cordahip_sig_batch* batch, uint64_t* ticket);
-/* timeout_ns < 0: wait forever. Returns the batch's result code. */
+/* timeout_ns < 0: wait forever; CORDAHIP_ERR_TIMEOUT keeps the ticket. */
 int cordahip_wait(cordahip_ctx* ctx, uint64_t ticket, int64_t timeout_ns);
 /* 1 = done (result retrievable with wait), 0 = pending, < 0 = error */
 int cordahip_poll(cordahip_ctx* ctx, uint64_t ticket);
@@ -211,6 +228,11 @@ typedef struct {
 } cordahip_signed_tx_batch;
 int cordahip_signed_tx_verify(cordahip_ctx* ctx, const cordahip_signed_tx_batch* batch);
 
+/* Ticketed forms of cordahip_signed_tx_verify / cordahip_tx_ids (SURVEY §8b
+ * cordahip_tx_submit): same results, completed through cordahip_wait/poll. */
+int cordahip_tx_submit(cordahip_ctx* ctx, const cordahip_signed_tx_batch* batch, uint64_t* ticket);
+int cordahip_txid_submit(cordahip_ctx* ctx, const cordahip_txid_batch* batch, uint64_t* ticket);
+
 /* Device-resident dense variant (all Ed25519, 32-byte keys, 64-byte sigs;
  * every array in HBM on `device`): K3 leaf hashes -> K4 Merkle roots ->
  * txid gather -> K1 verify -> K5 per-tx reduce, all on hip_stream. */
@@ -244,10 +266,20 @@ typedef struct {
   uint8_t* tx_status;          /* [ntx] out */
 } cordahip_filtered_tx_batch;
 int cordahip_filtered_tx_verify(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch);
+int cordahip_filtered_tx_submit(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch, uint64_t* ticket);
 
-/* Device time of the last kernel launched by the context on `device` (ms), measured
- * with HIP events on the stream the kernel ran on; -1 if unavailable. */
+/* Device time (ms) of the calling thread's most recent *_device call on
+ * `device`, from HIP events recorded around its launches on the stream it ran
+ * on (waits for them); -1 if the thread made no such call. Each call gets its
+ * own event pair from a per-device ring of 64, so concurrent callers on other
+ * threads or streams do not disturb it. */
 double cordahip_last_kernel_ms(cordahip_ctx* ctx, int device);
+
+/* The in-process partition rule: shard `shard` of `nshards` over n lanes is
+ * [*lo, *hi), contiguous, 64-aligned starts (whole verdict words), the last
+ * shard possibly short or empty. Every multi-device host path uses it (per
+ * scheme for generic batches; per transaction for tx batches, align 1). */
+void cordahip_shard_range(uint64_t n, uint32_t nshards, uint32_t shard, uint64_t align, uint64_t* lo, uint64_t* hi);
 
 #ifdef __cplusplus
 }

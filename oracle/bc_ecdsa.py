@@ -172,14 +172,17 @@ def der_encode(r: int, s: int) -> bytes:
     return b"\x30" + _der_len(len(body)) + body
 
 
-def verify_status(scheme: int, pub: bytes, sig: bytes, msg: bytes) -> int:
+def verify_status(scheme: int, pub: bytes, sig: bytes, msg: bytes, is_valid: bool = False) -> int:
+    """Crypto.doVerify semantics (Crypto.kt:472-483) by default; is_valid=True gives
+    Crypto.isValid (:534-541), which has no emptiness checks (the empty message is
+    hashed, an empty signature fails DER decoding)."""
     c = CURVES.get(scheme)
     if c is None:
         return UNSUPPORTED
     Q = decode_point(c, pub)  # key decode precedes doVerify's checks
     if Q is None:
         return BAD_KEY
-    if len(sig) == 0 or len(msg) == 0:
+    if not is_valid and (len(sig) == 0 or len(msg) == 0):
         return EMPTY
     rs = der_decode(sig)
     if rs is None:

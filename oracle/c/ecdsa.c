@@ -317,14 +317,15 @@ static int der_decode(const uint8_t* sig, size_t n, der_int_t out[2]) {
   return cnt == 2 ? 0 : -1;
 }
 
-int oracle_ecdsa_verify(int scheme, const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
-                        const uint8_t* msg, size_t msglen) {
+static int ec_verify(int scheme, const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
+                     const uint8_t* msg, size_t msglen, int is_valid) {
   pthread_once(&ec_once, ec_init);
   const curve_t* c = scheme == 2 ? &CURVE_K1 : scheme == 3 ? &CURVE_R1 : NULL;
   if (!c) return ORACLE_UNSUPPORTED;
   jac_t Q;
   if (decode_point(c, &Q, pub, publen)) return ORACLE_BAD_KEY;
-  if (siglen == 0 || msglen == 0) return ORACLE_EMPTY;
+  /* Crypto.doVerify require checks (Crypto.kt:475-476); Crypto.isValid (:534-541) has none */
+  if (!is_valid && (siglen == 0 || msglen == 0)) return ORACLE_EMPTY;
   der_int_t rs[2];
   if (der_decode(sig, siglen, rs)) return ORACLE_MALFORMED_SIG;
   const mod_t* N = &c->N;
@@ -364,6 +365,16 @@ int oracle_ecdsa_verify(int scheme, const uint8_t* pub, size_t publen, const uin
   from_mont(M, &x, &x);
   if (u256_cmp(&x, &N->m) >= 0) u256_sub(&x, &x, &N->m);
   return u256_cmp(&x, &rs[0].v) == 0 ? ORACLE_OK : ORACLE_BAD_SIG;
+}
+
+int oracle_ecdsa_verify(int scheme, const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
+                        const uint8_t* msg, size_t msglen) {
+  return ec_verify(scheme, pub, publen, sig, siglen, msg, msglen, 0);
+}
+
+int oracle_ecdsa_is_valid(int scheme, const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
+                          const uint8_t* msg, size_t msglen) {
+  return ec_verify(scheme, pub, publen, sig, siglen, msg, msglen, 1);
 }
 
 typedef struct {

@@ -342,15 +342,15 @@ static void sc_reduce64(uint8_t out[32], const uint8_t in[64]) {
 
 static void pthread_init(void) { init_consts(); }
 
-int oracle_ed25519_verify(const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
-                          const uint8_t* msg, size_t msglen) {
+static int ed_verify(const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen, const uint8_t* msg,
+                     size_t msglen, int is_valid) {
   pthread_once(&g_once, pthread_init);
   /* key decode happens at key construction (Kryo.kt:389-392), before verify */
   if (publen != 32) return ORACLE_BAD_KEY;
   ge_p3 A;
   if (ge_decode_i2p(&A, pub) != 0) return ORACLE_BAD_KEY;
-  /* Crypto.doVerify require checks (Crypto.kt:475-476) */
-  if (siglen == 0 || msglen == 0) return ORACLE_EMPTY;
+  /* Crypto.doVerify require checks (Crypto.kt:475-476); Crypto.isValid (:534-541) has none */
+  if (!is_valid && (siglen == 0 || msglen == 0)) return ORACLE_EMPTY;
   if (siglen != 64) return ORACLE_MALFORMED_SIG;
   uint8_t abyte[32];
   ge_tobytes(abyte, &A);
@@ -374,6 +374,16 @@ int oracle_ed25519_verify(const uint8_t* pub, size_t publen, const uint8_t* sig,
   uint8_t rc[32];
   ge_tobytes(rc, &R);
   return memcmp(rc, sig, 32) == 0 ? ORACLE_OK : ORACLE_BAD_SIG;
+}
+
+int oracle_ed25519_verify(const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
+                          const uint8_t* msg, size_t msglen) {
+  return ed_verify(pub, publen, sig, siglen, msg, msglen, 0);
+}
+
+int oracle_ed25519_is_valid(const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
+                            const uint8_t* msg, size_t msglen) {
+  return ed_verify(pub, publen, sig, siglen, msg, msglen, 1);
 }
 
 typedef struct {

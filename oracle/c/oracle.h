@@ -39,6 +39,11 @@ int oracle_slide(const uint8_t a[32], int8_t r[256]);
 int oracle_ed25519_verify(const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
                           const uint8_t* msg, size_t msglen);
 
+/* Same lane under Crypto.isValid semantics (Crypto.kt:534-541): no emptiness
+ * checks (an empty message is hashed; an empty signature fails the length check). */
+int oracle_ed25519_is_valid(const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
+                            const uint8_t* msg, size_t msglen);
+
 /* Dense batch: keys n*32, sigs n*64, msgs n*msglen; nthreads<=0 -> 1. */
 void oracle_ed25519_verify_batch(size_t n, const uint8_t* pubs, const uint8_t* sigs,
                                  const uint8_t* msgs, size_t msglen, uint8_t* status,
@@ -57,6 +62,8 @@ int oracle_merkle_root(const uint8_t* leaves, size_t nleaves, uint8_t root[32]);
  * SEC1 key, DER sig, msg) with BouncyCastle 1.57 semantics (oracle/bc_ecdsa.py). */
 int oracle_ecdsa_verify(int scheme, const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
                         const uint8_t* msg, size_t msglen);
+int oracle_ecdsa_is_valid(int scheme, const uint8_t* pub, size_t publen, const uint8_t* sig, size_t siglen,
+                          const uint8_t* msg, size_t msglen); /* Crypto.isValid semantics, as above */
 void oracle_ecdsa_verify_batch(size_t n, const uint8_t* scheme, const uint8_t* key, const uint64_t* key_off,
                                const uint8_t* sig, const uint64_t* sig_off, const uint8_t* msg,
                                const uint64_t* msg_off, uint8_t* status, int nthreads);

@@ -200,7 +200,7 @@ def double_scalar_mult_vartime(a_neg, h: bytes, s: bytes):
     return r
 
 
-def verify_status(pub: bytes, sig: bytes, msg: bytes) -> int:
+def verify_status(pub: bytes, sig: bytes, msg: bytes, is_valid: bool = False) -> int:
     """Per-lane status of Crypto.isValid/doVerify for EDDSA_ED25519_SHA512.
 
     Order of checks follows the reference call chain:
@@ -213,7 +213,7 @@ def verify_status(pub: bytes, sig: bytes, msg: bytes) -> int:
     A = decode_i2p(pub)
     if A is None:
         return BAD_KEY
-    if len(sig) == 0 or len(msg) == 0:
+    if not is_valid and (len(sig) == 0 or len(msg) == 0):  # is_valid: Crypto.isValid has no such check
         return EMPTY
     if len(sig) != 64:
         return MALFORMED_SIG

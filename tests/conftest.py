@@ -38,6 +38,8 @@ def load_oracle():
     lib.oracle_merkle_root.argtypes = [cp, sz, ctypes.c_char_p]
     lib.oracle_slide.argtypes = [cp, ctypes.c_char_p]
     lib.oracle_ecdsa_verify.argtypes = [ctypes.c_int, cp, sz, cp, sz, cp, sz]
+    lib.oracle_ecdsa_is_valid.argtypes = [ctypes.c_int, cp, sz, cp, sz, cp, sz]
+    lib.oracle_ed25519_is_valid.argtypes = [cp, sz, cp, sz, cp, sz]
     lib.oracle_ecdsa_verify_batch.argtypes = [sz] + [ctypes.c_void_p] * 8 + [ctypes.c_int]
     lib.oracle_tx_id.argtypes = [ctypes.c_void_p, ctypes.c_void_p, sz, ctypes.c_char_p]
     return lib

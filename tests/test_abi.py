@@ -41,7 +41,9 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_abi_version_and_errors(lib):
-    assert lib.cordahip_abi_version() == 1
+    from corda_amd import _lib
+    assert lib.cordahip_abi_version() == _lib.ABI_VERSION == 2
+    assert "#define CORDAHIP_ABI_VERSION 2u" in open(HEADER).read()
     assert lib.cordahip_strerror(0) == b"success"
     assert lib.cordahip_strerror(-7) == b"not implemented on the GPU path"
     assert lib.cordahip_strerror(12345) == b"unknown error"
@@ -52,7 +54,10 @@ def test_init_rejects_bad_args_without_device(lib):
     # no context: every entry point fails with INVALID_ARG instead of crashing
     assert lib.cordahip_sig_verify(None, None) == -1
     assert lib.cordahip_wait(None, 1, 0) == -1
+    assert lib.cordahip_poll(None, 1) == -1
     assert lib.cordahip_device_count(None) == 0
+    for f in ("cordahip_sig_submit", "cordahip_tx_submit", "cordahip_txid_submit", "cordahip_filtered_tx_submit"):
+        assert getattr(lib, f)(None, None, None) == -1, f
 
 
 def test_status_codes_match_header():
@@ -63,3 +68,38 @@ def test_status_codes_match_header():
                     "BAD_KEY": _lib.BAD_KEY, "UNSUPPORTED": _lib.UNSUPPORTED, "EMPTY": _lib.EMPTY}
     import i2p_ed25519 as ed
     assert (ed.OK, ed.BAD_SIG, ed.MALFORMED_SIG, ed.BAD_KEY, ed.UNSUPPORTED, ed.EMPTY) == (0, 1, 2, 3, 4, 5)
+
+
+def test_sig_batch_layout_matches_header():
+    """cordahip_sig_batch as ctypes sees it == the C struct (flags appended in ABI 2)."""
+    import ctypes
+    from corda_amd import _lib
+    assert [f[0] for f in _lib.SigBatch._fields_] == ["n", "scheme", "key", "key_off", "sig", "sig_off", "msg",
+                                                      "msg_off", "status", "verdict", "flags"]
+    assert ctypes.sizeof(_lib.SigBatch) == 11 * 8  # 10 8-byte fields + u32 flags padded to 8
+    src = open(HEADER).read()
+    assert "#define CORDAHIP_FLAG_IS_VALID 1u" in src and _lib.FLAG_IS_VALID == 1
+
+
+def test_shard_range_rule(lib):
+    """The in-process partition (cordahip_shard_range, used by every multi-device
+    host path: Ed25519, ECDSA, stream sections, tx batches): contiguous, covering,
+    disjoint, 64-aligned starts so each device owns whole verdict words."""
+    from corda_amd import _lib
+    for n in (0, 1, 63, 64, 65, 1000, 4096, 100003, 1 << 24):
+        for nd in (1, 2, 3, 7, 8):
+            for align in (1, 64):
+                prev = 0
+                for i in range(nd):
+                    lo, hi = _lib.shard_range(n, nd, i, align)
+                    assert lo == prev and lo <= hi <= n, (n, nd, align, i, lo, hi)
+                    if lo < n:
+                        assert lo % align == 0
+                    prev = hi
+                assert prev == n
+                # equal shares up to alignment: no device gets more than ceil(n/nd) rounded up to align
+                per = -(-(-(-n // nd)) // align) * align
+                assert all(_lib.shard_range(n, nd, i, align)[1] - _lib.shard_range(n, nd, i, align)[0] <= per
+                           for i in range(nd))
+    assert _lib.shard_range(100, 4, 9, 64) == (100, 100)  # out-of-range shard: empty
+    assert _lib.shard_range(100, 0, 0, 64) == (100, 100)

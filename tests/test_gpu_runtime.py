@@ -1,0 +1,308 @@
+"""Host-runtime contracts of libcordahip.so on the GPU, through the C-ABI:
+Crypto.isValid vs Crypto.doVerify semantics (empty clear data), ticketed tx
+batches (cordahip_tx_submit & co.), concurrent users of the shared device
+buffers on several streams, per-thread kernel timing, the dense ECDSA slot
+bound, and the multi-chunk workspace paths (forced small in a subprocess,
+since the workspace size is read once per process)."""
+import ctypes
+import hashlib
+import json
+import os
+import random
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ED = 4
+
+
+def _ed_sign(oracle, seed, msg):
+    pub, sig = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+    oracle.oracle_ed25519_sign(seed, msg, len(msg), pub, sig)
+    return pub.raw, sig.raw
+
+
+def _empty_message_lanes(oracle):
+    """Lanes around the empty-clear-data rule: valid signatures OVER the empty
+    message, corrupted ones, empty signatures, both curves and Ed25519."""
+    import bc_ecdsa as ec
+    rng = random.Random(77)
+    rows = []
+    for i in range(24):
+        seed = hashlib.sha256(b"empty-msg-%d" % i).digest()
+        msg = b"" if i % 3 else hashlib.sha256(b"m%d" % i).digest()
+        pub, sig = _ed_sign(oracle, seed, msg)
+        if i % 4 == 1:
+            sig = sig[:5] + bytes([sig[5] ^ 0x20]) + sig[6:]
+        if i % 6 == 5:
+            sig = b""
+        rows.append((ED, pub, sig, msg))
+    for i in range(24):
+        scheme = 2 + (i & 1)
+        c = ec.CURVES[scheme]
+        d = rng.randrange(1, c.n)
+        msg = b"" if i % 3 else hashlib.sha256(b"e%d" % i).digest()
+        r, s = ec.sign(scheme, d, msg, rng.randrange(1, c.n))
+        sig = ec.der_encode(r, s)
+        if i % 4 == 1:
+            sig = ec.der_encode(r, s ^ 4)
+        if i % 6 == 5:
+            sig = b""
+        pub = ec.keypair(scheme, d)
+        rows.append((scheme, pub if i % 5 else ec.compress(pub), sig, msg))
+    return rows
+
+
+def test_is_valid_vs_do_verify_on_empty_clear_data(engine, oracle):
+    """Crypto.isValid (Crypto.kt:534-541) has no emptiness checks: a signature over
+    the empty message verifies, an empty signature is the engine's length / DER
+    failure. Crypto.doVerify (:472-483) throws IllegalArgumentException first
+    (EMPTY). Both modes lane for lane against the oracle's two entry points."""
+    rows = _empty_message_lanes(oracle)
+    st_v, _ = engine.verify_batch(*zip(*rows))
+    st_i, vd_i = engine.verify_batch(*zip(*rows), is_valid=True)
+    for (sch, k, s, m), a, b in zip(rows, st_v, st_i):
+        if sch == ED:
+            want_v = oracle.oracle_ed25519_verify(k, len(k), s, len(s), m, len(m))
+            want_i = oracle.oracle_ed25519_is_valid(k, len(k), s, len(s), m, len(m))
+        else:
+            want_v = oracle.oracle_ecdsa_verify(sch, k, len(k), s, len(s), m, len(m))
+            want_i = oracle.oracle_ecdsa_is_valid(sch, k, len(k), s, len(s), m, len(m))
+        assert (int(a), int(b)) == (want_v, want_i), (sch, len(s), len(m))
+    # the cells that differ: valid over empty message OK under isValid, EMPTY under doVerify
+    empties_ok = [i for i, r in enumerate(rows) if not r[3] and r[2] and int(st_i[i]) == 0]
+    assert len(empties_ok) >= 12 and all(int(st_v[i]) == 5 for i in empties_ok)
+    assert all(int(st_i[i]) == 2 for i, r in enumerate(rows) if not r[2])  # empty sig: MALFORMED_SIG
+    for i in range(len(rows)):
+        assert ((int(vd_i[i // 64]) >> (i % 64)) & 1) == (int(st_i[i]) == 0)
+
+
+def _tx_batch(oracle, rng, ntx, tag):
+    """ntx transactions: random leaves, 1-3 Ed25519 signers over the oracle tx id,
+    ~10% of signatures corrupted, ~3% of transactions with a corrupted leaf AFTER
+    signing (the id changes: every signature fails). Returns host data and the
+    expected (ids, tx_status, first_bad, sig_status)."""
+    txs, sigs, ids = [], [], []
+    out = ctypes.create_string_buffer(32)
+    for t in range(ntx):
+        leaves = [bytes(rng.getrandbits(8) for _ in range(rng.choice((0, 7, 43, 55, 140, 150, 450))))
+                  for _ in range(rng.choice((1, 2, 5, 5, 9)))]
+        blob = np.frombuffer(b"".join(leaves) or b"\0", np.uint8).copy()
+        off = np.zeros(len(leaves) + 1, np.uint64)
+        off[1:] = np.cumsum([len(x) for x in leaves])
+        assert oracle.oracle_tx_id(blob.ctypes.data, off.ctypes.data, len(leaves), out) == 0
+        tid = out.raw
+        per = []
+        for k in range(rng.randrange(1, 4)):
+            pub, sig = _ed_sign(oracle, hashlib.sha256(b"%s-%d-%d" % (tag, t, k)).digest(), tid)
+            if rng.random() < 0.1:
+                sig = sig[:40] + bytes([sig[40] ^ 1]) + sig[41:]
+            per.append((ED, pub, sig))
+        if rng.random() < 0.03:
+            j = max(range(len(leaves)), key=lambda q: len(leaves[q]))
+            if leaves[j]:
+                leaves[j] = bytes([leaves[j][0] ^ 0x80]) + leaves[j][1:]
+                blob = np.frombuffer(b"".join(leaves), np.uint8).copy()
+                assert oracle.oracle_tx_id(blob.ctypes.data, off.ctypes.data, len(leaves), out) == 0
+                tid = out.raw
+        txs.append(leaves)
+        sigs.append(per)
+        ids.append(tid)
+    sig_st = []
+    tx_st, first = [], []
+    for t in range(ntx):
+        ss = [oracle.oracle_ed25519_verify(k, 32, s, 64, ids[t], 32) for (_, k, s) in sigs[t]]
+        sig_st += ss
+        bad = [i for i, x in enumerate(ss) if x]
+        first.append(bad[0] if bad else -1)
+        tx_st.append(ss[bad[0]] if bad else 0)
+    return txs, sigs, (ids, tx_st, first, sig_st)
+
+
+def _device_tx(torch, dev, txs, sigs):
+    leaves = [leaf for tx in txs for leaf in tx]
+    lb = np.frombuffer(b"".join(leaves) or b"\0", np.uint8).copy()
+    lo = np.zeros(len(leaves) + 1, np.int64)
+    lo[1:] = np.cumsum([len(x) for x in leaves])
+    to = np.zeros(len(txs) + 1, np.int64)
+    to[1:] = np.cumsum([len(tx) for tx in txs])
+    so = np.zeros(len(txs) + 1, np.int64)
+    so[1:] = np.cumsum([len(s) for s in sigs])
+    flat = [x for per in sigs for x in per]
+    K = np.frombuffer(b"".join(x[1] for x in flat), np.uint8).reshape(-1, 32).copy()
+    S = np.frombuffer(b"".join(x[2] for x in flat), np.uint8).reshape(-1, 64).copy()
+    t = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    ntx, ns = len(txs), len(flat)
+    return dict(leaf_bytes=t(lb), leaf_off=t(lo), tx_leaf_off=t(to), tx_sig_off=t(so), keys=t(K), sigs=t(S),
+                txid=torch.empty((ntx, 32), dtype=torch.uint8, device=dev),
+                tx_status=torch.empty(ntx, dtype=torch.uint8, device=dev),
+                first_bad=torch.empty(ntx, dtype=torch.int64, device=dev),
+                sig_status=torch.empty(ns, dtype=torch.uint8, device=dev))
+
+
+def _check_device(d, want):
+    ids, tx_st, first, sig_st = want
+    assert [bytes(x) for x in d["txid"].cpu().numpy()] == ids
+    assert [int(x) for x in d["tx_status"].cpu()] == tx_st
+    assert [int(x) for x in d["first_bad"].cpu()] == first
+    assert [int(x) for x in d["sig_status"].cpu()] == sig_st
+
+
+def test_concurrent_device_and_host_tx_users(engine, oracle):
+    """Two cordahip_signed_tx_verify_ed25519_device calls on two streams and a host
+    cordahip_tx_ids call from another thread, all in flight together, several rounds
+    with growing sizes (the shared tx buffers are re-allocated while an earlier
+    stream may still read them): every id and status matches the oracle."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    rng = random.Random(1234)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    for rnd, (na, nb, nh) in enumerate(((40, 90, 60), (300, 120, 200), (700, 1500, 400))):
+        ta, sa, wa = _tx_batch(oracle, rng, na, b"a%d" % rnd)
+        tb, sb, wb = _tx_batch(oracle, rng, nb, b"b%d" % rnd)
+        th, _, wh = _tx_batch(oracle, rng, nh, b"h%d" % rnd)
+        da, db = _device_tx(torch, dev, ta, sa), _device_tx(torch, dev, tb, sb)
+        torch.cuda.synchronize(dev)
+        host_out = {}
+
+        def host():
+            host_out["r"] = engine.tx_ids(th)
+
+        thr = threading.Thread(target=host)
+        engine.signed_tx_verify_ed25519_device(**da, stream=s1)
+        thr.start()
+        engine.signed_tx_verify_ed25519_device(**db, stream=s2)
+        thr.join()
+        torch.cuda.synchronize(dev)
+        _check_device(da, wa)
+        _check_device(db, wb)
+        ids, st = host_out["r"]
+        assert [x.tobytes() for x in ids] == wh[0] and (st == 0).all()
+
+
+def test_tx_submit_tickets(engine, oracle):
+    """cordahip_tx_submit / cordahip_txid_submit / cordahip_filtered_tx_submit:
+    several tickets in flight, polled, then waited in reverse order; results equal
+    the synchronous calls; a ticket is single-use (wait releases it)."""
+    from corda_amd._lib import EngineError
+    rng = random.Random(55)
+    batches = [_tx_batch(oracle, rng, n, b"tk%d" % i) for i, n in enumerate((50, 333, 7))]
+    tickets = [engine.signed_tx_verify(txs, sigs, async_=True) for txs, sigs, _ in batches]
+    tid = engine.tx_ids(batches[0][0], async_=True)
+    cases = json.load(open(os.path.join(ROOT, "tests", "golden", "pmt_vectors.json")))["cases"]
+    ftx = [([bytes.fromhex(x) for x in c["leaves"]], [(t, bytes.fromhex(h) if h else None) for t, h in c["tokens"]],
+            bytes.fromhex(c["root"])) for c in cases]
+    tf = engine.filtered_tx_verify(ftx, async_=True)
+    for t in tickets + [tid, tf]:
+        assert t.poll() in (False, True)
+    for t, (txs, sigs, want) in reversed(list(zip(tickets, batches))):
+        ids, tx_st, first, sig_st = t.wait()
+        assert [x.tobytes() for x in ids] == want[0]
+        assert [int(x) for x in tx_st] == want[1] and [int(x) for x in first] == want[2]
+        assert [int(x) for x in sig_st] == want[3]
+        with pytest.raises(EngineError) as ei:
+            t.wait()
+        assert ei.value.code == -6  # CORDAHIP_ERR_UNKNOWN_TICKET: released by the first wait
+    ids, st = tid.wait()
+    assert [x.tobytes() for x in ids] == batches[0][2][0]
+    assert [int(x) for x in tf.wait()] == [c["status"] for c in cases]
+
+
+def test_last_kernel_ms_is_per_thread(engine):
+    """Each thread reads the timing of ITS OWN most recent device call, not another
+    thread's (per-call event pairs)."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    res = {}
+    order = threading.Barrier(2)
+    done = threading.Barrier(2)
+
+    def run(tag, n, first):
+        s = torch.cuda.Stream(dev)
+        k = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+        g = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
+        m = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+        st = torch.empty(n, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        if not first:
+            order.wait()  # the small call is enqueued first, then the large one
+        engine.ed25519_verify_device(k, g, m, st, stream=s)
+        if first:
+            order.wait()
+        done.wait()  # both calls made before either thread reads its timing
+        res[tag] = engine.last_kernel_ms()
+
+    t1 = threading.Thread(target=run, args=("small", 64, True))
+    t2 = threading.Thread(target=run, args=("large", 1 << 16, False))
+    t1.start(); t2.start(); t1.join(); t2.join()
+    assert res["small"] > 0 and res["large"] > 0 and res["large"] > res["small"], res
+    assert engine.last_kernel_ms() == -1.0 or engine.last_kernel_ms() > 0  # this thread: its own (or none)
+
+
+def test_dense_ecdsa_sig_len_beyond_slot(engine, ec_vectors):
+    """ADVICE: sig_len > 72 on the dense device path (72-byte slots) must not read
+    past the slot; such a lane is MALFORMED_SIG (EMPTY for an empty message under
+    doVerify precedence stays behind the key check), neighbours unaffected —
+    including the LAST lane of the batch with sig_len 255."""
+    torch = pytest.importorskip("torch")
+    vs = [v for v in ec_vectors if len(v["pub"]) in (33, 65) and len(v["sig"]) <= 72 and len(v["msg"]) == 32
+          and v["status"] in (0, 1)][:130]
+    n = len(vs)
+    keys = np.zeros((n, 65), np.uint8)
+    sigs = np.zeros((n, 72), np.uint8)
+    kl = np.array([len(v["pub"]) for v in vs], np.uint8)
+    sl = np.array([len(v["sig"]) for v in vs], np.uint8)
+    for i, v in enumerate(vs):
+        keys[i, :len(v["pub"])] = np.frombuffer(v["pub"], np.uint8)
+        sigs[i, :len(v["sig"])] = np.frombuffer(v["sig"], np.uint8)
+    want = [v["status"] for v in vs]
+    for i, ln in ((n - 1, 255), (n // 2, 73), (3, 200)):
+        sl[i] = ln
+        want[i] = 2
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    sch = t(np.array([v["scheme"] for v in vs], np.uint8))
+    msgs = t(np.frombuffer(b"".join(v["msg"] for v in vs), np.uint8).reshape(n, 32))
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    engine.ecdsa_verify_device(sch, t(keys), t(kl), t(sigs), t(sl), msgs, st)
+    torch.cuda.synchronize()
+    assert [int(x) for x in st.cpu()] == want
+
+
+CHUNK_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, %(root)r); sys.path.insert(0, %(root)r + "/tests")
+from corda_amd.engine import Engine
+from conftest import load_oracle
+vs = json.load(open(%(root)r + "/tests/golden/ecdsa_vectors.json"))["vectors"]
+ed = json.load(open(%(root)r + "/tests/golden/ed25519_vectors.json"))["vectors"]
+# curve runs that do not end on a multiple of 64: 150 secp256k1 lanes, then P-256, then Ed25519
+k1 = [v for v in vs if v["scheme"] == 2][:150]
+r1 = [v for v in vs if v["scheme"] == 3][:173]
+rows = k1 + r1 + ed[:200]
+h = lambda x: bytes.fromhex(x)
+with Engine(1) as eng:
+    st, _ = eng.verify_batch([v.get("scheme", 4) for v in rows], [h(v["pub"]) for v in rows],
+                             [h(v["sig"]) for v in rows], [h(v["msg"]) for v in rows])
+bad = [(i, int(s), v["status"]) for i, (v, s) in enumerate(zip(rows, st)) if int(s) != v["status"]]
+print(json.dumps({"n": len(rows), "bad": bad[:10]}))
+sys.exit(1 if bad else 0)
+"""
+
+
+@pytest.mark.parametrize("slots", ["64", "128"])
+def test_workspace_chunking_subprocess(slots):
+    """ADVICE: the multi-chunk workspace paths (several prep / inversion / ladder
+    launch sets per batch; batch inversion runs crossing a chunk boundary AND the
+    secp256k1 / P-256 boundary; Ed25519 prep/ladder pairs over 64-lane chunks),
+    forced with tiny workspaces in a fresh process (the sizes are read once)."""
+    env = dict(os.environ, CORDAHIP_ECDSA_WS_SLOTS=slots, CORDAHIP_ED25519_WS_LANES=slots)
+    r = subprocess.run([sys.executable, "-c", CHUNK_SCRIPT % {"root": ROOT}], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["n"] == 523

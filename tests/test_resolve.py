@@ -206,6 +206,27 @@ def test_idless_transaction_fails_before_recording(oracle):
     assert res.recorded == [] and res.failed == 3 and isinstance(res.error, R.MerkleTreeException)
 
 
+def test_missing_signers_are_a_set_with_descriptions(oracle):
+    """getMissingSignatures is mustSign.filter{..}.toSet() (SignedTransaction.kt:106)
+    and needed = missing - allowed (:79): duplicate mustSign keys appear once, in
+    first-occurrence order; descriptions come from getMissingKeyDescriptions
+    (:114-124): commands with a missing signer, then "notary"."""
+    k = [_ed_pub(oracle, s) for s in SEEDS]
+    eng = OracleEngine(oracle)
+    stx, tid = _issue(oracle, b"dup", signers=(0,), must=[k[2], k[1], k[2], k[0], k[1], k[3]])
+    stx.commands = [("Issue(owner=1)", [k[1]]), ("Move(owner=0)", [k[0]]), ("Exit(owner=2,3)", [k[2], k[3]])]
+    stx.notary = k[3]
+    e = R.verify_signatures_batch(eng, [stx])[0].error
+    assert isinstance(e, R.SignaturesMissingException)
+    assert e.missing == [k[2], k[1], k[3]]  # set semantics, first-occurrence order
+    assert e.descriptions == ["Issue(owner=1)", "Exit(owner=2,3)", "notary"]
+    assert e.id == tid
+    e = R.verify_signatures_batch(eng, [stx], allowed_to_be_missing=[k[2], k[2]])[0].error
+    assert e.missing == [k[1], k[3]] and e.descriptions == ["Issue(owner=1)", "Exit(owner=2,3)", "notary"]
+    e = R.verify_signatures_batch(eng, [stx], allowed_to_be_missing=[k[2], k[3]])[0].error
+    assert e.missing == [k[1]] and e.descriptions == ["Issue(owner=1)"]
+
+
 def test_composite_key_fulfilment(oracle):
     k = [_ed_pub(oracle, s) for s in SEEDS]
     two_of_three = R.CompositeKey(2, ((k[0], 1), (k[1], 1), (k[2], 1)))
