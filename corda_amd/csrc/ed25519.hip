@@ -14,6 +14,10 @@
 //     slide()'s carry drop, the half-size scalars (c0, c1) and e = c1 S_eff,
 //     and the per-lane tables [0..8](-A), [0..8](-R) -> HBM workspace record;
 //   ed25519_ladder_half_kernel (ed25519_ladder.hip): [e]B + [c0](+-A) + [c1](-R) == O.
+// field products in hand-scheduled pairs (ge25519.hpp fe_mul_pair, fe25519_asm.hpp)
+#ifndef FE_USE_ASM2
+#define FE_USE_ASM2 1
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -369,6 +373,40 @@ CDEV bool ge_strict_ok(const ge_p3& R, const uint32_t w[8]) {
 
 CDEV void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8], const uint32_t c[8]);
 
+// an affine point (Z = 1) as X, Y, T (30 words, 16-B aligned slot of 40)
+CDEV void store_point(uint32_t* __restrict__ o, const ge_p3& p) {
+  uint4* o4 = reinterpret_cast<uint4*>(o);
+  uint32_t w[32];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    w[i] = p.X.v[i];
+    w[10 + i] = p.Y.v[i];
+    w[20 + i] = p.T.v[i];
+  }
+  w[30] = w[31] = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+CDEV void load_point(ge_p3& p, const uint32_t* __restrict__ o) {
+  const uint4* o4 = reinterpret_cast<const uint4*>(o);
+  uint32_t w[32];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint4 v = o4[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    p.X.v[i] = w[i];
+    p.Y.v[i] = w[10 + i];
+    p.T.v[i] = w[20 + i];
+  }
+  fe_set(p.Z, 1);
+}
+
 CDEV void store_table9(uint32_t* __restrict__ rec, const ge_p3& base) {
   ge_cached c;
   fe_set(c.YpX, 1);
@@ -411,29 +449,43 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
   uint8_t st = kStatusPending;
   uint32_t abyte[8], Rw[8];
   load8(Rw, reinterpret_cast<const uint32_t*>(sigs + i * 64));
-  // pass 0: A (i2p decode: y not range checked), pass 1: R (strict decode:
-  // encode(R') == Rw only if Rw is a canonical point encoding). One loop body
-  // keeps a single copy of the decompression + table code in the I-cache.
+  {
+    // A (i2p decode: y not range checked) and R (strict decode: encode(R') ==
+    // Rw only if Rw is a canonical point encoding) decompressed together: the
+    // two square-root exponentiations run as interleaved chains
+    uint32_t wa[8];
+    load8(wa, reinterpret_cast<const uint32_t*>(keys + i * 32));
+    ge_p3 A, R;
+    bool okA, okR;
+    ge_frombytes_i2p_pair(A, okA, wa, R, okR, Rw);
+    if (!okA) st = kStatusBadKey;  // key decode precedes doVerify (Kryo.kt:389-392)
+    else if (pre_status && pre_status[i] != kStatusOk) st = pre_status[i];
+    else if (msg_len == 0 && empty_is_error) st = kStatusEmpty;  // doVerify: Crypto.kt:476 (isValid hashes it)
+    fe_tobytes(abyte, A.Y);  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
+    abyte[7] |= fe_isnegative(A.X) << 31;
+    if (st == kStatusPending && !(okR && ge_strict_ok(R, Rw))) st = kStatusBadSig;  // no canonical point encodes to Rw
+    if (st != kStatusPending) {
+      ge_identity(A);
+      ge_identity(R);
+    }
+    // -A, -R parked in the last slot of their table (Z = 1: X, Y, T), so the
+    // table loop below holds one point at a time
+    fe_neg(A.X, A.X);
+    fe_neg(A.T, A.T);
+    fe_neg(R.X, R.X);
+    fe_neg(R.T, R.T);
+    store_point(rec + kWhTabA + 40 * 8, A);
+    store_point(rec + kWhTabR + 40 * 8, R);
+  }
+  PHASE_BARRIER();
+  // tables [k](-A), [k](-R): one loop body keeps a single copy of the table
+  // code in the I-cache
 #pragma unroll 1
   for (int pass = 0; pass < 2; pass++) {
-    uint32_t w[8];
-    if (pass == 0) load8(w, reinterpret_cast<const uint32_t*>(keys + i * 32));
-    else mp8_copy(w, Rw);
+    uint32_t* tab = rec + (pass ? kWhTabR : kWhTabA);
     ge_p3 P;
-    const bool ok = ge_frombytes_i2p(P, w);
-    if (pass == 0) {
-      if (!ok) st = kStatusBadKey;  // key decode precedes doVerify (Kryo.kt:389-392)
-      else if (pre_status && pre_status[i] != kStatusOk) st = pre_status[i];
-      else if (msg_len == 0 && empty_is_error) st = kStatusEmpty;  // doVerify: Crypto.kt:476 (isValid hashes it)
-      fe_tobytes(abyte, P.Y);  // EdDSAPublicKey.Abyte = A.toByteArray(): canonical
-      abyte[7] |= fe_isnegative(P.X) << 31;
-    } else if (st == kStatusPending && !(ok && ge_strict_ok(P, w))) {
-      st = kStatusBadSig;  // no canonical point encodes to Rw
-    }
-    if (st != kStatusPending) ge_identity(P);
-    fe_neg(P.X, P.X);
-    fe_neg(P.T, P.T);
-    store_table9(rec + (pass ? kWhTabR : kWhTabA), P);
+    load_point(P, tab + 40 * 8);  // read before store_table9 overwrites slot 8
+    store_table9(tab, P);
     PHASE_BARRIER();
   }
   uint32_t ka[8], kr[8], e[8];

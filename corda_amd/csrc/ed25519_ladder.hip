@@ -11,6 +11,10 @@
 // B' = [2^128]B from LDS. Digit positions are the same in every lane, so the
 // ladder never diverges; P == O is X == 0 and Y == Z (no inversion).
 // Verdict word per wave by ballot.
+// field products in hand-scheduled pairs (ge25519.hpp fe_mul_pair, fe25519_asm.hpp)
+#ifndef FE_USE_ASM2
+#define FE_USE_ASM2 1
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,7 +42,12 @@ CDEV void lds_niels(ge_niels& n, const uint32_t* lds, int idx) {
   }
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_ladder_half_kernel(
+// waves per SIMD the register allocation targets (2: up to 256 VGPRs)
+#ifndef ED_LADDER_WAVES
+#define ED_LADDER_WAVES 2
+#endif
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_LADDER_WAVES))) ed25519_ladder_half_kernel(
     uint64_t base, uint64_t m, const uint32_t* __restrict__ btab, const uint32_t* __restrict__ ws,
     uint8_t* __restrict__ status, unsigned long long* __restrict__ verdict) {
   __shared__ __attribute__((aligned(16))) uint32_t bl[2 * kBTableEntries * kLdsBStride];
