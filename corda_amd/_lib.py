@@ -31,7 +31,12 @@ EXPORTS = [
     "cordahip_tx_ids", "cordahip_signed_tx_verify", "cordahip_signed_tx_verify_ed25519_device",
     "cordahip_ecdsa_verify_device", "cordahip_stream_verify", "cordahip_filtered_tx_verify",
     "cordahip_tx_submit", "cordahip_txid_submit", "cordahip_filtered_tx_submit", "cordahip_shard_range",
+    "cordahip_kryo_encode",
 ]
+ERR_BUFFER_TOO_SMALL = -8
+# cordahip_kryo_item kinds (CORDAHIP_KRYO_*)
+KRYO_KINDS = {"raw": 0, "char": 1, "short": 2, "int": 3, "long": 4, "byte": 5, "boolean": 6, "float": 7,
+              "double": 8, "String": 9, "ed25519_key": 10, "public_key": 11, "kotlin_object": 12}
 ABI_VERSION = 2
 FLAG_IS_VALID = 1  # CORDAHIP_FLAG_IS_VALID: Crypto.isValid semantics (no emptiness checks)
 TX_NO_LEAVES, TX_NO_SIGNATURES, TX_BAD_TREE = 6, 7, 8
@@ -57,6 +62,13 @@ class SigBatch(ctypes.Structure):
         ("status", ctypes.c_void_p),
         ("verdict", ctypes.c_void_p),
         ("flags", ctypes.c_uint32),
+    ]
+
+
+class KryoItem(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_uint32), ("class_id", ctypes.c_uint32), ("value", ctypes.c_int64),
+        ("data", ctypes.c_void_p), ("len", ctypes.c_uint64),
     ]
 
 
@@ -150,6 +162,7 @@ def lib() -> ctypes.CDLL:
         "cordahip_txid_submit": (i32, [vp, ctypes.POINTER(TxidBatch), ctypes.POINTER(u64)]),
         "cordahip_filtered_tx_submit": (i32, [vp, ctypes.POINTER(FilteredTxBatch), ctypes.POINTER(u64)]),
         "cordahip_shard_range": (None, [u64, u32, u32, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "cordahip_kryo_encode": (i32, [ctypes.POINTER(KryoItem), u64, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(l, name)
@@ -164,6 +177,44 @@ def shard_range(n: int, nshards: int, shard: int, align: int = 64):
     lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
     lib().cordahip_shard_range(n, nshards, shard, align, ctypes.byref(lo), ctypes.byref(hi))
     return lo.value, hi.value
+
+
+def kryo_encode(items):
+    """Leaf preimages of transaction components (cordahip_kryo_encode; host only, no
+    device). items: (kind, value, class_id) with kind a KRYO_KINDS key; value: bytes
+    for raw / keys, str for String / kotlin_object (and char), int otherwise
+    (float / double: their IEEE bits). Returns the list of leaves (bytes)."""
+    import numpy as np
+    n = len(items)
+    arr = (KryoItem * max(n, 1))()
+    keep = []
+    for i, (kind, value, class_id) in enumerate(items):
+        it = arr[i]
+        it.kind, it.class_id = KRYO_KINDS[kind], class_id
+        if kind in ("String", "kotlin_object"):
+            b = value.encode("utf-16-le")
+            it.len = len(b) // 2
+        elif kind in ("raw", "ed25519_key", "public_key"):
+            b = bytes(value)
+            it.len = len(b)
+        else:
+            b = None
+            it.value = ord(value) if (kind == "char" and isinstance(value, str)) else int(value)
+        if b is not None:
+            buf = ctypes.create_string_buffer(b, max(len(b), 1))
+            keep.append(buf)
+            it.data = ctypes.addressof(buf)
+    off = np.zeros(n + 1, np.uint64)
+    cap = 0
+    rc = lib().cordahip_kryo_encode(arr, n, None, 0, off.ctypes.data)
+    if rc == ERR_BUFFER_TOO_SMALL:
+        cap = int(off[n])
+        out = np.zeros(cap, np.uint8)
+        rc = lib().cordahip_kryo_encode(arr, n, out.ctypes.data, cap, off.ctypes.data)
+    else:
+        out = np.zeros(1, np.uint8)
+    check(rc, "cordahip_kryo_encode")
+    return [out[int(off[i]):int(off[i + 1])].tobytes() for i in range(n)]
 
 
 def strerror(code: int) -> str:

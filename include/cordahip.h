@@ -65,6 +65,7 @@ extern "C" {
 #define CORDAHIP_ERR_TIMEOUT (-5)
 #define CORDAHIP_ERR_UNKNOWN_TICKET (-6)
 #define CORDAHIP_ERR_NOT_IMPLEMENTED (-7)
+/* -8 CORDAHIP_ERR_BUFFER_TOO_SMALL: see cordahip_kryo_encode */
 
 /* ---- signature schemes = Corda SignatureScheme.schemeNumberID ------------ */
 #define CORDAHIP_SCHEME_RSA_SHA256 1             /* Crypto.kt:77  (not on GPU -> UNSUPPORTED lane) */
@@ -267,6 +268,60 @@ typedef struct {
 } cordahip_filtered_tx_batch;
 int cordahip_filtered_tx_verify(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch);
 int cordahip_filtered_tx_submit(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch, uint64_t* ticket);
+
+/* ---- native Kryo leaf encoder ------------------------- *
+ * The Merkle leaf of a transaction component is SHA-256 of its p2p Kryo bytes:
+ *   serializedHash(x) = p2PKryo().withoutReferences { x.serialize(kryo).hash }
+ *       core/.../transactions/MerkleTransaction.kt:16-18
+ *   serialize = "corda\0\0\1" header + kryo.writeClassAndObject(x)
+ *       core/.../serialization/Kryo.kt:101,165-176
+ * cordahip_kryo_encode writes those preimages natively (no JVM re-serialisation)
+ * for the component kinds whose wire form is fixed by Kryo 4.0.0's published
+ * format plus Corda's own serializers; any other component travels as a RAW,
+ * already-serialised leaf. Output is the leaf CSR cordahip_tx_ids consumes.
+ * Kinds and their bytes after the header (varint = Kryo writeVarInt(x, true)):
+ *   RAW            data[len] copied verbatim (a complete leaf, header included)
+ *   CHAR/SHORT/INT/LONG/BYTE/BOOLEAN/FLOAT/DOUBLE  (boxed primitive, Kryo's
+ *                  default registrations 5/6/0/7/4/3/2/8): varint(id + 2), then
+ *                  the value big-endian in 2/2/4/8/1/1/4/8 bytes (value: bits)
+ *   STRING         varint(1 + 2), Output.writeString of the UTF-16 code units
+ *                  data[0..2*len) (little-endian u16): ASCII form for 2..63 ASCII
+ *                  chars, else UTF-8 length + modified UTF-8
+ *   ED25519_KEY    varint(class_id + 2), varint(32), A (Ed25519PublicKeySerializer,
+ *                  Kryo.kt:383-393); data = the 32-byte A
+ *   PUBLIC_KEY     varint(class_id + 2), varint(len), key.encoded (PublicKeySerializer,
+ *                  Kryo.kt:441-451, BCEC/BCRSA/SPHINCS keys); data = X.509 SPKI DER
+ *   KOTLIN_OBJECT  varint(NAME + 2 = 1), varint(name id 0), writeString(class
+ *                  name) and no body (CordaClassResolver.registerImplicit's
+ *                  KotlinObjectSerializer, CordaClassResolver.kt:76-99), e.g.
+ *                  "net.corda.core.contracts.TransactionType$General"; data =
+ *                  the class name as UTF-16 code units (len = chars)
+ * class_id = kryo.getRegistration(cls).id on the node (registration order of
+ * DefaultKryoCustomizer.kt is fixed per build; the JVM reads it once).
+ * off[0..n] receives the CSR offsets; returns CORDAHIP_ERR_BUFFER_TOO_SMALL with
+ * off[n] = the bytes needed when cap is too small. Host-only: no device work. */
+#define CORDAHIP_ERR_BUFFER_TOO_SMALL (-8)
+#define CORDAHIP_KRYO_RAW 0
+#define CORDAHIP_KRYO_CHAR 1
+#define CORDAHIP_KRYO_SHORT 2
+#define CORDAHIP_KRYO_INT 3
+#define CORDAHIP_KRYO_LONG 4
+#define CORDAHIP_KRYO_BYTE 5
+#define CORDAHIP_KRYO_BOOLEAN 6
+#define CORDAHIP_KRYO_FLOAT 7
+#define CORDAHIP_KRYO_DOUBLE 8
+#define CORDAHIP_KRYO_STRING 9
+#define CORDAHIP_KRYO_ED25519_KEY 10
+#define CORDAHIP_KRYO_PUBLIC_KEY 11
+#define CORDAHIP_KRYO_KOTLIN_OBJECT 12
+typedef struct {
+  uint32_t kind;       /* CORDAHIP_KRYO_* */
+  uint32_t class_id;   /* Kryo registration id (ED25519_KEY, PUBLIC_KEY) */
+  int64_t value;       /* primitive kinds: the value (FLOAT / DOUBLE: the IEEE bits) */
+  const uint8_t* data; /* RAW / STRING / key / class-name payload */
+  uint64_t len;        /* bytes (RAW, keys) or UTF-16 code units (STRING, KOTLIN_OBJECT) */
+} cordahip_kryo_item;
+int cordahip_kryo_encode(const cordahip_kryo_item* items, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* off);
 
 /* Device time (ms) of the calling thread's most recent *_device call on
  * `device`, from HIP events recorded around its launches on the stream it ran

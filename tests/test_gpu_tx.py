@@ -130,3 +130,33 @@ def test_leaf_sha256_every_length_and_alignment(engine):
     assert (st == 0).all()
     for t, tx in enumerate(txs):
         assert bytes(ids[t]) == hashlib.sha256(tx[0]).digest(), (t, len(tx[0]))
+
+
+def test_kryo_leaves_feed_tx_ids(engine, oracle):
+    """§8f rank 4: leaves made by the native Kryo encoder (cordahip_kryo_encode)
+    go straight into cordahip_tx_ids. The char leaves of PartialMerkleTreeTest.kt:22-25
+    give the derived fixture's ids; mixed transactions (native mustSign-key and
+    TransactionType leaves beside RAW JVM-serialised ones) match the oracle's id
+    over the same bytes (the native leaf bytes themselves: PARITY UNPINNED beyond
+    the char fixture, tests/test_kryo.py)."""
+    from corda_amd import _lib
+    import kryo_leaves as K
+    fixture = {t["name"]: t for t in _golden_txs()}
+    txs = [_lib.kryo_encode([("char", c, 0) for c in "abcdef"]), _lib.kryo_encode([("char", "a", 0)]),
+           _lib.kryo_encode([("char", c, 0) for c in "abc"])]
+    rng = random.Random(3)
+    for t in range(20):
+        items = [("raw", b"corda\x00\x00\x01" + bytes(rng.getrandbits(8) for _ in range(n)), 0) for n in (440, 140)]
+        items += [("ed25519_key", bytes(rng.getrandbits(8) for _ in range(32)), 71) for _ in range(t % 3 + 1)]
+        items.append(("kotlin_object", K.TRANSACTION_TYPE_GENERAL, 0))
+        txs.append(_lib.kryo_encode(items))
+    ids, st = engine.tx_ids(txs)
+    assert (st == 0).all()
+    assert [i.tobytes().hex() for i in ids[:3]] == [fixture[n]["id"] for n in ("ref_abcdef", "ref_one", "ref_three")]
+    out = ctypes.create_string_buffer(32)
+    for tx, i in zip(txs[3:], ids[3:]):
+        blob = np.frombuffer(b"".join(tx), np.uint8).copy()
+        off = np.zeros(len(tx) + 1, np.uint64)
+        off[1:] = np.cumsum([len(x) for x in tx])
+        assert oracle.oracle_tx_id(blob.ctypes.data, off.ctypes.data, len(tx), out) == 0
+        assert out.raw == i.tobytes()

@@ -1,0 +1,94 @@
+"""Native Kryo leaf encoder (cordahip_kryo_encode) on the CPU:
+the library's host-side encoder against the independent Python restatement of
+Kryo 4.0.0's wire format (oracle/kryo_leaves.py), and against the derived leaf
+fixture of PartialMerkleTreeTest.kt:22-25 ('a'..'f'.serialize(), the leaves
+of tests/golden/merkle_vectors.json "ref_*"). Everything beyond the char
+fixture is PARITY UNPINNED (no Kryo / JVM in this image): the bytes follow the
+published format and Corda's serializers, unconfirmed by a reference output.
+The GPU half (leaves -> cordahip_tx_ids -> the fixture's tx id) is in
+tests/test_gpu_tx.py::test_kryo_leaves_feed_tx_ids."""
+import json
+import os
+import random
+import struct
+
+import pytest
+
+import kryo_leaves as K
+from corda_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_char_leaves_match_the_derived_fixture():
+    fixture = {t["name"]: t for t in json.load(open(os.path.join(ROOT, "tests", "golden", "merkle_vectors.json")))["txs"]}
+    leaves = _lib.kryo_encode([("char", c, 0) for c in "abcdef"])
+    assert [x.hex() for x in leaves] == fixture["ref_abcdef"]["leaves"]
+    assert [x.hex() for x in _lib.kryo_encode([("char", "a", 0)])] == fixture["ref_one"]["leaves"]
+    assert leaves[0] == b"corda\x00\x00\x01\x07\x00a"  # header, char registration 5 + 2, 'a' big-endian
+
+
+def _random_items(rng):
+    items = []
+    strings = ["", "x", "ab", "a" * 63, "a" * 64, "b" * 200, "café", "€100", "😀 ok",
+               "\u0000\u007f", "MEGA_CORP", "O=Bank A,L=London,C=GB"]
+    for _ in range(400):
+        k = rng.choice(["char", "short", "int", "long", "byte", "boolean", "float", "double", "String",
+                        "ed25519_key", "public_key", "kotlin_object", "raw"])
+        if k == "char":
+            items.append((k, rng.randrange(0, 0x10000), 0))
+        elif k == "short":
+            items.append((k, rng.randrange(-2**15, 2**15), 0))
+        elif k == "int":
+            items.append((k, rng.randrange(-2**31, 2**31), 0))
+        elif k == "long":
+            items.append((k, rng.randrange(-2**63, 2**63), 0))
+        elif k == "byte":
+            items.append((k, rng.randrange(-128, 128), 0))
+        elif k == "boolean":
+            items.append((k, rng.randrange(2), 0))
+        elif k in ("float", "double"):
+            items.append((k, rng.uniform(-1e6, 1e6), 0))
+        elif k == "String":
+            items.append((k, rng.choice(strings) + "".join(chr(rng.randrange(32, 0x3000)) for _ in range(rng.randrange(0, 5))), 0))
+        elif k == "ed25519_key":
+            items.append((k, bytes(rng.getrandbits(8) for _ in range(32)), rng.randrange(0, 300)))
+        elif k == "public_key":
+            items.append((k, bytes(rng.getrandbits(8) for _ in range(rng.choice((88, 91, 294)))), rng.randrange(0, 300)))
+        elif k == "kotlin_object":
+            items.append((k, rng.choice([K.TRANSACTION_TYPE_GENERAL, "net.corda.core.contracts.TransactionType$NotaryChange",
+                                         "x", "y" * 70]), 0))
+        else:
+            items.append((k, bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 100))), 0))
+    return items
+
+
+def test_encoder_matches_python_restatement():
+    rng = random.Random(8)
+    items = _random_items(rng)
+    got = _lib.kryo_encode([(k, (struct.unpack(">i", struct.pack(">f", v))[0] if k == "float" else
+                                 struct.unpack(">q", struct.pack(">d", v))[0] if k == "double" else v), c)
+                            for k, v, c in items])
+    for (k, v, c), g in zip(items, got):
+        want = K.leaf(k, v, c)
+        assert g == want, (k, v, c, g.hex(), want.hex())
+
+
+def test_known_shapes():
+    gen = _lib.kryo_encode([("kotlin_object", K.TRANSACTION_TYPE_GENERAL, 0)])[0]
+    name = K.TRANSACTION_TYPE_GENERAL.encode()
+    assert gen == b"corda\x00\x00\x01" + b"\x01\x00" + name[:-1] + bytes([name[-1] | 0x80])
+    key = bytes(range(32))
+    assert _lib.kryo_encode([("ed25519_key", key, 77)])[0] == b"corda\x00\x00\x01" + bytes([79, 32]) + key
+    assert _lib.kryo_encode([("ed25519_key", key, 200)])[0][8:10] == bytes([0xCA, 0x01])  # varint(202)
+    assert _lib.kryo_encode([("String", "", 0), ("String", "a", 0), ("String", "ab", 0)]) == [
+        b"corda\x00\x00\x01\x03\x81", b"corda\x00\x00\x01\x03\x82a", b"corda\x00\x00\x01\x03a\xe2"]
+    assert _lib.kryo_encode([("int", 1, 0), ("long", -1, 0)]) == [
+        b"corda\x00\x00\x01\x02\x00\x00\x00\x01", b"corda\x00\x00\x01\x09" + b"\xff" * 8]
+
+
+def test_bad_items_are_rejected():
+    with pytest.raises(_lib.EngineError):
+        _lib.kryo_encode([("ed25519_key", b"short", 3)])
+    with pytest.raises(_lib.EngineError):
+        _lib.kryo_encode([("public_key", b"", 3)])
