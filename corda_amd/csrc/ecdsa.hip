@@ -26,6 +26,7 @@
 
 #include "der.hpp"
 #include "fp29.hpp"
+#include "fp29_asm.hpp"
 #include "fp29_consts.hpp"
 #include "mp256.hpp"
 #include "sc25519.hpp"
@@ -118,10 +119,60 @@ struct jpt {
   bool inf;
 };
 
+// Two independent field products. EC_USE_ASM2 (default): one generated asm
+// block per pair (fp29_asm.hpp, tools/gen_fp29_asm.py), bit-identical to two
+// f29_mul / f29_sqr calls; results may alias any operand. Only kernels with a
+// >= 164-VGPR budget (amdgpu_waves_per_eu(2) or fewer waves) may use them: the
+// asm's column accumulators are v160..v163.
+#ifndef EC_USE_ASM2
+#define EC_USE_ASM2 1
+#endif
+template <class F>
+CDEV void f29_mul_pair(f29& r0, const f29& a0, const f29& b0, f29& r1, const f29& a1, const f29& b1) {
+#if EC_USE_ASM2
+  if constexpr (F::kRed == 1) f29a_mul_mul_k1(r0, a0, b0, r1, a1, b1);
+  else f29a_mul_mul_r1(r0, a0, b0, r1, a1, b1);
+#else
+  f29 t0, t1;
+  f29_mul<F>(t0, a0, b0);
+  f29_mul<F>(t1, a1, b1);
+  r0 = t0;
+  r1 = t1;
+#endif
+}
+template <class F>
+CDEV void f29_sqr_pair(f29& r0, const f29& a0, f29& r1, const f29& a1) {
+#if EC_USE_ASM2
+  if constexpr (F::kRed == 1) f29a_sqr_sqr_k1(r0, a0, r1, a1);
+  else f29a_sqr_sqr_r1(r0, a0, r1, a1);
+#else
+  f29 t0, t1;
+  f29_sqr<F>(t0, a0);
+  f29_sqr<F>(t1, a1);
+  r0 = t0;
+  r1 = t1;
+#endif
+}
+template <class F>  // r0 = a0^2, r1 = a1 b1
+CDEV void f29_sqr_mul_pair(f29& r0, const f29& a0, f29& r1, const f29& a1, const f29& b1) {
+#if EC_USE_ASM2
+  if constexpr (F::kRed == 1) f29a_sqr_mul_k1(r0, a0, r1, a1, b1);
+  else f29a_sqr_mul_r1(r0, a0, r1, a1, b1);
+#else
+  f29 t0, t1;
+  f29_sqr<F>(t0, a0);
+  f29_mul<F>(t1, a1, b1);
+  r0 = t0;
+  r1 = t1;
+#endif
+}
+
 // 2P. a = -3: dbl-2001-b (3M + 5S); a = 0: dbl-2009-l (2M + 5S). Prime-order
 // curves have no 2-torsion, so only the point at infinity is exceptional.
 // Every f29_sub / f29_red below respects fp29.hpp's operand bounds (value
 // bounds in units of p in the comments; modelled in tests/test_fp29_model.py).
+// Independent products are issued in pairs (same operands as the formulas'
+// sequential statement, so the results are unchanged).
 template <class C>
 CDEV void jdbl(jpt& r, const jpt& p) {
   using F = typename C::F;
@@ -131,42 +182,36 @@ CDEV void jdbl(jpt& r, const jpt& p) {
   }
   f29 x3, y3, z3, t, u;
   if constexpr (C::kAm3) {
-    f29 delta, gamma, beta, a3, b4;
-    f29_sqr<F>(delta, p.Z);
-    f29_sqr<F>(gamma, p.Y);
-    f29_mul<F>(beta, p.X, gamma);
+    f29 delta, gamma, beta, a3, b4, yz;
+    f29_sqr_pair<F>(delta, p.Z, gamma, p.Y);
     f29_sub<F>(t, p.X, delta);  // < 4p
     f29_add(u, p.X, delta);     // < 4p
-    f29_mul<F>(a3, t, u);
+    f29_mul_pair<F>(beta, p.X, gamma, a3, t, u);
     f29_add(t, a3, a3);
     f29_add(t, t, a3);
     f29_red<F>(a3, t);          // alpha = 3 (X - delta)(X + delta)
-    f29_sqr<F>(x3, a3);
     f29_add(t, beta, beta);
     f29_add(t, t, t);
     f29_red<F>(b4, t);          // 4 beta
+    f29_add(yz, p.Y, p.Z);
+    f29_sqr_pair<F>(x3, a3, yz, yz);
     f29_sub<F>(x3, x3, b4);
     f29_sub<F>(t, x3, b4);      // < 6p
     f29_red<F>(x3, t);          // X3 = alpha^2 - 8 beta
-    f29_add(t, p.Y, p.Z);
-    f29_sqr<F>(t, t);
-    f29_sub<F>(t, t, gamma);
+    f29_sub<F>(t, yz, gamma);
     f29_sub<F>(t, t, delta);
     f29_red<F>(z3, t);          // Z3 = (Y + Z)^2 - gamma - delta
     f29_sub<F>(u, b4, x3);
-    f29_mul<F>(y3, a3, u);
     f29_add(t, gamma, gamma);
-    f29_sqr<F>(u, t);           // 4 gamma^2
-    f29_sub<F>(y3, y3, u);
-    f29_sub<F>(t, y3, u);
-    f29_red<F>(y3, t);          // Y3 = alpha (4 beta - X3) - 8 gamma^2
+    f29_sqr_mul_pair<F>(t, t, y3, a3, u);  // 4 gamma^2, alpha (4 beta - X3)
+    f29_sub<F>(y3, y3, t);
+    f29_sub<F>(u, y3, t);
+    f29_red<F>(y3, u);          // Y3 = alpha (4 beta - X3) - 8 gamma^2
   } else {
     f29 A, B, Cc, D, E;
-    f29_sqr<F>(A, p.X);
-    f29_sqr<F>(B, p.Y);
-    f29_sqr<F>(Cc, B);
+    f29_sqr_pair<F>(A, p.X, B, p.Y);
     f29_add(t, p.X, B);
-    f29_sqr<F>(t, t);
+    f29_sqr_pair<F>(Cc, B, t, t);
     f29_sub<F>(t, t, A);
     f29_sub<F>(t, t, Cc);       // < 6p
     f29_add(t, t, t);           // < 12p
@@ -174,7 +219,8 @@ CDEV void jdbl(jpt& r, const jpt& p) {
     f29_add(t, A, A);
     f29_add(t, t, A);
     f29_red<F>(E, t);           // E = 3 A
-    f29_sqr<F>(x3, E);
+    f29_add(t, p.Y, p.Y);
+    f29_sqr_mul_pair<F>(x3, E, z3, t, p.Z);  // E^2, Z3 = 2 Y Z
     f29_sub<F>(x3, x3, D);
     f29_sub<F>(t, x3, D);
     f29_red<F>(x3, t);          // X3 = E^2 - 2 D
@@ -186,8 +232,6 @@ CDEV void jdbl(jpt& r, const jpt& p) {
     f29_sub<F>(y3, y3, u);
     f29_sub<F>(t, y3, u);
     f29_red<F>(y3, t);          // Y3 = E (D - X3) - 8 C
-    f29_add(t, p.Y, p.Y);
-    f29_mul<F>(z3, t, p.Z);     // Z3 = 2 Y Z
   }
   r.X = x3;
   r.Y = y3;
@@ -256,7 +300,7 @@ CDEV void jadd(jpt& r, const jpt& p, const jpt& q) {
   r.inf = false;
 }
 
-// P + (x2, y2) affine (madd-2007-bl, 7M + 4S)
+// P + (x2, y2) affine (madd-2007-bl, 7M + 4S), products paired as in jdbl
 template <class C>
 CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
   using F = typename C::F;
@@ -268,10 +312,8 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
     return;
   }
   f29 z1z1, u2, s2, h, hh, i, j, rr, v, t, x3, y3, z3;
-  f29_sqr<F>(z1z1, p.Z);
-  f29_mul<F>(u2, x2, z1z1);
-  f29_mul<F>(t, y2, p.Z);
-  f29_mul<F>(s2, t, z1z1);
+  f29_sqr_mul_pair<F>(z1z1, p.Z, t, y2, p.Z);
+  f29_mul_pair<F>(u2, x2, z1z1, s2, t, z1z1);
   f29_sub<F>(t, u2, p.X);
   f29_red<F>(h, t);
   f29_sub<F>(t, s2, p.Y);
@@ -284,20 +326,17 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
     }
     return;
   }
-  f29_sqr<F>(hh, h);
+  f29_add(rr, rr, rr);
+  f29_sqr_pair<F>(hh, h, x3, rr);
   f29_add(i, hh, hh);
   f29_add(i, i, i);             // I = 4 HH, < 8p
-  f29_mul<F>(j, h, i);
-  f29_add(rr, rr, rr);
-  f29_mul<F>(v, p.X, i);
-  f29_sqr<F>(x3, rr);
+  f29_mul_pair<F>(j, h, i, v, p.X, i);
   f29_sub<F>(x3, x3, j);
   f29_sub<F>(x3, x3, v);
   f29_sub<F>(t, x3, v);
   f29_red<F>(x3, t);
   f29_sub<F>(t, v, x3);
-  f29_mul<F>(y3, rr, t);
-  f29_mul<F>(t, p.Y, j);
+  f29_mul_pair<F>(y3, rr, t, t, p.Y, j);
   f29_sub<F>(y3, y3, t);
   f29_sub<F>(y3, y3, t);
   f29_red<F>(y3, y3);
@@ -1134,17 +1173,16 @@ CDEV void ecdsa_affine_lane(uint32_t* __restrict__ rec) {
   for (int k = 8; k >= 2; k--) {
     f29 zi, z;
     if (k > 2) {
-      f29_mul<F>(zi, inv, pre[k - 3]);  // Z_k^-1
       ld_slot_z(z, tab + kEcPtWords * (k - 1));
-      f29_mul<F>(inv, inv, z);          // (Z_2 ... Z_{k-1})^-1
+      // Z_k^-1, (Z_2 ... Z_{k-1})^-1
+      f29_mul_pair<F>(zi, inv, pre[k - 3], inv, inv, z);
     } else {
       zi = inv;
     }
     f29 z2, z3, x, y;
     ld_aff(x, y, tab + kEcPtWords * (k - 1));
     f29_sqr<F>(z2, zi);
-    f29_mul<F>(z3, z2, zi);
-    f29_mul<F>(x, x, z2);
+    f29_mul_pair<F>(z3, z2, zi, x, x, z2);
     f29_mul<F>(y, y, z3);
     uint32_t w[20];
 #pragma unroll

@@ -1,0 +1,148 @@
+"""CPU check of the generated paired Montgomery products (corda_amd/csrc/fp29_asm.hpp).
+
+The header is emulated instruction by instruction (v_mad_u64_u32, v_mul_lo_u32,
+v_and_b32, v_lshrrev_b64, v_lshlrev_b32, v_mov_b32 on 32/64-bit registers) for
+random operands within f29_mul's bounds and compared with a restatement of
+fp29.hpp's product-scanning f29_mul / f29_sqr (and with a b R^-1 mod p). The
+GPU-side bit-identity check is tools/microbench/fp29_asm_check.hip.
+"""
+import os
+import random
+import re
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "corda_amd", "csrc", "fp29_asm.hpp")
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import gen_fp29_asm  # noqa: E402
+
+M64 = (1 << 64) - 1
+M32 = (1 << 32) - 1
+M29 = (1 << 29) - 1
+
+
+def parse_header(text):
+    """{function name: (asm lines, {operand name: C expression or int})}"""
+    funcs = {}
+    for m in re.finditer(r"CDEV void (f29a_\w+)\(.*?\n  asm\(\n(.*?)\n      : (.*?)\n      : (.*?)\n      : ", text, re.S):
+        name, body, outs, ins = m.groups()
+        lines = [l.strip()[1:-3] for l in body.split("\n")]
+        ops = {}
+        for o in re.finditer(r'\[(\w+)\] "=?&?([vs])"\(([^)]*)\)', outs + "," + ins):
+            expr = o.group(3)
+            ops[o.group(1)] = int(expr.rstrip("u")) if expr[0].isdigit() else expr
+        funcs[name] = (lines, ops)
+    return funcs
+
+
+def emulate(lines, ops, a, b):
+    """Run one asm body; a/b: {0: limbs, 1: limbs}; returns (r0 limbs, r1 limbs)."""
+    vals = {}
+    for n, e in ops.items():
+        if isinstance(e, int):
+            vals[n] = e
+            continue
+        mm = re.fullmatch(r"([ab])([01])\.v\[(\d)\]", e)
+        if mm:
+            vals[n] = (a if mm.group(1) == "a" else b)[int(mm.group(2))][int(mm.group(3))]
+    acc = {"v[160:161]": 0, "v[162:163]": 0}
+
+    def val(x):
+        x = x.strip()
+        if x.startswith("%["):
+            return vals[x[2:-1]]
+        if x in acc:
+            return acc[x]
+        if x in ("v160", "v162"):
+            return acc["v[%s:%d]" % (x[1:], int(x[1:]) + 1)] & M32
+        return int(x, 0)
+
+    def dst(x):
+        assert x.startswith("%["), x
+        return x[2:-1]
+
+    for line in lines:
+        op, rest = line.split(" ", 1)
+        x = [t.strip() for t in rest.split(",")]
+        if op == "v_mad_u64_u32":
+            assert x[1] == "vcc"
+            acc[x[0]] = (val(x[2]) * val(x[3]) + val(x[4])) & M64
+        elif op == "v_mul_lo_u32":
+            vals[dst(x[0])] = (val(x[1]) * val(x[2])) & M32
+        elif op == "v_and_b32":
+            vals[dst(x[0])] = val(x[1]) & val(x[2])
+        elif op == "v_lshrrev_b64":
+            acc[x[0]] = val(x[2]) >> int(x[1])
+        elif op == "v_lshlrev_b32":
+            vals[dst(x[0])] = (val(x[2]) << int(x[1])) & M32
+        elif op == "v_mov_b32":
+            vals[dst(x[0])] = val(x[1])
+        else:
+            raise AssertionError("unexpected instruction " + op)
+    out = []
+    for p in range(2):
+        out.append([vals["t%d_%d" % (k, p)] for k in range(9)])
+    return out
+
+
+def f29_mul_model(curve, a, b):
+    """fp29.hpp f29_mul (f29_sqr computes the same sum with doubled cross terms)."""
+    m, minv = gen_fp29_asm.CURVES[curve]
+    acc, q, t = 0, [0] * 9, [0] * 9
+    for k in range(9):
+        for j in range(k):
+            acc += a[j] * b[k - j] + q[j] * m[k - j]
+        acc += a[k] * b[0]
+        q[k] = (((acc & M32) * (minv or 1)) & M32) & M29
+        acc += q[k] * m[0]
+        assert acc < 1 << 64
+        acc >>= 29
+    for k in range(9, 17):
+        for j in range(k - 8, 9):
+            acc += a[j] * b[k - j] + q[j] * m[k - j]
+        assert acc < 1 << 64
+        t[k - 9] = acc & M29
+        acc >>= 29
+    t[8] = acc & M32
+    return t
+
+
+def value(limbs):
+    return sum(x << (29 * i) for i, x in enumerate(limbs))
+
+
+def test_header_is_generated():
+    with open(HDR) as f:
+        assert f.read() == gen_fp29_asm.render(), "re-run tools/gen_fp29_asm.py"
+
+
+@pytest.mark.parametrize("curve", ["k1", "r1"])
+@pytest.mark.parametrize("shape", ["mul_mul", "sqr_sqr", "sqr_mul"])
+def test_pairs_match_f29_mul(curve, shape):
+    with open(HDR) as f:
+        funcs = parse_header(f.read())
+    lines, ops = funcs["f29a_%s_%s" % (shape, curve)]
+    kinds = shape.split("_")
+    m, _ = gen_fp29_asm.CURVES[curve]
+    p = value(m)
+    rinv = pow(2, -261, p)
+    rng = random.Random(hash((curve, shape)) & 0xffff)
+
+    def rnd():  # < 2^257 (< 4p): within f29_mul's operand bounds
+        return [rng.getrandbits(29) for _ in range(8)] + [rng.getrandbits(25)]
+
+    edge = [[M29] * 8 + [(1 << 25) - 1], [0] * 9, [1] + [0] * 8]
+    for it in range(60):
+        a = {0: edge[it] if it < 3 else rnd(), 1: rnd()}
+        b = {0: rnd(), 1: edge[it] if it < 3 else rnd()}
+        for q in range(2):
+            if kinds[q] == "sqr":
+                b[q] = a[q]
+        got = emulate(lines, ops, a, b)
+        for q in range(2):
+            want = f29_mul_model(curve, a[q], b[q])
+            assert got[q] == want
+            assert value(want) % p == value(a[q]) * value(b[q]) * rinv % p
+            assert value(want) < 2 * p

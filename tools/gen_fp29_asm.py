@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Generate corda_amd/csrc/fp29_asm.hpp: radix-2^29 Montgomery products
+(fp29.hpp f29_mul / f29_sqr, R = 2^261) of TWO independent operand pairs as one
+gfx950 inline-asm block, per curve (secp256k1 "k1", P-256 "r1") and per pair
+shape (mul+mul, sqr+sqr, sqr+mul).
+
+Same reason as tools/gen_fe_asm.py: product scanning keeps ONE running 64-bit
+accumulator per product (column k's sum continues from column k-1's, shifted
+right by 29), which LLVM re-associates at a cost of one 64-bit add per column
+(17 per product); here the accumulator is the v_mad_u64_u32 addend throughout
+and the two products' chains are interleaved instruction by instruction.
+
+The terms, their order and every mask, shift and q computation are exactly
+fp29.hpp's, so the results are bit-identical (tools/microbench/fp29_asm_check.hip
+compares them on the GPU). Modulus limbs are SGPR operands (zero limbs skipped,
+as in fp29.hpp); secp256k1 computes q = (acc * kMinv) mod 2^29, P-256 (kMinv = 1)
+q = acc mod 2^29.
+
+Run: python3 tools/gen_fp29_asm.py  (rewrites the header)
+"""
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "corda_amd", "csrc", "fp29_asm.hpp")
+M29 = "0x1fffffff"
+ACC = ("v[160:161]", "v[162:163]")
+ACC_LO = ("v160", "v162")
+
+CURVES = {
+    # p limbs (radix 2^29), -p^-1 mod 2^29 (None: 1)
+    "k1": ([0x1ffffc2f, 0x1ffffff7, 0x1fffffff, 0x1fffffff, 0x1fffffff, 0x1fffffff, 0x1fffffff, 0x1fffffff,
+            0x00ffffff], 0x12253531),
+    "r1": ([0x1fffffff, 0x1fffffff, 0x1fffffff, 0x000001ff, 0x00000000, 0x00000000, 0x00040000, 0x1fe00000,
+            0x00ffffff], None),
+}
+
+
+def product_terms(kind):
+    """fp29.hpp's instruction order for one product: a list of steps per column.
+    Steps: ('mad', a, b) | ('madq', j, i) (q_j * m_i) | ('q', k) | ('shift',) | ('out', k)."""
+    cols = []
+    for k in range(17):
+        st = []
+        if k < 9:
+            if kind == "mul":
+                for j in range(k):
+                    st.append(("mad", "a%d" % j, "b%d" % (k - j)))
+                    st.append(("madq", j, k - j))
+                st.append(("mad", "a%d" % k, "b0"))
+            else:
+                for j in range(k):
+                    if 2 * j < k:
+                        st.append(("mad", "a2_%d" % j, "a%d" % (k - j)))
+                if k % 2 == 0:
+                    st.append(("mad", "a%d" % (k // 2), "a%d" % (k // 2)))
+                for j in range(k):
+                    st.append(("madq", j, k - j))
+            st.append(("q", k))
+            st.append(("madq", k, 0))
+            st.append(("shift",))
+        else:
+            if kind == "mul":
+                for j in range(k - 8, 9):
+                    st.append(("mad", "a%d" % j, "b%d" % (k - j)))
+                    st.append(("madq", j, k - j))
+            else:
+                for j in range(k - 8, 9):
+                    if 2 * j < k:
+                        st.append(("mad", "a2_%d" % j, "a%d" % (k - j)))
+                if k % 2 == 0:
+                    st.append(("mad", "a%d" % (k // 2), "a%d" % (k // 2)))
+                for j in range(k - 8, 9):
+                    st.append(("madq", j, k - j))
+            st.append(("out", k - 9))
+            st.append(("shift",))
+        cols.append(st)
+    cols.append([("top",)])
+    return cols
+
+
+def expand(kind, p, curve):
+    """Asm lines of one product p (0/1) as a list of per-column instruction lists."""
+    m, minv = CURVES[curve]
+    cols = []
+    for st in product_terms(kind):
+        lines = []
+        for s in st:
+            if s[0] == "mad":
+                lines.append(("dep", "v_mad_u64_u32 %s, vcc, %%[%s_%d], %%[%s_%d], %s" % (ACC[p], s[1], p, s[2], p, ACC[p])))
+            elif s[0] == "madq":
+                j, i = s[1], s[2]
+                if m[i] == 0:
+                    continue
+                lines.append(("dep", "v_mad_u64_u32 %s, vcc, %%[q%d_%d], %%[m%d], %s" % (ACC[p], j, p, i, ACC[p])))
+            elif s[0] == "q":
+                k = s[1]
+                if minv is None:
+                    lines.append(("dep", "v_and_b32 %%[q%d_%d], %s, %s" % (k, p, M29, ACC_LO[p])))
+                else:
+                    lines.append(("dep", "v_mul_lo_u32 %%[q%d_%d], %s, %%[minv]" % (k, p, ACC_LO[p])))
+                    lines.append(("dep", "v_and_b32 %%[q%d_%d], %s, %%[q%d_%d]" % (k, p, M29, k, p)))
+            elif s[0] == "shift":
+                lines.append(("dep", "v_lshrrev_b64 %s, 29, %s" % (ACC[p], ACC[p])))
+            elif s[0] == "out":
+                lines.append(("dep", "v_and_b32 %%[t%d_%d], %s, %s" % (s[1], p, M29, ACC_LO[p])))
+            elif s[0] == "top":
+                lines.append(("dep", "v_mov_b32 %%[t8_%d], %s" % (p, ACC_LO[p])))
+        cols.append([l for _, l in lines])
+    return cols
+
+
+def interleave(c0, c1):
+    """Alternate the two products' instruction streams, column by column."""
+    out = []
+    for a, b in zip(c0, c1):
+        n = max(len(a), len(b))
+        for i in range(n):
+            if i < len(a):
+                out.append(a[i])
+            if i < len(b):
+                out.append(b[i])
+    return out
+
+
+def gen(curve, kinds):
+    m, minv = CURVES[curve]
+    lines = []
+    # the first column of each product starts from 0: rewrite its first mad's addend
+    per = []
+    for p, kind in enumerate(kinds):
+        cols = expand(kind, p, curve)
+        first = cols[0][0]
+        cols[0][0] = first[: first.rfind(",")] + ", 0"
+        if kind == "sqr":
+            cols[0] = ["v_lshlrev_b32 %%[a2_%d_%d], 1, %%[a%d_%d]" % (j, p, j, p) for j in range(8)] + cols[0]
+        per.append(cols)
+    lines = interleave(per[0], per[1])
+    body = "\n".join('        "%s\\n"' % l for l in lines)
+    outs, ins = [], []
+    decl = []
+    for p, kind in enumerate(kinds):
+        outs += ['[t%d_%d] "=&v"(o%d.v[%d])' % (k, p, p, k) for k in range(9)]
+        outs += ['[q%d_%d] "=&v"(q%d[%d])' % (k, p, p, k) for k in range(9)]
+        decl.append("uint32_t q%d[9];" % p)
+        if kind == "sqr":
+            outs += ['[a2_%d_%d] "=&v"(a2_%d[%d])' % (j, p, p, j) for j in range(8)]
+            decl.append("uint32_t a2_%d[8];" % p)
+        ins += ['[a%d_%d] "v"(a%d.v[%d])' % (k, p, p, k) for k in range(9)]
+        if kind == "mul":
+            ins += ['[b%d_%d] "v"(b%d.v[%d])' % (k, p, p, k) for k in range(9)]
+    for i in range(9):
+        if m[i]:
+            ins.append('[m%d] "s"(%du)' % (i, m[i]))
+    if minv is not None:
+        ins.append('[minv] "s"(%du)' % minv)
+    return body, ",\n        ".join(outs), ",\n        ".join(ins), "\n  ".join(decl)
+
+
+HEADER = '''// GENERATED by tools/gen_fp29_asm.py -- do not edit; re-run the script.
+//
+// Radix-2^29 Montgomery products (fp29.hpp f29_mul / f29_sqr) of two
+// independent operand pairs, each as ONE gfx950 inline-asm block: the running
+// column accumulator is the v_mad_u64_u32 addend throughout (no re-associated
+// 64-bit adds), the two products' chains interleaved instruction by
+// instruction. Bit-identical to fp29.hpp (tools/microbench/fp29_asm_check.hip).
+#pragma once
+#include "fp29.hpp"
+
+#ifndef FE_ASM_ACC_CLOBBERS
+#define FE_ASM_ACC_CLOBBERS "v160", "v161", "v162", "v163"  // accumulators (tools/gen_fe_asm.py)
+#endif
+
+namespace cordahip {
+'''
+
+
+FUNCS = (
+    (("mul", "mul"), "mul_mul", "f29& r0, const f29& a0, const f29& b0, f29& r1, const f29& a1, const f29& b1"),
+    (("sqr", "sqr"), "sqr_sqr", "f29& r0, const f29& a0, f29& r1, const f29& a1"),
+    (("sqr", "mul"), "sqr_mul", "f29& r0, const f29& a0, f29& r1, const f29& a1, const f29& b1"),
+)
+
+
+def render():
+    """The header's full text."""
+    parts = [HEADER]
+    for curve in ("k1", "r1"):
+        for kinds, name, sig in FUNCS:
+            body, outs, ins, decl = gen(curve, kinds)
+            parts.append('''CDEV void f29a_%s_%s(%s) {
+  f29 o0, o1;
+  %s
+  asm(
+%s
+      : %s
+      : %s
+      : "vcc", FE_ASM_ACC_CLOBBERS);
+  r0 = o0;
+  r1 = o1;
+}
+''' % (name, curve, sig, decl, body, outs, ins))
+    parts.append("}  // namespace cordahip\n")
+    return "\n".join(parts)
+
+
+def main():
+    with open(OUT, "w") as f:
+        f.write(render())
+    print("wrote", OUT)
+
+
+if __name__ == "__main__":
+    main()
