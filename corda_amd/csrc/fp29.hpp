@@ -50,36 +50,64 @@ CDEV uint32_t sconst(uint32_t x) {
   return x;
 }
 
-// r = a b R^-1 mod p (norm, < 2p). Product scanning (FIPS): column k
-// accumulates a_j b_{k-j} and q_j m_{k-j}; for k < 9 the column then picks q_k
-// so that its low 29 bits vanish.
+// ---- Montgomery reduction in special form (both curves) --------------------
+// r = (a b + Q p) / 2^261 with Q = sum q_k 2^(29 k) chosen column by column so
+// that the low 261 bits vanish (product scanning: column k accumulates the
+// a_j b_(k-j) and the q terms that land in it). The q_k and the result are
+// those of a generic REDC over p's 9 limbs; only the q terms are cheaper:
+//   P-256: p = 2^256 - 2^224 + 2^192 + 2^96 - 1 == -1 (mod 2^29), so
+//     q_k = column mod 2^29 and its -q_k term clears exactly those bits (the
+//     shift does it, no instruction); the rest is q_k 2^9 in column k+3, q_k 2^18
+//     in k+6, q_k m7 in k+7 and q_k m8 in k+8 (m7 2^203 + m8 2^232 = 2^256 - 2^224):
+//     4 products per q instead of 7.
+//   secp256k1: p = m0 + m1 2^29 + (2^232 - 2^58) + m8 2^232; the six all-ones
+//     limbs (2^232 - 2^58) become -q_k in column k+2 and +q_k in column k+8
+//     (there with m8: q_k 2^24). The -q_k is added as (2^29 - 1 - q_k) >= 0 with
+//     the bias carried upwards (2^29 - q_0 in column 2, 2^29 - 1 in columns
+//     11..15, -1 in column 16: sum 0), so no column value is ever negative:
+//     4 products per q instead of 9.
+// Column sums stay < 2^64 for f29_mul's operand bounds (tests/test_fp29_asm.py
+// checks every column exactly; fp29_asm.hpp is the same schedule in asm pairs).
+template <class F>
+CDEV void f29_redc_terms(uint64_t& acc, const uint32_t* q, const uint32_t* qn, int k) {
+  if constexpr (F::kRed == 1) {
+    if (k >= 1 && k <= 9) acc += (uint64_t)q[k - 1] * sconst(F::m(1));
+    if (k >= 2 && k <= 10) acc += qn[k - 2];
+    if (k >= 11 && k <= 15) acc += kMask29;
+    if (k == 16) acc -= 1;
+    if (k >= 8) acc += (uint64_t)q[k - 8] * sconst(1u << 24);
+  } else {
+    if (k >= 3 && k <= 11) acc += (uint64_t)q[k - 3] * sconst(1u << 9);
+    if (k >= 6 && k <= 14) acc += (uint64_t)q[k - 6] * sconst(1u << 18);
+    if (k >= 7 && k <= 15) acc += (uint64_t)q[k - 7] * sconst(F::m(7));
+    if (k >= 8) acc += (uint64_t)q[k - 8] * sconst(F::m(8));
+  }
+}
+// column k < 9: pick q_k (and clear the column's low 29 bits)
+template <class F>
+CDEV void f29_redc_q(uint64_t& acc, uint32_t* q, uint32_t* qn, int k) {
+  if constexpr (F::kRed == 1) {
+    q[k] = ((uint32_t)acc * F::kMinv) & kMask29;
+    qn[k] = (k == 0 ? (1u << 29) : kMask29) - q[k];
+    acc += (uint64_t)q[k] * sconst(F::m(0));
+  } else {
+    q[k] = (uint32_t)acc & kMask29;  // acc - q_k: the p == -1 term
+  }
+}
+
+// r = a b R^-1 mod p (norm, < 2p)
 template <class F>
 CDEV void f29_mul(f29& r, const f29& a, const f29& b) {
-  uint32_t q[9], mk[9];
-#pragma unroll
-  for (int i = 0; i < 9; i++) mk[i] = F::m(i) ? sconst(F::m(i)) : 0u;
+  uint32_t q[9], qn[9];
   uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-#pragma unroll
-    for (int j = 0; j < k; j++) {
-      acc += (uint64_t)a.v[j] * b.v[k - j];
-      if (F::m(k - j)) acc += (uint64_t)q[j] * mk[k - j];
-    }
-    acc += (uint64_t)a.v[k] * b.v[0];
-    q[k] = (F::kMinvOne ? (uint32_t)acc : (uint32_t)acc * F::kMinv) & kMask29;
-    acc += (uint64_t)q[k] * mk[0];
-    acc >>= 29;
-  }
   f29 t;
 #pragma unroll
-  for (int k = 9; k < 17; k++) {
+  for (int k = 0; k < 17; k++) {
 #pragma unroll
-    for (int j = k - 8; j < 9; j++) {
-      acc += (uint64_t)a.v[j] * b.v[k - j];
-      if (F::m(k - j)) acc += (uint64_t)q[j] * mk[k - j];
-    }
-    t.v[k - 9] = (uint32_t)acc & kMask29;
+    for (int j = (k > 8 ? k - 8 : 0); j <= (k < 8 ? k : 8); j++) acc += (uint64_t)a.v[j] * b.v[k - j];
+    f29_redc_terms<F>(acc, q, qn, k);
+    if (k < 9) f29_redc_q<F>(acc, q, qn, k);
+    else t.v[k - 9] = (uint32_t)acc & kMask29;
     acc >>= 29;
   }
   t.v[8] = (uint32_t)acc;
@@ -89,35 +117,19 @@ CDEV void f29_mul(f29& r, const f29& a, const f29& b) {
 // r = a^2 R^-1 mod p: 45 distinct limb products (off-diagonal ones doubled)
 template <class F>
 CDEV void f29_sqr(f29& r, const f29& a) {
-  uint32_t q[9], mk[9], a2[9];
+  uint32_t q[9], qn[9], a2[9];
 #pragma unroll
-  for (int i = 0; i < 9; i++) {
-    mk[i] = F::m(i) ? sconst(F::m(i)) : 0u;
-    a2[i] = a.v[i] << 1;
-  }
+  for (int i = 0; i < 9; i++) a2[i] = a.v[i] << 1;
   uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-#pragma unroll
-    for (int j = 0; 2 * j < k; j++) acc += (uint64_t)a2[j] * a.v[k - j];
-    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
-#pragma unroll
-    for (int j = 0; j < k; j++)
-      if (F::m(k - j)) acc += (uint64_t)q[j] * mk[k - j];
-    q[k] = (F::kMinvOne ? (uint32_t)acc : (uint32_t)acc * F::kMinv) & kMask29;
-    acc += (uint64_t)q[k] * mk[0];
-    acc >>= 29;
-  }
   f29 t;
 #pragma unroll
-  for (int k = 9; k < 17; k++) {
+  for (int k = 0; k < 17; k++) {
 #pragma unroll
-    for (int j = k - 8; 2 * j < k; j++) acc += (uint64_t)a2[j] * a.v[k - j];
+    for (int j = (k > 8 ? k - 8 : 0); 2 * j < k; j++) acc += (uint64_t)a2[j] * a.v[k - j];
     if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
-#pragma unroll
-    for (int j = k - 8; j < 9; j++)
-      if (F::m(k - j)) acc += (uint64_t)q[j] * mk[k - j];
-    t.v[k - 9] = (uint32_t)acc & kMask29;
+    f29_redc_terms<F>(acc, q, qn, k);
+    if (k < 9) f29_redc_q<F>(acc, q, qn, k);
+    else t.v[k - 9] = (uint32_t)acc & kMask29;
     acc >>= 29;
   }
   t.v[8] = (uint32_t)acc;

@@ -3,7 +3,8 @@
 The header is emulated instruction by instruction (v_mad_u64_u32, v_mul_lo_u32,
 v_and_b32, v_lshrrev_b64, v_lshlrev_b32, v_mov_b32 on 32/64-bit registers) for
 random operands within f29_mul's bounds and compared with a restatement of
-fp29.hpp's product-scanning f29_mul / f29_sqr (and with a b R^-1 mod p). The
+a generic product-scanning REDC over p's nine limbs (and with a b R^-1 mod p);
+every column value is checked to stay in [0, 2^64) at each use. The
 GPU-side bit-identity check is tools/microbench/fp29_asm_check.hip.
 """
 import os
@@ -47,16 +48,19 @@ def emulate(lines, ops, a, b):
         mm = re.fullmatch(r"([ab])([01])\.v\[(\d)\]", e)
         if mm:
             vals[n] = (a if mm.group(1) == "a" else b)[int(mm.group(2))][int(mm.group(3))]
-    acc = {"v[160:161]": 0, "v[162:163]": 0}
+    acc = {"v[160:161]": 0, "v[162:163]": 0}  # exact integers: a wrap is an error
 
     def val(x):
         x = x.strip()
         if x.startswith("%["):
             return vals[x[2:-1]]
         if x in acc:
+            assert 0 <= acc[x] < 1 << 64, "column value out of range"
             return acc[x]
         if x in ("v160", "v162"):
-            return acc["v[%s:%d]" % (x[1:], int(x[1:]) + 1)] & M32
+            v = acc["v[%s:%d]" % (x[1:], int(x[1:]) + 1)]
+            assert 0 <= v < 1 << 64, "column value out of range"
+            return v & M32
         return int(x, 0)
 
     def dst(x):
@@ -68,11 +72,18 @@ def emulate(lines, ops, a, b):
         x = [t.strip() for t in rest.split(",")]
         if op == "v_mad_u64_u32":
             assert x[1] == "vcc"
-            acc[x[0]] = (val(x[2]) * val(x[3]) + val(x[4])) & M64
+            acc[x[0]] = val(x[2]) * val(x[3]) + (acc[x[4]] if x[4] in acc else val(x[4]))
+        elif op == "v_lshl_add_u64":  # only the bias -1: (-1 << 0) + acc
+            assert x[1:3] == ["-1", "0"] and x[3] == x[0]
+            acc[x[0]] -= 1
         elif op == "v_mul_lo_u32":
             vals[dst(x[0])] = (val(x[1]) * val(x[2])) & M32
         elif op == "v_and_b32":
             vals[dst(x[0])] = val(x[1]) & val(x[2])
+        elif op == "v_sub_u32":
+            r = val(x[1]) - val(x[2])
+            assert r >= 0
+            vals[dst(x[0])] = r
         elif op == "v_lshrrev_b64":
             acc[x[0]] = val(x[2]) >> int(x[1])
         elif op == "v_lshlrev_b32":
@@ -88,7 +99,8 @@ def emulate(lines, ops, a, b):
 
 
 def f29_mul_model(curve, a, b):
-    """fp29.hpp f29_mul (f29_sqr computes the same sum with doubled cross terms)."""
+    """Generic product-scanning REDC over p's nine limbs (fp29.hpp before the
+    special-form reduction; the special form must give the same limbs)."""
     m, minv = gen_fp29_asm.CURVES[curve]
     acc, q, t = 0, [0] * 9, [0] * 9
     for k in range(9):
@@ -133,10 +145,13 @@ def test_pairs_match_f29_mul(curve, shape):
     def rnd():  # < 2^257 (< 4p): within f29_mul's operand bounds
         return [rng.getrandbits(29) for _ in range(8)] + [rng.getrandbits(25)]
 
-    edge = [[M29] * 8 + [(1 << 25) - 1], [0] * 9, [1] + [0] * 8]
+    loose = 0x4C1BF828  # 2^30.25: f29_mul's loose limb bound (both operands)
+    edge = [[M29] * 8 + [(1 << 25) - 1], [0] * 9, [1] + [0] * 8, [loose] * 8 + [1 << 24]]
     for it in range(60):
-        a = {0: edge[it] if it < 3 else rnd(), 1: rnd()}
-        b = {0: rnd(), 1: edge[it] if it < 3 else rnd()}
+        a = {0: edge[it] if it < len(edge) else rnd(), 1: rnd()}
+        b = {0: rnd(), 1: edge[it] if it < len(edge) else rnd()}
+        if it == len(edge) - 1:
+            a[1] = b[0] = edge[it]
         for q in range(2):
             if kinds[q] == "sqr":
                 b[q] = a[q]

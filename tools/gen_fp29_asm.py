@@ -11,10 +11,12 @@ right by 29), which LLVM re-associates at a cost of one 64-bit add per column
 and the two products' chains are interleaved instruction by instruction.
 
 The terms, their order and every mask, shift and q computation are exactly
-fp29.hpp's, so the results are bit-identical (tools/microbench/fp29_asm_check.hip
-compares them on the GPU). Modulus limbs are SGPR operands (zero limbs skipped,
-as in fp29.hpp); secp256k1 computes q = (acc * kMinv) mod 2^29, P-256 (kMinv = 1)
-q = acc mod 2^29.
+fp29.hpp's (its special-form REDC: P-256 4 q terms per column digit and no m0
+term, secp256k1 4 q terms plus the (2^29 - 1 - q) bias terms), so the results
+are bit-identical to fp29.hpp and to a generic REDC
+(tests/test_fp29_asm.py emulates the header on the CPU,
+tools/microbench/fp29_asm_check.hip compares it on the GPU). Constants are
+SGPR operands.
 
 Run: python3 tools/gen_fp29_asm.py  (rewrites the header)
 """
@@ -35,44 +37,55 @@ CURVES = {
 }
 
 
-def product_terms(kind):
-    """fp29.hpp's instruction order for one product: a list of steps per column.
-    Steps: ('mad', a, b) | ('madq', j, i) (q_j * m_i) | ('q', k) | ('shift',) | ('out', k)."""
+def redc_terms(curve, k):
+    """fp29.hpp f29_redc_terms: the q terms (and bias constants) of column k."""
+    st = []
+    if curve == "k1":
+        if 1 <= k <= 9:
+            st.append(("madq", k - 1, "m1"))
+        if 2 <= k <= 10:
+            st.append(("madqn", k - 2))
+        if 11 <= k <= 15:
+            st.append(("addM",))
+        if k == 16:
+            st.append(("minus1",))
+        if k >= 8:
+            st.append(("madq", k - 8, "c24"))
+    else:
+        if 3 <= k <= 11:
+            st.append(("madq", k - 3, "c9"))
+        if 6 <= k <= 14:
+            st.append(("madq", k - 6, "c18"))
+        if 7 <= k <= 15:
+            st.append(("madq", k - 7, "m7"))
+        if k >= 8:
+            st.append(("madq", k - 8, "m8"))
+    return st
+
+
+def product_terms(kind, curve):
+    """fp29.hpp's f29_mul / f29_sqr schedule for one product: a list of steps per
+    column. Steps: ('mad', a, b) | ('madq', j, const) (q_j * const) | ('madqn', j)
+    (+ qn_j) | ('addM',) | ('minus1',) | ('q', k) | ('out', k) | ('shift',) | ('top',)."""
     cols = []
     for k in range(17):
         st = []
-        if k < 9:
-            if kind == "mul":
-                for j in range(k):
-                    st.append(("mad", "a%d" % j, "b%d" % (k - j)))
-                    st.append(("madq", j, k - j))
-                st.append(("mad", "a%d" % k, "b0"))
-            else:
-                for j in range(k):
-                    if 2 * j < k:
-                        st.append(("mad", "a2_%d" % j, "a%d" % (k - j)))
-                if k % 2 == 0:
-                    st.append(("mad", "a%d" % (k // 2), "a%d" % (k // 2)))
-                for j in range(k):
-                    st.append(("madq", j, k - j))
-            st.append(("q", k))
-            st.append(("madq", k, 0))
-            st.append(("shift",))
+        lo, hi = max(0, k - 8), min(k, 8)
+        if kind == "mul":
+            for j in range(lo, hi + 1):
+                st.append(("mad", "a%d" % j, "b%d" % (k - j)))
         else:
-            if kind == "mul":
-                for j in range(k - 8, 9):
-                    st.append(("mad", "a%d" % j, "b%d" % (k - j)))
-                    st.append(("madq", j, k - j))
-            else:
-                for j in range(k - 8, 9):
-                    if 2 * j < k:
-                        st.append(("mad", "a2_%d" % j, "a%d" % (k - j)))
-                if k % 2 == 0:
-                    st.append(("mad", "a%d" % (k // 2), "a%d" % (k // 2)))
-                for j in range(k - 8, 9):
-                    st.append(("madq", j, k - j))
+            for j in range(lo, hi + 1):
+                if 2 * j < k:
+                    st.append(("mad", "a2_%d" % j, "a%d" % (k - j)))
+            if k % 2 == 0:
+                st.append(("mad", "a%d" % (k // 2), "a%d" % (k // 2)))
+        st += redc_terms(curve, k)
+        if k < 9:
+            st.append(("q", k))
+        else:
             st.append(("out", k - 9))
-            st.append(("shift",))
+        st.append(("shift",))
         cols.append(st)
     cols.append([("top",)])
     return cols
@@ -80,32 +93,36 @@ def product_terms(kind):
 
 def expand(kind, p, curve):
     """Asm lines of one product p (0/1) as a list of per-column instruction lists."""
-    m, minv = CURVES[curve]
     cols = []
-    for st in product_terms(kind):
+    for st in product_terms(kind, curve):
         lines = []
         for s in st:
             if s[0] == "mad":
-                lines.append(("dep", "v_mad_u64_u32 %s, vcc, %%[%s_%d], %%[%s_%d], %s" % (ACC[p], s[1], p, s[2], p, ACC[p])))
+                lines.append("v_mad_u64_u32 %s, vcc, %%[%s_%d], %%[%s_%d], %s" % (ACC[p], s[1], p, s[2], p, ACC[p]))
             elif s[0] == "madq":
-                j, i = s[1], s[2]
-                if m[i] == 0:
-                    continue
-                lines.append(("dep", "v_mad_u64_u32 %s, vcc, %%[q%d_%d], %%[m%d], %s" % (ACC[p], j, p, i, ACC[p])))
+                lines.append("v_mad_u64_u32 %s, vcc, %%[q%d_%d], %%[%s], %s" % (ACC[p], s[1], p, s[2], ACC[p]))
+            elif s[0] == "madqn":
+                lines.append("v_mad_u64_u32 %s, vcc, %%[qn%d_%d], 1, %s" % (ACC[p], s[1], p, ACC[p]))
+            elif s[0] == "addM":
+                lines.append("v_mad_u64_u32 %s, vcc, %%[mask], 1, %s" % (ACC[p], ACC[p]))
+            elif s[0] == "minus1":
+                lines.append("v_lshl_add_u64 %s, -1, 0, %s" % (ACC[p], ACC[p]))
             elif s[0] == "q":
                 k = s[1]
-                if minv is None:
-                    lines.append(("dep", "v_and_b32 %%[q%d_%d], %s, %s" % (k, p, M29, ACC_LO[p])))
+                if curve == "k1":
+                    lines.append("v_mul_lo_u32 %%[q%d_%d], %s, %%[minv]" % (k, p, ACC_LO[p]))
+                    lines.append("v_and_b32 %%[q%d_%d], %s, %%[q%d_%d]" % (k, p, M29, k, p))
+                    lines.append("v_sub_u32 %%[qn%d_%d], %s, %%[q%d_%d]" % (k, p, "0x20000000" if k == 0 else M29, k, p))
+                    lines.append("v_mad_u64_u32 %s, vcc, %%[q%d_%d], %%[m0], %s" % (ACC[p], k, p, ACC[p]))
                 else:
-                    lines.append(("dep", "v_mul_lo_u32 %%[q%d_%d], %s, %%[minv]" % (k, p, ACC_LO[p])))
-                    lines.append(("dep", "v_and_b32 %%[q%d_%d], %s, %%[q%d_%d]" % (k, p, M29, k, p)))
+                    lines.append("v_and_b32 %%[q%d_%d], %s, %s" % (k, p, M29, ACC_LO[p]))
             elif s[0] == "shift":
-                lines.append(("dep", "v_lshrrev_b64 %s, 29, %s" % (ACC[p], ACC[p])))
+                lines.append("v_lshrrev_b64 %s, 29, %s" % (ACC[p], ACC[p]))
             elif s[0] == "out":
-                lines.append(("dep", "v_and_b32 %%[t%d_%d], %s, %s" % (s[1], p, M29, ACC_LO[p])))
+                lines.append("v_and_b32 %%[t%d_%d], %s, %s" % (s[1], p, M29, ACC_LO[p]))
             elif s[0] == "top":
-                lines.append(("dep", "v_mov_b32 %%[t8_%d], %s" % (p, ACC_LO[p])))
-        cols.append([l for _, l in lines])
+                lines.append("v_mov_b32 %%[t8_%d], %s" % (p, ACC_LO[p]))
+        cols.append(lines)
     return cols
 
 
@@ -142,24 +159,27 @@ def gen(curve, kinds):
         outs += ['[t%d_%d] "=&v"(o%d.v[%d])' % (k, p, p, k) for k in range(9)]
         outs += ['[q%d_%d] "=&v"(q%d[%d])' % (k, p, p, k) for k in range(9)]
         decl.append("uint32_t q%d[9];" % p)
+        if curve == "k1":
+            outs += ['[qn%d_%d] "=&v"(qn%d[%d])' % (k, p, p, k) for k in range(9)]
+            decl.append("uint32_t qn%d[9];" % p)
         if kind == "sqr":
             outs += ['[a2_%d_%d] "=&v"(a2_%d[%d])' % (j, p, p, j) for j in range(8)]
             decl.append("uint32_t a2_%d[8];" % p)
         ins += ['[a%d_%d] "v"(a%d.v[%d])' % (k, p, p, k) for k in range(9)]
         if kind == "mul":
             ins += ['[b%d_%d] "v"(b%d.v[%d])' % (k, p, p, k) for k in range(9)]
-    for i in range(9):
-        if m[i]:
-            ins.append('[m%d] "s"(%du)' % (i, m[i]))
-    if minv is not None:
-        ins.append('[minv] "s"(%du)' % minv)
+    if curve == "k1":
+        consts = [("m0", m[0]), ("m1", m[1]), ("c24", 1 << 24), ("mask", (1 << 29) - 1), ("minv", minv)]
+    else:
+        consts = [("c9", 1 << 9), ("c18", 1 << 18), ("m7", m[7]), ("m8", m[8])]
+    ins += ['[%s] "s"(%du)' % c for c in consts]
     return body, ",\n        ".join(outs), ",\n        ".join(ins), "\n  ".join(decl)
 
 
 HEADER = '''// GENERATED by tools/gen_fp29_asm.py -- do not edit; re-run the script.
 //
-// Radix-2^29 Montgomery products (fp29.hpp f29_mul / f29_sqr) of two
-// independent operand pairs, each as ONE gfx950 inline-asm block: the running
+// Radix-2^29 Montgomery products (fp29.hpp f29_mul / f29_sqr, special-form
+// REDC) of two independent operand pairs, each as ONE gfx950 inline-asm block: the running
 // column accumulator is the v_mad_u64_u32 addend throughout (no re-associated
 // 64-bit adds), the two products' chains interleaved instruction by
 // instruction. Bit-identical to fp29.hpp (tools/microbench/fp29_asm_check.hip).
