@@ -1197,26 +1197,26 @@ CDEV void ecdsa_affine_lane(uint32_t* __restrict__ rec) {
   }
 }
 
+// One kernel per curve (launched over the whole chunk; the other curve's lanes
+// exit at once, and the partition makes them whole waves): the register
+// allocations differ (P-256 fits 164 VGPRs = 3 waves per SIMD, secp256k1's
+// GLV ladder needs ~214 = 2 waves), and a combined kernel runs both at the
+// larger one.
+template <int S>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ecdsa_ladder_kernel(
     const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, uint64_t base, uint64_t m,
-    const uint32_t* __restrict__ gtab_k1, const uint32_t* __restrict__ gtab_r1, uint32_t* __restrict__ ws,
-    uint8_t* __restrict__ status) {
+    const uint32_t* __restrict__ gtab, uint32_t* __restrict__ ws, uint8_t* __restrict__ status) {
   const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= m) return;
   const uint64_t slot = base + li;
   const uint64_t i = perm ? perm[slot] : slot;
-  if (status[i] != kEcPending) return;
+  if (scheme[i] != S || status[i] != kEcPending) return;
   uint32_t* rec = ws + li * kEcWords;
   // table-to-affine pass fused into the ladder: as a kernel of its own its
   // uncoalesced record traffic cost 14.8 ms per 2^24 lanes; here it overlaps the
   // VALU-bound ladder of the SIMD's other waves (same thread writes, then reads)
-  if (scheme[i] == 2) {
-    ecdsa_affine_lane<Curve<2>>(rec);
-    status[i] = ecdsa_ladder_lane<Curve<2>>(rec, gtab_k1);
-  } else {
-    ecdsa_affine_lane<Curve<3>>(rec);
-    status[i] = ecdsa_ladder_lane<Curve<3>>(rec, gtab_r1);
-  }
+  ecdsa_affine_lane<Curve<S>>(rec);
+  status[i] = ecdsa_ladder_lane<Curve<S>>(rec, gtab);
 }
 
 // ---------------------------------------------------------------------------
@@ -1266,7 +1266,8 @@ hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const
     const uint64_t nt = (m + kEcInvBatch - 1) / kEcInvBatch;
     hipLaunchKernelGGL(ecdsa_inv_kernel, dim3((uint32_t)((nt + 255) / 256)), dim3(256), 0, s, base, m, counters6,
                        ws);
-    hipLaunchKernelGGL(ecdsa_ladder_kernel, g, dim3(256), 0, s, perm, scheme, base, m, gk1, gr1, ws, status);
+    hipLaunchKernelGGL(ecdsa_ladder_kernel<2>, g, dim3(256), 0, s, perm, scheme, base, m, gk1, ws, status);
+    hipLaunchKernelGGL(ecdsa_ladder_kernel<3>, g, dim3(256), 0, s, perm, scheme, base, m, gr1, ws, status);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -37,6 +37,9 @@
 #define T_LSHLADD(k) "v_lshl_add_u32 %" S(k) ", %" S(k) ", 1, %16\n"
 #define T_ANDOR(k) "v_and_or_b32 %" S(k) ", %" S(k) ", %16, %17\n"
 #define T_CNDMASK(k) "v_cndmask_b32 %" S(k) ", %" S(k) ", %16, vcc\n"
+#define T_CNDMASKS(k) "v_cndmask_b32_e64 %" S(k) ", %" S(k) ", %16, %18\n"
+#define T_BFI(k) "v_bfi_b32 %" S(k) ", %17, %" S(k) ", %16\n"
+#define T_XOR(k) "v_xor_b32 %" S(k) ", %" S(k) ", %16\n"
 #define T_ADDCO(k) "v_add_co_u32 %" S(k) ", vcc, %" S(k) ", %16\n"
 #define T_SUB(k) "v_sub_u32 %" S(k) ", %16, %" S(k) "\n"
 #define T_MOV(k) "v_mov_b32 %" S(k) ", %16\n"
@@ -49,12 +52,14 @@
 #define T_ADD64(k) "v_lshl_add_u64 %" S(k) ", %19, 0, %" S(k) "\n"
 
 enum { K_ADD, K_AND, K_LSHL, K_LSHR, K_MULLO, K_MUL19, K_MAD24, K_ALIGN, K_BFE, K_ADD3, K_LSHLADD, K_ANDOR,
-       K_CNDMASK, K_ADDCO, K_SUB, K_MOV, K_FMA32, K_MAD64, K_MAD64C, K_LSHR64, K_LSHLADD64, K_N };
+       K_CNDMASK, K_ADDCO, K_SUB, K_MOV, K_FMA32, K_MAD64, K_MAD64C, K_LSHR64, K_LSHLADD64, K_CNDMASKS, K_BFI, K_XOR,
+       K_N };
 static const char* kName[K_N] = {"v_add_u32", "v_and_b32", "v_lshlrev_b32", "v_lshrrev_b32", "v_mul_lo_u32",
                                  "v_mul_lo_u32 x19", "v_mad_u32_u24", "v_alignbit_b32", "v_bfe_u32", "v_add3_u32",
                                  "v_lshl_add_u32", "v_and_or_b32", "v_cndmask_b32", "v_add_co_u32", "v_sub_u32",
                                  "v_mov_b32", "v_fma_f32", "v_mad_u64_u32", "v_mad_u64_u32 x19",
-                                 "v_lshrrev_b64", "v_lshl_add_u64"};
+                                 "v_lshrrev_b64", "v_lshl_add_u64", "v_cndmask_b32_e64 (SGPR pair)",
+                                 "v_bfi_b32", "v_xor_b32"};
 
 template <int K>
 __global__ void __launch_bounds__(256) bench(uint32_t* out, uint32_t seed, int iters, unsigned long long* clk) {
@@ -63,6 +68,7 @@ __global__ void __launch_bounds__(256) bench(uint32_t* out, uint32_t seed, int i
   uint32_t m = seed ^ threadIdx.x, m2 = seed * 3u + threadIdx.x;
   uint64_t m64 = ((uint64_t)m2 << 32) | m;
   unsigned long long cc = 0;
+  const unsigned long long sm = __builtin_amdgcn_read_exec() ^ (unsigned long long)seed;  // a uniform 64-bit lane mask
 #pragma unroll
   for (int c = 0; c < 16; c++) {
     x[c] = seed * (c + 1) + threadIdx.x;
@@ -75,6 +81,7 @@ __global__ void __launch_bounds__(256) bench(uint32_t* out, uint32_t seed, int i
 #pragma unroll
     for (int u = 0; u < 4; u++) {
 #define BODY32(T) asm volatile(R16(T) : XS : "v"(m), "v"(m2) : "vcc")
+#define BODY32S(T) asm volatile(R16(T) : XS : "v"(m), "v"(m2), "s"(sm) : "vcc")
 #define BODY64(T) asm volatile(R16(T) : YS : "v"(m), "v"(m2), "s"(cc), "v"(m64) : "vcc")
       if (K == K_ADD) BODY32(T_ADD);
       if (K == K_AND) BODY32(T_AND);
@@ -97,6 +104,9 @@ __global__ void __launch_bounds__(256) bench(uint32_t* out, uint32_t seed, int i
       if (K == K_MAD64C) BODY64(T_MAD64C);
       if (K == K_LSHR64) BODY64(T_LSHR64);
       if (K == K_LSHLADD64) BODY64(T_LSHLADD64);
+      if (K == K_CNDMASKS) BODY32S(T_CNDMASKS);
+      if (K == K_BFI) BODY32(T_BFI);
+      if (K == K_XOR) BODY32(T_XOR);
     }
   }
   if (threadIdx.x == 0 && blockIdx.x == 0) {
