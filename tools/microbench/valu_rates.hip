@@ -40,6 +40,11 @@
 #define T_CNDMASKS(k) "v_cndmask_b32_e64 %" S(k) ", %" S(k) ", %16, %18\n"
 #define T_BFI(k) "v_bfi_b32 %" S(k) ", %17, %" S(k) ", %16\n"
 #define T_XOR(k) "v_xor_b32 %" S(k) ", %" S(k) ", %16\n"
+// mp256.hpp mac(): a 64-bit MAC whose carry-out (VCC) is caught by v_addc (VCC in);
+// y[k] at %0..%15, x[k] at %16..%31, m at %32, m2 at %33; reported per instruction
+#define T_MACP(k, h) "v_mad_u64_u32 %" S(k) ", vcc, %32, %33, %" S(k) "\n v_addc_co_u32 %" S(h) ", vcc, 0, %" S(h) ", vcc\n"
+#define R16P(T) T(0, 16) T(1, 17) T(2, 18) T(3, 19) T(4, 20) T(5, 21) T(6, 22) T(7, 23) T(8, 24) T(9, 25) \
+  T(10, 26) T(11, 27) T(12, 28) T(13, 29) T(14, 30) T(15, 31)
 #define T_ADDCO(k) "v_add_co_u32 %" S(k) ", vcc, %" S(k) ", %16\n"
 #define T_SUB(k) "v_sub_u32 %" S(k) ", %16, %" S(k) "\n"
 #define T_MOV(k) "v_mov_b32 %" S(k) ", %16\n"
@@ -53,13 +58,13 @@
 
 enum { K_ADD, K_AND, K_LSHL, K_LSHR, K_MULLO, K_MUL19, K_MAD24, K_ALIGN, K_BFE, K_ADD3, K_LSHLADD, K_ANDOR,
        K_CNDMASK, K_ADDCO, K_SUB, K_MOV, K_FMA32, K_MAD64, K_MAD64C, K_LSHR64, K_LSHLADD64, K_CNDMASKS, K_BFI, K_XOR,
-       K_N };
+       K_MACP, K_N };
 static const char* kName[K_N] = {"v_add_u32", "v_and_b32", "v_lshlrev_b32", "v_lshrrev_b32", "v_mul_lo_u32",
                                  "v_mul_lo_u32 x19", "v_mad_u32_u24", "v_alignbit_b32", "v_bfe_u32", "v_add3_u32",
                                  "v_lshl_add_u32", "v_and_or_b32", "v_cndmask_b32", "v_add_co_u32", "v_sub_u32",
                                  "v_mov_b32", "v_fma_f32", "v_mad_u64_u32", "v_mad_u64_u32 x19",
                                  "v_lshrrev_b64", "v_lshl_add_u64", "v_cndmask_b32_e64 (SGPR pair)",
-                                 "v_bfi_b32", "v_xor_b32"};
+                                 "v_bfi_b32", "v_xor_b32", "v_mad_u64_u32 + v_addc_co_u32 (VCC carry)"};
 
 template <int K>
 __global__ void __launch_bounds__(256) bench(uint32_t* out, uint32_t seed, int iters, unsigned long long* clk) {
@@ -107,6 +112,7 @@ __global__ void __launch_bounds__(256) bench(uint32_t* out, uint32_t seed, int i
       if (K == K_CNDMASKS) BODY32S(T_CNDMASKS);
       if (K == K_BFI) BODY32(T_BFI);
       if (K == K_XOR) BODY32(T_XOR);
+      if (K == K_MACP) asm volatile(R16P(T_MACP) : YS, XS : "v"(m), "v"(m2) : "vcc");
     }
   }
   if (threadIdx.x == 0 && blockIdx.x == 0) {
@@ -135,7 +141,7 @@ static int run(int blocks, int iters, uint32_t* dout, unsigned long long* dclk, 
   unsigned long long clk[2];
   CHECK(hipMemcpy(clk, dclk, sizeof(clk), hipMemcpyDeviceToHost));
   const double ghz = (double)clk[0] / ((double)clk[1] / 100e6) / 1e9;  // memrealtime ticks at 100 MHz
-  const double wave_insts = (double)blocks * 4.0 * iters * 4.0 * 16.0;   // 4 waves/block, 4 x 16 per iter
+  const double wave_insts = (double)blocks * 4.0 * iters * 4.0 * 16.0 * (K == K_MACP ? 2.0 : 1.0);  // 4 waves/block, 4 x 16 per iter
   const double cyc = ghz * 1e9 * ms * 1e-3 / (wave_insts / (ncu * 4.0));
   printf("{\"op\": \"%s\", \"cycles_per_wave_inst\": %.2f, \"clock_ghz\": %.3f, \"ms\": %.3f}\n", kName[K], cyc,
          ghz, ms);
