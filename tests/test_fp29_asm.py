@@ -86,6 +86,8 @@ def emulate(lines, ops, a, b):
             vals[dst(x[0])] = r
         elif op == "v_lshrrev_b64":
             acc[x[0]] = val(x[2]) >> int(x[1])
+        elif op == "v_add_u32":
+            vals[dst(x[0])] = (val(x[1]) + val(x[2])) & M32
         elif op == "v_lshlrev_b32":
             vals[dst(x[0])] = (val(x[2]) << int(x[1])) & M32
         elif op == "v_mov_b32":

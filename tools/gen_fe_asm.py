@@ -71,8 +71,14 @@ def gen(kind):
         for nm in need:
             base, idx = nm.split("_")
             src = ("g_%s" % idx) if base == "g19" else ("f_%s" % idx)
-            if base in ("f2", "f4"):
-                lines.append("v_lshlrev_b32 %%[%s%d], %d, %%[%s%d]" % (nm, p, 1 if base == "f2" else 2, src, p))
+            # doublings as adds: v_add_u32 issues at ~2.3 cycles per wave64
+            # instruction, v_lshlrev_b32 at ~4.0 (profiles/r02_valu_rates.jsonl)
+            if base == "f2":
+                lines.append("v_add_u32 %%[%s%d], %%[%s%d], %%[%s%d]" % (nm, p, src, p, src, p))
+            elif base == "f4" and ("f2_" + idx) in need:  # sorted: f2_i is already there
+                lines.append("v_add_u32 %%[%s%d], %%[f2_%s%d], %%[f2_%s%d]" % (nm, p, idx, p, idx, p))
+            elif base == "f4":
+                lines.append("v_lshlrev_b32 %%[%s%d], 2, %%[%s%d]" % (nm, p, src, p))
             elif base in ("g19", "f19"):
                 lines.append("v_mul_lo_u32 %%[%s%d], %%[%s%d], 19" % (nm, p, src, p))
     for k in range(10):

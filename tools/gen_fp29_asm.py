@@ -149,7 +149,8 @@ def gen(curve, kinds):
         first = cols[0][0]
         cols[0][0] = first[: first.rfind(",")] + ", 0"
         if kind == "sqr":
-            cols[0] = ["v_lshlrev_b32 %%[a2_%d_%d], 1, %%[a%d_%d]" % (j, p, j, p) for j in range(8)] + cols[0]
+            # 2a as an add: v_add_u32 issues at ~2.3 cycles, v_lshlrev_b32 at ~4.0
+            cols[0] = ["v_add_u32 %%[a2_%d_%d], %%[a%d_%d], %%[a%d_%d]" % (j, p, j, p, j, p) for j in range(8)] + cols[0]
         per.append(cols)
     lines = interleave(per[0], per[1])
     body = "\n".join('        "%s\\n"' % l for l in lines)

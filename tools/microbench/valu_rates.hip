@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); return 1; } } while (0)
@@ -126,7 +127,7 @@ __global__ void __launch_bounds__(256) bench(uint32_t* out, uint32_t seed, int i
 }
 
 template <int K>
-static int run(int blocks, int iters, uint32_t* dout, unsigned long long* dclk, int ncu) {
+static int run(int blocks, int iters, uint32_t* dout, unsigned long long* dclk, int ncu, int waves) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
@@ -143,27 +144,30 @@ static int run(int blocks, int iters, uint32_t* dout, unsigned long long* dclk, 
   const double ghz = (double)clk[0] / ((double)clk[1] / 100e6) / 1e9;  // memrealtime ticks at 100 MHz
   const double wave_insts = (double)blocks * 4.0 * iters * 4.0 * 16.0 * (K == K_MACP ? 2.0 : 1.0);  // 4 waves/block, 4 x 16 per iter
   const double cyc = ghz * 1e9 * ms * 1e-3 / (wave_insts / (ncu * 4.0));
-  printf("{\"op\": \"%s\", \"cycles_per_wave_inst\": %.2f, \"clock_ghz\": %.3f, \"ms\": %.3f}\n", kName[K], cyc,
-         ghz, ms);
+  printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_wave_inst\": %.2f, \"clock_ghz\": %.3f, \"ms\": %.3f}\n",
+         kName[K], waves, cyc, ghz, ms);
   CHECK(hipEventDestroy(e0));
   CHECK(hipEventDestroy(e1));
   return 0;
 }
 
 template <int K>
-static int run_all(uint32_t* dout, unsigned long long* dclk, int ncu) {
-  if (run<K>(ncu * 8, 2048, dout, dclk, ncu)) return 1;
-  if constexpr (K + 1 < K_N) return run_all<K + 1>(dout, dclk, ncu);
+static int run_all(uint32_t* dout, unsigned long long* dclk, int ncu, int waves) {
+  if (run<K>(ncu * waves, 2048, dout, dclk, ncu, waves)) return 1;
+  if constexpr (K + 1 < K_N) return run_all<K + 1>(dout, dclk, ncu, waves);
   return 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
   hipDeviceProp_t p;
   CHECK(hipGetDeviceProperties(&p, 0));
   uint32_t* dout;
   unsigned long long* dclk;
   CHECK(hipMalloc(&dout, (size_t)p.multiProcessorCount * 8 * 256 * sizeof(uint32_t)));
   CHECK(hipMalloc(&dclk, 2 * sizeof(unsigned long long)));
-  printf("{\"arch\": \"%s\", \"cus\": %d, \"waves_per_simd\": 8}\n", p.gcnArchName, p.multiProcessorCount);
-  return run_all<0>(dout, dclk, p.multiProcessorCount);
+  // waves per SIMD from argv (default 8: the issue-cost table); 256-thread
+  // blocks = one wave per SIMD each
+  const int waves = argc > 1 ? atoi(argv[1]) : 8;
+  printf("{\"arch\": \"%s\", \"cus\": %d, \"waves_per_simd\": %d}\n", p.gcnArchName, p.multiProcessorCount, waves);
+  return run_all<0>(dout, dclk, p.multiProcessorCount, waves);
 }
