@@ -55,7 +55,7 @@ class C2:
     # one step = the split verification pass: prep (decode A/R, SHA-512, lattice
     # reduction -> per-lane workspace) + ladder, one launch pair per 2^20 lanes
     kernel = "ed25519_prep_half_kernel + ed25519_ladder_half_kernel"
-    pmc = "r01_pmc_ed25519_split.json"
+    pmc = "r02_pmc_ed25519_split.json"
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -186,7 +186,7 @@ class C1(C2):
 # ---- C3: mixed secp256k1 / P-256 ECDSA ----------------------------------------
 class C3:
     kernel = "ecdsa_prep_kernel + ecdsa_inv_kernel + ecdsa_ladder_kernel"
-    pmc = "r01_pmc_ecdsa_verify.json"
+    pmc = "r02_pmc_ecdsa_verify.json"
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -537,7 +537,8 @@ def main():
             "corpus_gen_s": t_gen,
         }
         if world == 1 and not args.no_cpu_baseline:
-            sample = args.cpu_sample or {"c1": 1 << 20, "c2": 1 << 17, "c3": 1 << 16, "c4": 1 << 16, "c5": 1 << 16}[args.workload]
+            # bounded samples sized for ~10 s of 16-thread CPU work each (C1: its whole 2^20 set)
+            sample = args.cpu_sample or {"c1": 1 << 20, "c2": 1 << 22, "c3": 1 << 20, "c4": 1 << 20, "c5": 1 << 21}[args.workload]
             out["cpu_baseline"] = wl.cpu_baseline(min(sample, wl.units))
         print(json.dumps(out), flush=True)
     eng.close()

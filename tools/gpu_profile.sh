@@ -16,7 +16,7 @@ for wl in ${PMC_WLS:-c3 c2}; do
   WL=$wl TAG=$wl bash $R/tools/gpu_pmc.sh > $O/pmc_$wl.log 2>&1 || { echo "pmc $wl failed"; tail -5 $O/pmc_$wl.log; exit 1; }
   echo "pmc $wl done"
 done
-if [ -x $R/ab_libs/valu_rates ]; then
+if [ "${CAL:-1}" = 1 ] && [ -x $R/ab_libs/valu_rates ]; then
   timeout -k 10 120 $R/ab_libs/valu_rates > $O/valu_rates.jsonl || { echo "valu_rates failed"; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d /tmp/cal -o cal -- $R/ab_libs/valu_rates > $O/cal.log 2>&1 || { echo "calibration pmc failed"; tail -5 $O/cal.log; exit 1; }
   find /tmp/cal -name "*counter_collection.csv" -exec cp {} $O/cal.csv \;
