@@ -253,7 +253,7 @@ class C3:
 # ---- C4: SignedTransaction.verifySignatures on cash-issue transactions --------
 class C4:
     kernel = "sha256_leaves + merkle_root + ed25519 prep/ladder + tx_reduce"
-    pmc = "r01_pmc_c4.json"
+    pmc = "r02_pmc_c4.json"
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
