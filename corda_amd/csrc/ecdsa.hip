@@ -187,51 +187,31 @@ CDEV void jdbl(jpt& r, const jpt& p) {
     f29_sub<F>(t, p.X, delta);  // < 4p
     f29_add(u, p.X, delta);     // < 4p
     f29_mul_pair<F>(beta, p.X, gamma, a3, t, u);
-    f29_add(t, a3, a3);
-    f29_add(t, t, a3);
-    f29_red<F>(a3, t);          // alpha = 3 (X - delta)(X + delta)
-    f29_add(t, beta, beta);
-    f29_add(t, t, t);
-    f29_red<F>(b4, t);          // 4 beta
+    f29_mulk_red<F, 3>(a3, a3);  // alpha = 3 (X - delta)(X + delta)
+    f29_mulk_red<F, 4>(b4, beta);
     f29_add(yz, p.Y, p.Z);
     f29_sqr_pair<F>(x3, a3, yz, yz);
-    f29_sub<F>(x3, x3, b4);
-    f29_sub<F>(t, x3, b4);      // < 6p
-    f29_red<F>(x3, t);          // X3 = alpha^2 - 8 beta
-    f29_sub<F>(t, yz, gamma);
-    f29_sub<F>(t, t, delta);
-    f29_red<F>(z3, t);          // Z3 = (Y + Z)^2 - gamma - delta
+    f29_sub2_red<F>(x3, x3, b4, b4);       // X3 = alpha^2 - 8 beta
+    f29_sub2_red<F>(z3, yz, gamma, delta);  // Z3 = (Y + Z)^2 - gamma - delta
     f29_sub<F>(u, b4, x3);
     f29_add(t, gamma, gamma);
     f29_sqr_mul_pair<F>(t, t, y3, a3, u);  // 4 gamma^2, alpha (4 beta - X3)
-    f29_sub<F>(y3, y3, t);
-    f29_sub<F>(u, y3, t);
-    f29_red<F>(y3, u);          // Y3 = alpha (4 beta - X3) - 8 gamma^2
+    f29_sub2_red<F>(y3, y3, t, t);          // Y3 = alpha (4 beta - X3) - 8 gamma^2
   } else {
     f29 A, B, Cc, D, E;
     f29_sqr_pair<F>(A, p.X, B, p.Y);
     f29_add(t, p.X, B);
     f29_sqr_pair<F>(Cc, B, t, t);
-    f29_sub<F>(t, t, A);
-    f29_sub<F>(t, t, Cc);       // < 6p
-    f29_add(t, t, t);           // < 12p
-    f29_red<F>(D, t);           // D = 2 ((X + B)^2 - A - C)
-    f29_add(t, A, A);
-    f29_add(t, t, A);
-    f29_red<F>(E, t);           // E = 3 A
+    f29_sub2_red<F>(t, t, A, Cc);
+    f29_mulk_red<F, 2>(D, t);    // D = 2 ((X + B)^2 - A - C)
+    f29_mulk_red<F, 3>(E, A);    // E = 3 A
     f29_add(t, p.Y, p.Y);
     f29_sqr_mul_pair<F>(x3, E, z3, t, p.Z);  // E^2, Z3 = 2 Y Z
-    f29_sub<F>(x3, x3, D);
-    f29_sub<F>(t, x3, D);
-    f29_red<F>(x3, t);          // X3 = E^2 - 2 D
+    f29_sub2_red<F>(x3, x3, D, D);           // X3 = E^2 - 2 D
     f29_sub<F>(t, D, x3);
     f29_mul<F>(y3, E, t);
-    f29_add(t, Cc, Cc);
-    f29_add(t, t, t);
-    f29_red<F>(u, t);           // 4 C
-    f29_sub<F>(y3, y3, u);
-    f29_sub<F>(t, y3, u);
-    f29_red<F>(y3, t);          // Y3 = E (D - X3) - 8 C
+    f29_mulk_red<F, 4>(u, Cc);   // 4 C
+    f29_sub2_red<F>(y3, y3, u, u);  // Y3 = E (D - X3) - 8 C
   }
   r.X = x3;
   r.Y = y3;
@@ -314,10 +294,8 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
   f29 z1z1, u2, s2, h, hh, i, j, rr, v, t, x3, y3, z3;
   f29_sqr_mul_pair<F>(z1z1, p.Z, t, y2, p.Z);
   f29_mul_pair<F>(u2, x2, z1z1, s2, t, z1z1);
-  f29_sub<F>(t, u2, p.X);
-  f29_red<F>(h, t);
-  f29_sub<F>(t, s2, p.Y);
-  f29_red<F>(rr, t);
+  f29_sub_red<F>(h, u2, p.X);
+  f29_sub_red<F>(rr, s2, p.Y);
   if (f29_iszero<F>(h)) {
     if (f29_iszero<F>(rr)) {
       jdbl<C>(r, p);
@@ -331,20 +309,13 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
   f29_add(i, hh, hh);
   f29_add(i, i, i);             // I = 4 HH, < 8p
   f29_mul_pair<F>(j, h, i, v, p.X, i);
-  f29_sub<F>(x3, x3, j);
-  f29_sub<F>(x3, x3, v);
-  f29_sub<F>(t, x3, v);
-  f29_red<F>(x3, t);
+  f29_sub3_red<F>(x3, x3, j, v, v);  // X3 = r^2 - J - 2 V
   f29_sub<F>(t, v, x3);
   f29_mul_pair<F>(y3, rr, t, t, p.Y, j);
-  f29_sub<F>(y3, y3, t);
-  f29_sub<F>(y3, y3, t);
-  f29_red<F>(y3, y3);
+  f29_sub2_red<F>(y3, y3, t, t);     // Y3 = r (V - X3) - 2 Y1 J
   f29_add(t, p.Z, h);
   f29_sqr<F>(t, t);
-  f29_sub<F>(t, t, z1z1);
-  f29_sub<F>(t, t, hh);
-  f29_red<F>(z3, t);
+  f29_sub2_red<F>(z3, t, z1z1, hh);  // Z3 = (Z1 + H)^2 - Z1Z1 - HH
   r.X = x3;
   r.Y = y3;
   r.Z = z3;

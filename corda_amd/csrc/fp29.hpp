@@ -167,17 +167,10 @@ CDEV void f29_cneg(f29& r, bool neg) {
   for (int i = 0; i < 9; i++) r.v[i] = neg ? n.v[i] : r.v[i];
 }
 
-// limbs < 2^31.5, value < 2^260  ->  norm, value < 2p
+// limbs 0..7 of r normalised (< 2^29), top = the value's bits >= 2^232 (value
+// < 2^260)  ->  r norm, value < 2p: folds the bits >= 2^256.
 template <class F>
-CDEV void f29_red(f29& r, const f29& a) {
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint32_t t = a.v[i] + c;
-    r.v[i] = t & kMask29;
-    c = t >> 29;
-  }
-  const uint32_t top = a.v[8] + c;
+CDEV void f29_fold(f29& r, uint32_t top) {
   const uint32_t q = top >> 24;  // the value's bits >= 2^256 (q < 16)
   r.v[8] = top & 0xffffffu;
   if (F::kRed == 1) {
@@ -199,6 +192,72 @@ CDEV void f29_red(f29& r, const f29& a) {
       r.v[i + 1] += (uint32_t)cs;
     }
   }
+}
+
+// limbs < 2^31.5, value < 2^260  ->  norm, value < 2p
+template <class F>
+CDEV void f29_red(f29& r, const f29& a) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a.v[i] + c;
+    r.v[i] = t & kMask29;
+    c = t >> 29;
+  }
+  f29_fold<F>(r, a.v[8] + c);
+}
+
+// The point formulas' "subtract, subtract, reduce" steps in ONE carry pass:
+// r = red(a + 2p - b), red(a + 4p - b - c), red(a + 6p - b - c - d). The
+// subtrahends are norm (value <= 2p, limbs < 2^29 + 2^15), the minuend's limbs
+// < 2^30.5 (a product output or a sum of two norms); F::sub4p / sub6p keep
+// every limb in [0, 2^32) (tools/gen_fp29_consts.py subkp). Value < a + 6p
+// < 2^260, so the fold applies. Same residue as the f29_sub / f29_red chains
+// they replace (another representative: every comparison goes through f29_canon).
+template <class F>
+CDEV void f29_sub_red(f29& r, const f29& a, const f29& b) {
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a.v[i] + F::sub2p(i) - b.v[i] + cy;
+    r.v[i] = t & kMask29;
+    cy = t >> 29;
+  }
+  f29_fold<F>(r, a.v[8] + F::sub2p(8) - b.v[8] + cy);
+}
+template <class F>
+CDEV void f29_sub2_red(f29& r, const f29& a, const f29& b, const f29& c) {
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a.v[i] + F::sub4p(i) - b.v[i] - c.v[i] + cy;
+    r.v[i] = t & kMask29;
+    cy = t >> 29;
+  }
+  f29_fold<F>(r, a.v[8] + F::sub4p(8) - b.v[8] - c.v[8] + cy);
+}
+template <class F>
+CDEV void f29_sub3_red(f29& r, const f29& a, const f29& b, const f29& c, const f29& d) {
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a.v[i] + F::sub6p(i) - b.v[i] - c.v[i] - d.v[i] + cy;
+    r.v[i] = t & kMask29;
+    cy = t >> 29;
+  }
+  f29_fold<F>(r, a.v[8] + F::sub6p(8) - b.v[8] - c.v[8] - d.v[8] + cy);
+}
+// r = red(K a), K <= 4, a norm
+template <class F, int K>
+CDEV void f29_mulk_red(f29& r, const f29& a) {
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a.v[i] * K + cy;
+    r.v[i] = t & kMask29;
+    cy = t >> 29;
+  }
+  f29_fold<F>(r, a.v[8] * K + cy);
 }
 
 // canonical residue in [0, p), limbs fully normalised

@@ -35,6 +35,7 @@ class Fp29:
         self.m = gen.limbs29(p)
         self.minv = gen.minv29(p)
         self.s2p = gen.sub2p(p)
+        self.skp = {2: self.s2p, 4: gen.subkp(p, 4), 6: gen.subkp(p, 6)}
         self.r2 = gen.limbs29(R * R % p)
         self.one = gen.limbs29(R % p)
 
@@ -86,15 +87,12 @@ class Fp29:
         assert self.val(r) == self.val(a) + 2 * self.p - self.val(b)
         return r
 
-    def red(self, a):
-        assert all(0 <= x < U32 for x in a) and self.val(a) < 1 << 260
-        r, c = [0] * 9, 0
-        for i in range(8):
-            t = a[i] + c
-            assert t < U32
-            r[i], c = t & M29, t >> 29
-        top = a[8] + c
-        assert top < U32
+    def fold(self, r, top):
+        """fp29.hpp f29_fold: limbs 0..7 normalised, top = bits >= 2^232."""
+        assert all(0 <= x <= M29 for x in r[:8]) and 0 <= top < U32
+        v_in = self.val(r[:8] + [top])
+        assert v_in < 1 << 260
+        r = list(r)
         q = top >> 24
         r[8] = top & 0xFFFFFF
         if self.kred == 1:
@@ -112,8 +110,47 @@ class Fp29:
                 r[i + 1] += cs
         assert all(0 <= x < U32 for x in r)
         assert all(x < (1 << 29) + (1 << 15) for x in r[:8])
-        assert self.val(r) % self.p == self.val(a) % self.p and self.val(r) < 2 * self.p
+        assert self.val(r) % self.p == v_in % self.p and self.val(r) < 2 * self.p
         return r
+
+    def red(self, a):
+        assert all(0 <= x < U32 for x in a) and self.val(a) < 1 << 260
+        r, c = [0] * 9, 0
+        for i in range(8):
+            t = a[i] + c
+            assert t < U32
+            r[i], c = t & M29, t >> 29
+        top = a[8] + c
+        assert top < U32
+        return self.fold(r, top)
+
+    def subs_red(self, a, *bs):
+        """f29_sub_red / f29_sub2_red / f29_sub3_red: red(a + 2k p - sum bs) in one pass."""
+        k = 2 * len(bs)
+        s = self.skp[k]
+        for b in bs:
+            assert self.val(b) <= 2 * self.p and all(x < (1 << 29) + (1 << 15) for x in b)
+        r, c = [0] * 9, 0
+        for i in range(8):
+            t = a[i] + s[i] - sum(b[i] for b in bs) + c
+            assert 0 <= t < U32, "limb %d out of range" % i
+            r[i], c = t & M29, t >> 29
+        top = a[8] + s[8] - sum(b[8] for b in bs) + c
+        assert 0 <= top < U32
+        out = self.fold(r, top)
+        assert self.val(out) % self.p == (self.val(a) - sum(self.val(b) for b in bs)) % self.p
+        return out
+
+    def mulk_red(self, a, k):
+        """f29_mulk_red: red(k a) in one pass, a norm."""
+        r, c = [0] * 9, 0
+        for i in range(8):
+            t = a[i] * k + c
+            assert t < U32
+            r[i], c = t & M29, t >> 29
+        top = a[8] * k + c
+        assert top < U32
+        return self.fold(r, top)
 
     def canon(self, a):
         t = self.red(a)
@@ -154,31 +191,31 @@ def jdbl(F, am3, P):
     X, Y, Z = P
     if am3:
         delta, gamma = F.sqr(Z), F.sqr(Y)
-        beta = F.mul(X, gamma)
         t, u = F.sub(X, delta), F.add(X, delta)
-        a3 = F.mul(t, u)
-        a3 = F.red(F.add(F.add(a3, a3), a3))
-        x3 = F.sqr(a3)
-        t = F.add(beta, beta)
-        b4 = F.red(F.add(t, t))
-        x3 = F.red(F.sub(F.sub(x3, b4), b4))
-        t = F.sqr(F.add(Y, Z))
-        z3 = F.red(F.sub(F.sub(t, gamma), delta))
-        y3 = F.mul(a3, F.sub(b4, x3))
-        u = F.sqr(F.add(gamma, gamma))
-        y3 = F.red(F.sub(F.sub(y3, u), u))
+        beta, a3 = F.mul(X, gamma), F.mul(t, u)
+        a3 = F.mulk_red(a3, 3)
+        b4 = F.mulk_red(beta, 4)
+        yz = F.add(Y, Z)
+        x3, yz = F.sqr(a3), F.sqr(yz)
+        x3 = F.subs_red(x3, b4, b4)
+        z3 = F.subs_red(yz, gamma, delta)
+        u = F.sub(b4, x3)
+        t = F.add(gamma, gamma)
+        t, y3 = F.sqr(t), F.mul(a3, u)
+        y3 = F.subs_red(y3, t, t)
     else:
         A, B = F.sqr(X), F.sqr(Y)
-        C = F.sqr(B)
-        t = F.sub(F.sub(F.sqr(F.add(X, B)), A), C)
-        D = F.red(F.add(t, t))
-        E = F.red(F.add(F.add(A, A), A))
-        x3 = F.red(F.sub(F.sub(F.sqr(E), D), D))
+        t = F.add(X, B)
+        C, t = F.sqr(B), F.sqr(t)
+        t = F.subs_red(t, A, C)
+        D = F.mulk_red(t, 2)
+        E = F.mulk_red(A, 3)
+        t = F.add(Y, Y)
+        x3, z3 = F.sqr(E), F.mul(t, Z)
+        x3 = F.subs_red(x3, D, D)
         y3 = F.mul(E, F.sub(D, x3))
-        t = F.add(C, C)
-        u = F.red(F.add(t, t))
-        y3 = F.red(F.sub(F.sub(y3, u), u))
-        z3 = F.mul(F.add(Y, Y), Z)
+        u = F.mulk_red(C, 4)
+        y3 = F.subs_red(y3, u, u)
     return (x3, y3, z3)
 
 
@@ -211,24 +248,22 @@ def jmadd(F, am3, P, x2, y2):
     if P is None:
         return (x2, y2, list(F.one))
     X1, Y1, Z1 = P
-    z1z1 = F.sqr(Z1)
-    u2 = F.mul(x2, z1z1)
-    s2 = F.mul(F.mul(y2, Z1), z1z1)
-    h, rr = F.red(F.sub(u2, X1)), F.red(F.sub(s2, Y1))
+    z1z1, t = F.sqr(Z1), F.mul(y2, Z1)
+    u2, s2 = F.mul(x2, z1z1), F.mul(t, z1z1)
+    h, rr = F.subs_red(u2, X1), F.subs_red(s2, Y1)
     if F.iszero(h):
         return jdbl(F, am3, P) if F.iszero(rr) else None
-    hh = F.sqr(h)
+    rr = F.add(rr, rr)
+    hh, x3 = F.sqr(h), F.sqr(rr)
     i = F.add(hh, hh)
     i = F.add(i, i)
-    j = F.mul(h, i)
-    rr = F.add(rr, rr)
-    v = F.mul(X1, i)
-    x3 = F.red(F.sub(F.sub(F.sub(F.sqr(rr), j), v), v))
-    y3 = F.mul(rr, F.sub(v, x3))
-    t = F.mul(Y1, j)
-    y3 = F.red(F.sub(F.sub(y3, t), t))
-    t = F.sub(F.sub(F.sqr(F.add(Z1, h)), z1z1), hh)
-    return (x3, y3, F.red(t))
+    j, v = F.mul(h, i), F.mul(X1, i)
+    x3 = F.subs_red(x3, j, v, v)
+    t = F.sub(v, x3)
+    y3, t = F.mul(rr, t), F.mul(Y1, j)
+    y3 = F.subs_red(y3, t, t)
+    t = F.sqr(F.add(Z1, h))
+    return (x3, y3, F.subs_red(t, z1z1, hh))
 
 
 def affine(F, P):
@@ -278,6 +313,11 @@ def test_field_ops_extremes(scheme):
             F.mul(F.add(la, la), F.add(lb, lb))           # 4p x 4p
             F.sub(la, lb)
             F.red(F.add(F.add(la, la), F.add(la, la)))    # 8p, limbs < 2^31
+            m = F.mul(la, lb)                               # norm minuends / subtrahends
+            F.subs_red(m, la)
+            F.subs_red(m, la, lb)
+            F.subs_red(m, la, lb, la)
+            F.mulk_red(la, 4)
         F.sqr(F.add(la, la))
         assert F.val(F.canon(la)) == a % p
         assert F.from_mont(F.to_mont(a % p)) == a % p

@@ -58,6 +58,20 @@ def words32(x):
     return [(x >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
 
 
+def subkp(p, k):
+    """k p (k = 4, 6) as 9 limbs whose limbs 0..7 lie in [2^31 - 4, 2^31 + 2^29): each
+    borrows 2^31 (= 4 x 2^29) from the next, so up to three norm subtrahends
+    (limbs < 2^29 + 2^15) never take a limb below zero and a norm minuend plus the
+    limb stays below 2^32 (fp29.hpp f29_sub2_red / f29_sub3_red)."""
+    d = [v for v in limbs29(k * p)]
+    for i in range(8):
+        d[i] += 2**31
+        d[i + 1] -= 4
+    assert sum(v << (29 * i) for i, v in enumerate(d)) == k * p
+    assert all(2**31 - 4 <= v < 2**31 + 2**29 for v in d[:8]) and 0 <= d[8] < 2**29
+    return d
+
+
 def sub2p(p):
     """2p as 9 limbs whose limbs 0..7 are >= 2^29 - 1 (each borrows 2^29 from the next)."""
     d = [2 * v for v in limbs29(p)]
@@ -195,6 +209,8 @@ def emit_field(name, p, kred, consts, comment):
     out = ["// %s" % comment, "struct %s {" % name]
     out.append("  F29_LIMBS(m, %s)" % _hex(limbs29(p)))
     out.append("  F29_LIMBS(sub2p, %s)" % _hex(sub2p(p)))
+    out.append("  F29_LIMBS(sub4p, %s)" % _hex(subkp(p, 4)))
+    out.append("  F29_LIMBS(sub6p, %s)" % _hex(subkp(p, 6)))
     out.append("  F29_LIMBS(r2, %s)  // R^2 mod p" % _hex(limbs29(R * R % p)))
     out.append("  F29_LIMBS(one, %s)  // R mod p" % _hex(limbs29(R % p)))
     for tag, v in consts:
