@@ -323,8 +323,14 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
 }
 
 // ---- G tables: entry k (0..128) = [k]G affine (Montgomery, canonical) ------
-// tables [0, 129) = [k]G and, for secp256k1, [129, 258) = [k](lambda G) = (beta x, y)
-static constexpr int kGEntries = 129;
+// Booth windows of kGBits over the fixed base: 12-bit digits (|d| <= 2048) cut
+// the ladder's G additions from 32 to 22 (P-256) and from 34 to 22 (secp256k1's
+// two 129-bit halves) for tables of 2049 affine entries (164 KB each, resident
+// in L2); the window is a multiple of the 4-bit Q window so both share the
+// doublings. Tables [0, kGEntries) = [k]G and, for secp256k1,
+// [kGEntries, 2 kGEntries) = [k](lambda G) = (beta x, y).
+static constexpr int kGBits = 12;
+static constexpr int kGEntries = (1 << (kGBits - 1)) + 1;
 static constexpr int kGEntryWords = 20;  // x[9], y[9], 2 pad: five 16-B loads
 static constexpr int kGTables = 2;
 
@@ -347,7 +353,7 @@ __global__ void __launch_bounds__(64) ecdsa_gtable_kernel(uint32_t* __restrict__
   f29_const_one<F>(G.Z);
   G.inf = false;
   R.inf = true;
-  for (int bit = 7; bit >= 0; bit--) {
+  for (int bit = kGBits - 1; bit >= 0; bit--) {
     jdbl<C>(R, R);
     if ((k >> bit) & 1) jadd<C>(R, R, G);
   }
@@ -727,8 +733,8 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
         f29_cneg<F>(y2, (d2 < 0) != nb2);
         jmadd<C>(acc, acc, x2, y2);
       }
-      if ((j & 1) == 0) {
-        const int g1 = booth_digit<8>(a1.v, j >> 1), g2 = booth_digit<8>(a2.v, j >> 1);
+      if (j % (kGBits / 4) == 0) {
+        const int g1 = booth_digit<kGBits>(a1.v, j / (kGBits / 4)), g2 = booth_digit<kGBits>(a2.v, j / (kGBits / 4));
         f29 gx, gy;
         if (g1) {
           load_g(gx, gy, gtab, g1 < 0 ? -g1 : g1);
@@ -761,8 +767,8 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
         f29_cneg<F>(ty, (dq < 0) != neg2);
         jmadd<C>(acc, acc, tx, ty);
       }
-      if ((j & 1) == 0) {
-        const int dg = booth_digit<8>(u1.v, j >> 1);
+      if (j % (kGBits / 4) == 0) {
+        const int dg = booth_digit<kGBits>(u1.v, j / (kGBits / 4));
         if (dg) {
           f29 gx, gy;
           load_g(gx, gy, gtab, dg < 0 ? -dg : dg);
