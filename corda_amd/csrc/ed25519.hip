@@ -46,35 +46,19 @@ CDEV void ge_base(ge_p3& b) {
   fe_set(b.Z, 1);
 }
 
-// B' = [2^128]B (second fixed base of the half-size-scalar ladder)
-CDEV void ge_base128(ge_p3& b) {
-  const uint32_t bx[10] = {0xb7e824, 0x11eb98, 0x7cbf90, 0x4e1739, 0x2639a17,
-                           0x14e29a0, 0x29cc270, 0x6592a5, 0x3f3c45f, 0x1309ebf};
-  const uint32_t by[10] = {0x3f5a66b, 0xaf4452, 0x93cb77, 0xf28d26, 0x24342f8,
-                           0xc29c3a, 0x8f5b13, 0x10fb2be, 0x26526dc, 0x17cb267};
-  const uint32_t bt[10] = {0x2f1338a, 0x1cc7251, 0x1b53d3c, 0x13331d, 0x51e192,
-                           0x1924b6a, 0xab0003, 0x5fa9c, 0x3d0bf46, 0x168593};
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    b.X.v[i] = bx[i];
-    b.Y.v[i] = by[i];
-    b.T.v[i] = bt[i];
-  }
-  fe_set(b.Z, 1);
-}
-
-// tab: entries [0, 129) = [k]B, entries [129, 258) = [k]B'
+// tab: entries [0, kBTableEntries) = [k]B, then [k]B' with B' = [2^132]B
 __global__ void __launch_bounds__(64) ed25519_btable_kernel(uint32_t* __restrict__ tab) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= 2 * kBTableEntries) return;
   const int k = g % kBTableEntries;
   ge_p3 B, P;
-  if (g < kBTableEntries) ge_base(B);
-  else ge_base128(B);
+  ge_base(B);
+  if (g >= kBTableEntries)
+    for (int t = 0; t < kBDigits * kBBits; t++) ge_dbl<true>(B, B);
   ge_cached bc;
   ge_to_cached(bc, B);
   ge_identity(P);
-  for (int bit = 7; bit >= 0; bit--) {
+  for (int bit = kBBits - 1; bit >= 0; bit--) {
     ge_dbl<true>(P, P);
     if ((k >> bit) & 1) ge_add<true>(P, P, bc);
   }
@@ -100,24 +84,6 @@ __global__ void __launch_bounds__(64) ed25519_btable_kernel(uint32_t* __restrict
   o[31] = 0;
 }
 
-CDEV void load_niels(ge_niels& n, const uint32_t* __restrict__ tab, int idx) {
-  const uint4* e = reinterpret_cast<const uint4*>(tab + idx * kBEntryWords);
-  uint32_t w[32];
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    const uint4 v = e[q];
-    w[4 * q] = v.x;
-    w[4 * q + 1] = v.y;
-    w[4 * q + 2] = v.z;
-    w[4 * q + 3] = v.w;
-  }
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    n.ypx.v[i] = w[i];
-    n.ymx.v[i] = w[10 + i];
-    n.xy2d.v[i] = w[20 + i];
-  }
-}
 
 // ---------------------------------------------------------------------------
 // SHA-512 over  seg0(32 B, registers) || seg1(32 B, registers, optional) || msg

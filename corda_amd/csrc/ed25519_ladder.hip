@@ -7,8 +7,8 @@
 // half-size scalars (T. Pornin, ePrint 2020/454; the equivalence argument is in
 // ed25519.hip above half_scalars). 4-bit Booth windows over the per-lane
 // [0..8](-A), [0..8](-R) tables (gathered from the workspace one window ahead,
-// so the four doublings hide the load), 8-bit Booth windows over B and
-// B' = [2^128]B from LDS. Digit positions are the same in every lane, so the
+// so the four doublings hide the load), 12-bit Booth windows over B and
+// B' = [2^132]B from L2-resident tables. Digit positions are the same in every lane, so the
 // ladder never diverges; P == O is X == 0 and Y == Z (no inversion).
 // Verdict word per wave by ballot.
 // field products in hand-scheduled pairs (ge25519.hpp fe_mul_pair, fe25519_asm.hpp)
@@ -23,25 +23,6 @@
 
 namespace cordahip {
 
-CDEV void lds_niels(ge_niels& n, const uint32_t* lds, int idx) {
-  const uint4* e = reinterpret_cast<const uint4*>(lds + idx * kLdsBStride);
-  uint32_t w[32];
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    const uint4 v = e[q];
-    w[4 * q] = v.x;
-    w[4 * q + 1] = v.y;
-    w[4 * q + 2] = v.z;
-    w[4 * q + 3] = v.w;
-  }
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    n.ypx.v[i] = w[i];
-    n.ymx.v[i] = w[10 + i];
-    n.xy2d.v[i] = w[20 + i];
-  }
-}
-
 // waves per SIMD the register allocation targets (2: up to 256 VGPRs)
 #ifndef ED_LADDER_WAVES
 #define ED_LADDER_WAVES 2
@@ -50,12 +31,6 @@ CDEV void lds_niels(ge_niels& n, const uint32_t* lds, int idx) {
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_LADDER_WAVES))) ed25519_ladder_half_kernel(
     uint64_t base, uint64_t m, const uint32_t* __restrict__ btab, const uint32_t* __restrict__ ws,
     uint8_t* __restrict__ status, unsigned long long* __restrict__ verdict) {
-  __shared__ __attribute__((aligned(16))) uint32_t bl[2 * kBTableEntries * kLdsBStride];
-  for (int t = threadIdx.x; t < 2 * kBTableEntries * 8; t += blockDim.x) {
-    const int e = t >> 3, q = t & 7;
-    reinterpret_cast<uint4*>(bl + e * kLdsBStride)[q] = reinterpret_cast<const uint4*>(btab + e * kBEntryWords)[q];
-  }
-  __syncthreads();
   const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = li < m;
   const uint64_t lc = active ? li : m - 1;  // inactive lanes replay the last record, discard it
@@ -66,8 +41,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_LAD
   load8(e, rec + kWhE);
   const bool c0neg = rec[kWhFlags] & 1u;  // [c0](-A) with c0 < 0 is [|c0|]A: flip the digit signs
   const int bits = max(mp8_bitlen(ka), mp8_bitlen(kr));
-  const int W = max(wave_max((bits + 1 + 3) / 4), 1);
-  const uint32_t* bl128 = bl + kBTableEntries * kLdsBStride;
+  // at least the windows the fixed-base digits need (e's low half: 11 digits
+  // of 12 bits = windows 0..30); |c0|, c1 ~ 2^128 give 33
+  const int W = max(wave_max((bits + 1 + 3) / 4), (kBDigits - 1) * (kBBits / 4) + 1);
+  const uint32_t* btab2 = btab + kBTableEntries * kBEntryWords;
   ge_p3 P;
   ge_identity(P);
   for (int j = W - 1; j >= 0; j--) {
@@ -83,17 +60,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_LAD
     }
     cached_cneg(ca, (da < 0) != c0neg);
     ge_add<true>(P, P, ca);
+    // fixed-base window: the L2 gather of each niels entry is issued one
+    // addition ahead of its use (registers allow no more)
+    // (W is the wave's maximum and may exceed 33: the low half's windows end at
+    // digit kBDigits - 1, the high half's digits ride on B')
+    const bool bwin = j % (kBBits / 4) == 0 && j < kBDigits * (kBBits / 4);
     cached_cneg(cr, dr < 0);
-    if ((j & 1) == 0 && j < 32) {
+    if (bwin) {
+      const int d0 = booth_digit<kBBits>(e, j / (kBBits / 4));
+      const int d1 = booth_digit<kBBits>(e, j / (kBBits / 4) + kBDigits);
+      ge_niels nb0, nb1;
+      load_niels(nb0, btab, d0 < 0 ? -d0 : d0);
       ge_add<true>(P, P, cr);
-      const int d0 = booth_digit<8>(e, j >> 1), d1 = booth_digit<8>(e, (j >> 1) + 16);
-      ge_niels nb;
-      lds_niels(nb, bl, d0 < 0 ? -d0 : d0);
-      niels_cneg(nb, d0 < 0);
-      ge_madd<true>(P, P, nb);
-      lds_niels(nb, bl128, d1 < 0 ? -d1 : d1);
-      niels_cneg(nb, d1 < 0);
-      ge_madd<false>(P, P, nb);
+      load_niels(nb1, btab2, d1 < 0 ? -d1 : d1);
+      niels_cneg(nb0, d0 < 0);
+      ge_madd<true>(P, P, nb0);
+      niels_cneg(nb1, d1 < 0);
+      ge_madd<false>(P, P, nb1);
     } else {
       ge_add<false>(P, P, cr);
     }

@@ -18,11 +18,16 @@
 
 namespace cordahip {
 
-// B table: entry k (0..128) = [k]B as affine niels (y+x, y-x, 2d*x*y); 32
-// u32 per entry (30 limbs + 2 pad); entries [129, 258) = [k]B', B' = [2^128]B.
-static constexpr int kBTableEntries = 129;
+// B tables for Booth windows of kBBits over e = e_lo + 2^132 e_hi: entry k
+// (0..2048) = [k]B as affine niels (y+x, y-x, 2d*x*y), 32 u32 per entry (30
+// limbs + 2 pad); entries [kBTableEntries, 2 kBTableEntries) = [k]B',
+// B' = [2^(11 kBBits)]B = [2^132]B. 2 x 256 KB, resident in L2. 12-bit windows
+// give 22 fixed-base additions per verification (8-bit ones from LDS: 32); the
+// window is a multiple of the ladder's 4-bit one so both share the doublings.
+static constexpr int kBBits = 12;
+static constexpr int kBDigits = 11;  // per half: 11 x 12 = 132 bits
+static constexpr int kBTableEntries = (1 << (kBBits - 1)) + 1;
 static constexpr int kBEntryWords = 32;
-static constexpr int kLdsBStride = 36;  // words per B entry in LDS (bank spread)
 static constexpr uint8_t kStatusPending = 0xff;
 
 // Per-lane workspace record (2,992 B, 16-B aligned fields):
@@ -33,6 +38,25 @@ static constexpr int kWhKr = kWhKa + 8;
 static constexpr int kWhE = kWhKa + 16;
 static constexpr int kWhFlags = kWhKa + 24;      // bit 0: c0 < 0
 static constexpr int kWhLaneWords = kWhKa + 28;  // 748 words
+
+CDEV void load_niels(ge_niels& n, const uint32_t* __restrict__ tab, int idx) {
+  const uint4* e = reinterpret_cast<const uint4*>(tab + idx * kBEntryWords);
+  uint32_t w[32];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint4 v = e[q];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    n.ypx.v[i] = w[i];
+    n.ymx.v[i] = w[10 + i];
+    n.xy2d.v[i] = w[20 + i];
+  }
+}
 
 // conditional negation of a niels / cached point: swap (y+x, y-x), negate t
 CDEV void niels_cneg(ge_niels& n, bool neg) {
