@@ -6,11 +6,10 @@
 //                       h mod L, S_eff, lattice reduction -> workspace record
 //   ed25519_ladder.hip  ladder: [e]B + [c0](+-A) + [c1](-R) == O, verdict ballot
 //
-// The two live in separate translation units so each gets the field-multiply
-// instruction shape that suits it (fe25519.hpp FE_ASM_MAC): prep is dominated
-// by the serial square chains of two decompressions (latency-bound: column
-// sums re-associated for ILP), the ladder by independent products of the
-// group formulas (throughput-bound: carries ride in the MAC addend).
+// The two live in separate translation units, each register-allocated for its
+// own shape: prep is dominated by the two decompressions' square chains (run as
+// one paired chain), the ladder by the group formulas' independent products;
+// both issue those products as generated asm pairs (fe25519_asm.hpp).
 #pragma once
 #include "fe25519.hpp"
 #include "ge25519.hpp"

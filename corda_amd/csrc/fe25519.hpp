@@ -102,33 +102,14 @@ CDEV void fe_cmov(fe& r, const fe& a, bool c) {
   for (int i = 0; i < 10; i++) r.v[i] = c ? a.v[i] : r.v[i];
 }
 
-CDEV void fe_carry64(fe& r, uint64_t h[10]) {
-  uint64_t c;
-  c = h[0] >> 26; h[1] += c; h[0] &= M26;
-  c = h[4] >> 26; h[5] += c; h[4] &= M26;
-  c = h[1] >> 25; h[2] += c; h[1] &= M25;
-  c = h[5] >> 25; h[6] += c; h[5] &= M25;
-  c = h[2] >> 26; h[3] += c; h[2] &= M26;
-  c = h[6] >> 26; h[7] += c; h[6] &= M26;
-  c = h[3] >> 25; h[4] += c; h[3] &= M25;
-  c = h[7] >> 25; h[8] += c; h[7] &= M25;
-  c = h[4] >> 26; h[5] += c; h[4] &= M26;
-  c = h[8] >> 26; h[9] += c; h[8] &= M26;
-  c = h[9] >> 25; h[9] &= M25; h[0] += c * 19;
-  c = h[0] >> 26; h[0] &= M26; h[1] += c;
-#pragma unroll
-  for (int i = 0; i < 10; i++) r.v[i] = (uint32_t)h[i];
-}
-
-// Carry-chained column reduction (default, FE_CARRY_CHAIN != 0): column k's
-// 64-bit accumulator STARTS at the carry out of column k-1, so the carry
-// costs no add (it rides in v_mad_u64_u32's 64-bit addend) — one shift and
-// one mask per limb, plus one fold of 19 * carry(limb 9) into limbs 0/1.
-// Bounds: column sums < 2^62.5 plus a carry < 2^38; the final carry c < 2^38,
-// 19c < 2^42.3, so limb 1 grows by < 2^16.4 -> output tight.
-#ifndef FE_CARRY_CHAIN
-#define FE_CARRY_CHAIN 1
-#endif
+// Carry-chained column reduction: column k's 64-bit accumulator STARTS at the
+// carry out of column k-1, so the carry costs no add (it rides in
+// v_mad_u64_u32's 64-bit addend) — one shift and one mask per limb, plus one
+// fold of 19 * carry(limb 9) into limbs 0/1. Bounds: column sums < 2^62.5 plus
+// a carry < 2^38; the final carry c < 2^38, 19c < 2^42.3, so limb 1 grows by
+// < 2^16.4 -> output tight. (LLVM still re-associates the carry into an extra
+// 64-bit add per column; the group formulas' paired products avoid that with
+// generated asm, fe25519_asm.hpp.)
 
 // 19 * x, opaque to LLVM: with a visible constant factor InstCombine
 // factors sums of wrapped products as 19 * (64-bit sum), which costs a 64x32
@@ -139,27 +120,7 @@ CDEV uint32_t mul19(uint32_t x) {
   return r;
 }
 
-// acc + a * b as ONE v_mad_u64_u32 the compiler cannot re-associate. With
-// plain C++ LLVM starts every column at 0 (for ILP) and adds the incoming
-// carry at the end with a separate 64-bit add -- one extra VALU op per column.
-// Opaque MACs keep the carry as the chain's initial addend; the independent
-// multiplications of a group operation supply the ILP instead.
-#ifndef FE_ASM_MAC
-#define FE_ASM_MAC 0  // 1 measured: microbench +2-6%, full C2 -4% (192.2 vs 184.9 ms); kept for A/B
-#endif
-CDEV uint64_t mac64(uint32_t a, uint32_t b, uint64_t acc) {
-#if FE_ASM_MAC == 2
-  uint64_t r;
-  asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(acc) : "vcc");
-  return r;
-#elif FE_ASM_MAC == 1
-  uint64_t r = acc + (uint64_t)a * b;
-  asm("" : "+v"(r));  // empty: only pins the association order
-  return r;
-#else
-  return acc + (uint64_t)a * b;
-#endif
-}
+CDEV uint64_t mac64(uint32_t a, uint32_t b, uint64_t acc) { return acc + (uint64_t)a * b; }
 
 CDEV void fe_fold_top(fe& r, uint64_t c) {
   const uint64_t t = (uint64_t)r.v[0] + c * 19u;
@@ -167,54 +128,9 @@ CDEV void fe_fold_top(fe& r, uint64_t c) {
   r.v[1] += (uint32_t)(t >> 26);
 }
 
-// Term-major accumulation (FE_TERM_MAJOR): the ten 64-bit column sums grow
-// side by side, term t of every column before term t+1 of any, so the wave's
-// instruction stream holds ten independent v_mad_u64_u32 chains instead of one
-// dependent chain per column (a dependent v_mad_u64_u32 waits ~12 cycles; an
-// independent one issues every ~4). One sequential carry pass follows: per
-// column an and, a 64-bit shift and a 64-bit add (the same count as the
-// carry-chained form's and + shift + re-associated add).
-#ifndef FE_TERM_MAJOR
-#define FE_TERM_MAJOR 0
-#endif
-CDEV void fe_carry_cols(fe& o, uint64_t h[10]) {
-  uint64_t c = 0;
-#pragma unroll
-  for (int k = 0; k < 10; k++) {
-    const uint64_t a = h[k] + c;
-    o.v[k] = (uint32_t)a & ((k & 1) ? M25 : M26);
-    c = a >> limb_bits(k);
-  }
-  fe_fold_top(o, c);
-}
-
 // h = f * g. Column k collects f_i g_j with i + j == k (mod 10); wrapped
 // terms carry 2^255 == 19, and odd*odd terms carry an extra 2 (radix 2^25.5).
 CDEV void fe_mul(fe& r, const fe& f, const fe& g) {
-#if FE_TERM_MAJOR
-  uint32_t g19[10], f2[10];
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    g19[i] = mul19(g.v[i]);
-    f2[i] = f.v[i] << 1;
-  }
-  uint64_t h[10];
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-#pragma unroll
-    for (int k = 0; k < 10; k++) {
-      const int j = (k - i + 10) % 10;
-      const bool wrap = (i + j) >= 10;
-      const bool oo = (i & 1) && (j & 1);
-      const uint32_t a = oo ? f2[i] : f.v[i];
-      const uint32_t b = wrap ? g19[j] : g.v[j];
-      h[k] = i == 0 ? (uint64_t)a * b : mac64(a, b, h[k]);
-    }
-  }
-  fe o;
-  fe_carry_cols(o, h);
-  r = o;
-#elif FE_CARRY_CHAIN
   uint32_t g19[10], f2[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
@@ -240,30 +156,6 @@ CDEV void fe_mul(fe& r, const fe& f, const fe& g) {
   }
   fe_fold_top(o, c);
   r = o;  // r may alias f or g
-#else
-  uint32_t g19[10], f2[10];
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    g19[i] = mul19(g.v[i]);
-    f2[i] = f.v[i] << 1;
-  }
-  uint64_t h[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) {
-    uint64_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-      const int j = (k - i + 10) % 10;
-      const bool wrap = (i + j) >= 10;
-      const bool oo = (i & 1) && (j & 1);
-      const uint32_t a = oo ? f2[i] : f.v[i];
-      const uint32_t b = wrap ? g19[j] : g.v[j];
-      acc += (uint64_t)a * b;
-    }
-    h[k] = acc;
-  }
-  fe_carry64(r, h);
-#endif
 }
 
 // h = f^2 (55 products)
@@ -275,37 +167,6 @@ CDEV void fe_sq(fe& r, const fe& f) {
     f4[i] = f.v[i] << 2;
     f19[i] = mul19(f.v[i]);
   }
-#if FE_TERM_MAJOR
-  // term-major over the (i, j >= i) pairs of each column: step t adds the t-th
-  // pair of every column that has one (columns hold 5 or 6 pairs)
-  uint64_t h[10];
-  bool started[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) started[k] = false;
-#pragma unroll
-  for (int t = 0; t < 6; t++) {
-#pragma unroll
-    for (int k = 0; k < 10; k++) {
-      int cnt = 0;
-#pragma unroll
-      for (int i = 0; i < 10; i++) {
-        const int j = (k - i + 10) % 10;
-        if (j < i) continue;
-        if (cnt++ != t) continue;
-        const bool wrap = (i + j) >= 10;
-        const bool oo = (i & 1) && (j & 1);
-        const int mult = (i < j ? 2 : 1) * (oo ? 2 : 1);  // 1, 2 or 4
-        const uint32_t a = mult == 1 ? f.v[i] : (mult == 2 ? f2[i] : f4[i]);
-        const uint32_t b = wrap ? f19[j] : f.v[j];
-        h[k] = started[k] ? mac64(a, b, h[k]) : (uint64_t)a * b;
-        started[k] = true;
-      }
-    }
-  }
-  fe o;
-  fe_carry_cols(o, h);
-  r = o;
-#elif FE_CARRY_CHAIN
   fe o;
   uint64_t c = 0;
 #pragma unroll
@@ -327,26 +188,6 @@ CDEV void fe_sq(fe& r, const fe& f) {
   }
   fe_fold_top(o, c);
   r = o;  // r may alias f or g
-#else
-  uint64_t h[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) {
-    uint64_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-      const int j = (k - i + 10) % 10;
-      if (j < i) continue;
-      const bool wrap = (i + j) >= 10;
-      const bool oo = (i & 1) && (j & 1);
-      const int mult = (i < j ? 2 : 1) * (oo ? 2 : 1);  // 1, 2 or 4
-      const uint32_t a = mult == 1 ? f.v[i] : (mult == 2 ? f2[i] : f4[i]);
-      const uint32_t b = wrap ? f19[j] : f.v[j];
-      acc += (uint64_t)a * b;
-    }
-    h[k] = acc;
-  }
-  fe_carry64(r, h);
-#endif
 }
 
 // n squarings, kept as a loop: a fully unrolled chain lets the scheduler
