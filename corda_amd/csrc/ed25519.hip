@@ -46,7 +46,7 @@ CDEV void ge_base(ge_p3& b) {
   fe_set(b.Z, 1);
 }
 
-// tab: entries [0, kBTableEntries) = [k]B, then [k]B' with B' = [2^132]B
+// tab: entries [0, kBTableEntries) = [k]B, then [k]B' with B' = [2^128]B
 __global__ void __launch_bounds__(64) ed25519_btable_kernel(uint32_t* __restrict__ tab) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= 2 * kBTableEntries) return;

@@ -7,8 +7,8 @@
 // half-size scalars (T. Pornin, ePrint 2020/454; the equivalence argument is in
 // ed25519.hip above half_scalars). 4-bit Booth windows over the per-lane
 // [0..8](-A), [0..8](-R) tables (gathered from the workspace one window ahead,
-// so the four doublings hide the load), 12-bit Booth windows over B and
-// B' = [2^132]B from L2-resident tables. Digit positions are the same in every lane, so the
+// so the four doublings hide the load), 16-bit Booth windows over B and
+// B' = [2^128]B from L2/MALL-resident tables (ed25519_ws.hpp). Digit positions are the same in every lane, so the
 // ladder never diverges; P == O is X == 0 and Y == Z (no inversion).
 // Verdict word per wave by ballot.
 // field products in hand-scheduled pairs (ge25519.hpp fe_mul_pair, fe25519_asm.hpp)
@@ -41,8 +41,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_LAD
   load8(e, rec + kWhE);
   const bool c0neg = rec[kWhFlags] & 1u;  // [c0](-A) with c0 < 0 is [|c0|]A: flip the digit signs
   const int bits = max(mp8_bitlen(ka), mp8_bitlen(kr));
-  // at least the windows the fixed-base digits need (e's low half: 11 digits
-  // of 12 bits = windows 0..30); |c0|, c1 ~ 2^128 give 33
+  // at least the windows the fixed-base digits need (e's low half: kBDigits
+  // digits of kBBits bits); |c0|, c1 ~ 2^128 give 33
   const int W = max(wave_max((bits + 1 + 3) / 4), (kBDigits - 1) * (kBBits / 4) + 1);
   const uint32_t* btab2 = btab + kBTableEntries * kBEntryWords;
   ge_p3 P;

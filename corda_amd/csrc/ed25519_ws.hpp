@@ -17,14 +17,15 @@
 
 namespace cordahip {
 
-// B tables for Booth windows of kBBits over e = e_lo + 2^132 e_hi: entry k
-// (0..2048) = [k]B as affine niels (y+x, y-x, 2d*x*y), 32 u32 per entry (30
+// B tables for Booth windows of kBBits over e = e_lo + 2^128 e_hi: entry k
+// (0..2^15) = [k]B as affine niels (y+x, y-x, 2d*x*y), 32 u32 per entry (30
 // limbs + 2 pad); entries [kBTableEntries, 2 kBTableEntries) = [k]B',
-// B' = [2^(11 kBBits)]B = [2^132]B. 2 x 256 KB, resident in L2. 12-bit windows
-// give 22 fixed-base additions per verification (8-bit ones from LDS: 32); the
-// window is a multiple of the ladder's 4-bit one so both share the doublings.
-static constexpr int kBBits = 12;
-static constexpr int kBDigits = 11;  // per half: 11 x 12 = 132 bits
+// B' = [2^(kBDigits kBBits)]B = [2^128]B. 2 x 4.2 MB, L2/MALL-resident. 16-bit
+// windows give 16 fixed-base additions per verification (12-bit: 22, 8-bit
+// from LDS: 32; profiles/r02_c2_bwin12_ab.json); the window is a multiple of
+// the ladder's 4-bit one so both share the doublings.
+static constexpr int kBBits = 16;
+static constexpr int kBDigits = 8;  // per half: 8 x 16 = 128 bits
 static constexpr int kBTableEntries = (1 << (kBBits - 1)) + 1;
 static constexpr int kBEntryWords = 32;
 static constexpr uint8_t kStatusPending = 0xff;
