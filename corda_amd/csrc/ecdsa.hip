@@ -511,7 +511,7 @@ static constexpr int kEcR = kEcE + 8;           // r
 static constexpr int kEcZ = kEcR + 8;           // prod of the table's Z (k = 2..8), Montgomery mod p (12 words)
 static constexpr int kEcZW = kEcZ + 12;         // prefix products, then that product's inverse (12 words)
 static constexpr int kEcWords = kEcZW + 12;     // 280 words = 1120 B
-static constexpr int kEcInvBatch = 16;          // signatures per thread in the batch inversion
+static constexpr int kEcInvBatch = 64;          // signatures per thread in the batch inversion
 static constexpr uint8_t kEcPending = 0xff;     // slot whose verdict the ladder decides
 
 CDEV void st256(uint32_t* __restrict__ o, const u256& v) {
