@@ -16,7 +16,9 @@ Other workloads (`--workload`), same contract, used for profiling the other rows
 Contract: `python bench.py --gpus N --steps K --warmup W` (N > 1 under
 torch.distributed.run, one rank per GPU); rank 0 prints ONE JSON line.
 Weak scaling: every rank verifies its own batch; value = all ranks'
-verifications / max-over-ranks wall time of the K timed steps.
+verifications / max-over-ranks wall time of the K timed steps. C5 also has a
+strong-scaling mode, `--global-log2 G` (a fixed 2^28 stream split
+over the ranks; "scaling": "strong").
 """
 from __future__ import annotations
 
@@ -374,16 +376,32 @@ class C5:
         self.exp_ed, self.exp_ec = self.exp_ed.cpu(), self.exp_ec.cpu()
         del pubs, sigs, msgs, scheme, keys, key_len, esigs, sig_len, emsgs
         self.n_ed, self.n_ec = n_ed, n_ec
-        self.units = n
+        # strong scaling (--global-log2 G): the rank's share of a fixed 2^G batch
+        # is its 2^batch_log2 corpus streamed `passes` times per step
+        self.passes = 1
+        if args.global_log2:
+            world = int(os.environ.get("WORLD_SIZE", "1"))
+            share = (1 << args.global_log2) // world
+            if share % n:
+                raise SystemExit("--global-log2: 2^%d / %d ranks is not a multiple of 2^%d"
+                                 % (args.global_log2, world, args.batch_log2))
+            self.passes = share // n
+        self.units = n * self.passes
         self.macs = (n_ed * LIMB_MACS["ed25519"] + n_ec * (LIMB_MACS["p256"] + LIMB_MACS["secp256k1"]) // 2) // n
         self.workload = ("C5: verifier-module queue drain, 2^%d mixed sigs per GPU per step (80%% Ed25519, 10%% P-256, "
                          "10%% secp256k1, 1%% corrupted) streamed from pinned host memory, H2D/D2H included"
                          % args.batch_log2)
         self.data = "synthetic: C2 and C3 corpora (GPU-signed), copied to pinned host memory before timing"
-        self.config = {"batch_per_gpu": n, "ed25519": n_ed, "ecdsa": n_ec, "chunk": 1 << 22, "stages": 3}
+        self.config = {"batch_per_gpu": n * self.passes, "ed25519": n_ed, "ecdsa": n_ec, "chunk": 1 << 22,
+                       "stages": 3}
+        if args.global_log2:
+            self.workload += "; strong scaling: a fixed 2^%d global batch, this rank's share = %d passes" % (
+                args.global_log2, self.passes)
+            self.config["global_batch"] = 1 << args.global_log2
 
     def step(self):
-        self.eng.stream_verify(self.ed, self.ec)
+        for _ in range(self.passes):
+            self.eng.stream_verify(self.ed, self.ec)
 
     def check(self):
         from corda_amd.corpus import REJECT_ANY
@@ -440,7 +458,11 @@ def main():
     ap.add_argument("--c4-txs", type=int, default=10_000_000 // 8)
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--global-log2", type=int, default=None,
+                    help="C5 only: strong scaling over a fixed 2^G global batch (SURVEY 8d C5: G = 28)")
     args = ap.parse_args()
+    if args.global_log2 and args.workload != "c5":
+        ap.error("--global-log2 applies to --workload c5")
     if args.batch_log2 is None:
         args.batch_log2 = 20 if args.workload == "c1" else 24
 
@@ -521,7 +543,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_log2 else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": wl.data,
