@@ -15,6 +15,9 @@
 //     and the per-lane tables [0..8](-A), [0..8](-R) -> HBM workspace record;
 //   ed25519_ladder_half_kernel (ed25519_ladder.hip): [e]B + [c0](+-A) + [c1](-R) == O.
 // field products in hand-scheduled pairs (ge25519.hpp fe_mul_pair, fe25519_asm.hpp)
+#ifndef FE_QUAD
+#define FE_QUAD 0  // prep keeps pairs (register pressure)
+#endif
 #ifndef FE_USE_ASM2
 #define FE_USE_ASM2 1
 #endif

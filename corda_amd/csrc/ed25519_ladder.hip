@@ -23,6 +23,22 @@
 
 namespace cordahip {
 
+// booth_digit (sc25519.hpp) over a scalar stored word-major in LDS: word w of
+// this thread's scalar at col[w * 256]
+template <int W>
+CDEV int booth_digit_col(const uint32_t* col, int j) {
+  const int lo = W * j - 1;  // may be -1
+  uint32_t v;
+  if (lo < 0) {
+    v = (col[0] << 1) & ((1u << (W + 1)) - 1);
+  } else {
+    const int w = lo >> 5, sh = lo & 31;
+    const uint64_t hi = w + 1 <= 7 ? col[(w + 1) * 256] : 0u;
+    v = (uint32_t)(((hi << 32) | col[w * 256]) >> sh) & ((1u << (W + 1)) - 1);
+  }
+  return (int)((v + 1) >> 1) - (int)((v >> W) << W);
+}
+
 // waves per SIMD the register allocation targets (2: up to 256 VGPRs)
 #ifndef ED_LADDER_WAVES
 #define ED_LADDER_WAVES 2
@@ -35,12 +51,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_LAD
   const bool active = li < m;
   const uint64_t lc = active ? li : m - 1;  // inactive lanes replay the last record, discard it
   const uint32_t* rec = ws + lc * kWhLaneWords;
-  uint32_t ka[8], kr[8], e[8];
-  load8(ka, rec + kWhKa);
-  load8(kr, rec + kWhKr);
-  load8(e, rec + kWhE);
+  // |c0|, c1 and e live in LDS (word-major, one column per thread): each window
+  // reads two words of each, and the 24 VGPRs they would pin across the loop
+  // go to the group formulas' wider product blocks instead
+  __shared__ uint32_t sk[24][256];
+  const uint32_t* ska = &sk[0][threadIdx.x];
+  const uint32_t* skr = &sk[8][threadIdx.x];
+  const uint32_t* ske = &sk[16][threadIdx.x];
+  int bits;
+  {
+    uint32_t ka[8], kr[8], e[8];
+    load8(ka, rec + kWhKa);
+    load8(kr, rec + kWhKr);
+    load8(e, rec + kWhE);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      sk[q][threadIdx.x] = ka[q];
+      sk[8 + q][threadIdx.x] = kr[q];
+      sk[16 + q][threadIdx.x] = e[q];
+    }
+    bits = max(mp8_bitlen(ka), mp8_bitlen(kr));
+  }
   const bool c0neg = rec[kWhFlags] & 1u;  // [c0](-A) with c0 < 0 is [|c0|]A: flip the digit signs
-  const int bits = max(mp8_bitlen(ka), mp8_bitlen(kr));
   // at least the windows the fixed-base digits need (e's low half: kBDigits
   // digits of kBBits bits); |c0|, c1 ~ 2^128 give 33
   const int W = max(wave_max((bits + 1 + 3) / 4), (kBDigits - 1) * (kBBits / 4) + 1);
@@ -48,7 +80,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_LAD
   ge_p3 P;
   ge_identity(P);
   for (int j = W - 1; j >= 0; j--) {
-    const int da = booth_digit<4>(ka, j), dr = booth_digit<4>(kr, j);
+    const int da = booth_digit_col<4>(ska, j), dr = booth_digit_col<4>(skr, j);
     ge_cached ca, cr;  // issued before the doublings, consumed after them
     load_cached(ca, rec + kWhTabA + 40 * (da < 0 ? -da : da));
     load_cached(cr, rec + kWhTabR + 40 * (dr < 0 ? -dr : dr));
@@ -67,8 +99,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_LAD
     const bool bwin = j % (kBBits / 4) == 0 && j < kBDigits * (kBBits / 4);
     cached_cneg(cr, dr < 0);
     if (bwin) {
-      const int d0 = booth_digit<kBBits>(e, j / (kBBits / 4));
-      const int d1 = booth_digit<kBBits>(e, j / (kBBits / 4) + kBDigits);
+      const int d0 = booth_digit_col<kBBits>(ske, j / (kBBits / 4));
+      const int d1 = booth_digit_col<kBBits>(ske, j / (kBBits / 4) + kBDigits);
       ge_niels nb0, nb1;
       load_niels(nb0, btab, d0 < 0 ? -d0 : d0);
       ge_add<true>(P, P, cr);

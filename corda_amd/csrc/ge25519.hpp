@@ -43,6 +43,39 @@ CDEV void fe_sq_pair(fe& r0, const fe& f0, fe& r1, const fe& f1) {
 #endif
 }
 
+// Three and four independent products (the additions' first stage and every
+// formula's output stage): with FE_USE_ASM2 and FE_QUAD (per translation unit;
+// the ladder's) one asm block with three / four interleaved chains
+// (fe25519_asm.hpp: two chains per wave leave the dependent v_mad_u64_u32
+// latency partly exposed at two waves per SIMD; +1% on C2,
+// profiles/r02_c2_quad_ab.json). The prep keeps pairs (register pressure).
+#ifndef FE_QUAD
+#define FE_QUAD 1
+#endif
+
+CDEV void fe_mul_triple(fe& r0, const fe& f0, const fe& g0, fe& r1, const fe& f1, const fe& g1, fe& r2,
+                        const fe& f2, const fe& g2) {
+#if FE_USE_ASM2 && FE_QUAD
+  fe_mul3(r0, f0, g0, r1, f1, g1, r2, f2, g2);
+#else
+  fe o2;
+  fe_mul(o2, f2, g2);
+  fe_mul_pair(r0, f0, g0, r1, f1, g1);
+  r2 = o2;
+#endif
+}
+CDEV void fe_mul_quad(fe& r0, const fe& f0, const fe& g0, fe& r1, const fe& f1, const fe& g1, fe& r2,
+                      const fe& f2, const fe& g2, fe& r3, const fe& f3, const fe& g3) {
+#if FE_USE_ASM2 && FE_QUAD
+  fe_mul4(r0, f0, g0, r1, f1, g1, r2, f2, g2, r3, f3, g3);
+#else
+  fe o2, o3;
+  fe_mul_pair(o2, f2, g2, o3, f3, g3);
+  fe_mul_pair(r0, f0, g0, r1, f1, g1);
+  r2 = o2;
+  r3 = o3;
+#endif
+}
 struct ge_p3 {      // x = X/Z, y = Y/Z, x*y = T/Z
   fe X, Y, Z, T;
 };
@@ -69,7 +102,10 @@ CDEV void ge_to_cached(ge_cached& c, const ge_p3& p) {
   fe_mul(c.T2d, p.T, d2);
 }
 
-// r = 2p. WANT_T: compute T (needed when an addition follows).
+// r = 2p. WANT_T: compute T (needed when an addition follows). The four
+// squarings stay two pairs: as one 4-chain block they need more registers than
+// the ladder has while its table gathers are in flight (and measured no faster
+// where they fit).
 template <bool WANT_T>
 CDEV void ge_dbl(ge_p3& r, const ge_p3& p) {
   fe a, b, c, e, f, g, h, t;
@@ -81,9 +117,8 @@ CDEV void ge_dbl(ge_p3& r, const ge_p3& p) {
   fe_sub_loose(g, a, b);   // G' = A - B          (= -G), <= 3x
   fe_add(f, c, c);
   fe_add(f, f, g);         // F' = 2Z^2 + G'      (= -F), <= 5x: f-operand only
-  fe_mul_pair(r.X, f, e, r.Y, g, h);
-  if (WANT_T) fe_mul_pair(r.Z, f, g, r.T, e, h);
-  else fe_mul(r.Z, f, g);
+  if (WANT_T) fe_mul_quad(r.X, f, e, r.Y, g, h, r.Z, f, g, r.T, e, h);
+  else fe_mul_triple(r.X, f, e, r.Y, g, h, r.Z, f, g);
 }
 
 // r = p + q (q cached). WANT_T as above.
@@ -92,16 +127,14 @@ CDEV void ge_add(ge_p3& r, const ge_p3& p, const ge_cached& q) {
   fe a, b, c, d, e, f, g, h, t, u;
   fe_sub_loose(t, p.Y, p.X);  // <= 3x
   fe_add(u, p.Y, p.X);
-  fe_mul_pair(a, t, q.YmX, b, u, q.YpX);
-  fe_mul_pair(c, p.T, q.T2d, d, p.Z, q.Z);
+  fe_mul_quad(a, t, q.YmX, b, u, q.YpX, c, p.T, q.T2d, d, p.Z, q.Z);
   fe_add(d, d, d);            // 2x
   fe_sub_loose(e, b, a);      // <= 3x
   fe_sub_loose(f, d, c);      // <= 4x: f-operand only
   fe_add(g, d, c);            // <= 3x
   fe_add(h, b, a);            // 2x
-  fe_mul_pair(r.X, f, e, r.Y, g, h);
-  if (WANT_T) fe_mul_pair(r.Z, f, g, r.T, e, h);
-  else fe_mul(r.Z, f, g);
+  if (WANT_T) fe_mul_quad(r.X, f, e, r.Y, g, h, r.Z, f, g, r.T, e, h);
+  else fe_mul_triple(r.X, f, e, r.Y, g, h, r.Z, f, g);
 }
 
 // r = p + q (q affine niels: saves the Z multiplication)
@@ -110,16 +143,14 @@ CDEV void ge_madd(ge_p3& r, const ge_p3& p, const ge_niels& q) {
   fe a, b, c, d, e, f, g, h, t, u;
   fe_sub_loose(t, p.Y, p.X);
   fe_add(u, p.Y, p.X);
-  fe_mul_pair(a, t, q.ymx, b, u, q.ypx);
-  fe_mul(c, p.T, q.xy2d);
+  fe_mul_triple(a, t, q.ymx, b, u, q.ypx, c, p.T, q.xy2d);
   fe_add(d, p.Z, p.Z);
   fe_sub_loose(e, b, a);
   fe_sub_loose(f, d, c);
   fe_add(g, d, c);
   fe_add(h, b, a);
-  fe_mul_pair(r.X, f, e, r.Y, g, h);
-  if (WANT_T) fe_mul_pair(r.Z, f, g, r.T, e, h);
-  else fe_mul(r.Z, f, g);
+  if (WANT_T) fe_mul_quad(r.X, f, e, r.Y, g, h, r.Z, f, g, r.T, e, h);
+  else fe_mul_triple(r.X, f, e, r.Y, g, h, r.Z, f, g);
 }
 
 // Canonical encoding (i2p GroupElement.toByteArray / ref10 ge_tobytes):

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Generate corda_amd/csrc/fe25519_asm.hpp: GF(2^255-19) products of TWO
-independent operand pairs as one gfx950 inline-asm block each (fe_mul2,
-fe_sq2), in the radix-2^25.5 representation of fe25519.hpp.
+"""Generate corda_amd/csrc/fe25519_asm.hpp: GF(2^255-19) products of TWO,
+THREE or FOUR independent operand pairs as one gfx950 inline-asm block each
+(fe_mul2, fe_sq2, fe_mul3, fe_mul4, fe_sq4), in the radix-2^25.5
+representation of fe25519.hpp.
 
 Why asm: the column accumulation wants the incoming carry as the addend of the
 column's first v_mad_u64_u32, so carries cost no instruction. LLVM re-associates
@@ -9,9 +10,12 @@ such a chain ((carry + p0) + p1 ... -> (p0 + ... + p9) + carry) and pays one
 64-bit add per column (v_lshl_add_u64, a 4-cycle VOP3 on gfx950: 10 per
 product, ~8% of a product's issue cycles; tools/microbench/valu_rates.hip). A
 carry-chained column is a dependent chain (v_mad_u64_u32 waits ~12 cycles for
-its predecessor), so two independent products are interleaved instruction by
-instruction: with two waves per SIMD that is four chains in flight, enough to
-keep the SIMD issuing a v_mad_u64_u32 every ~4 cycles.
+its predecessor), so independent products are interleaved instruction by
+instruction. Two chains per wave at two waves per SIMD still leave the pair
+~25% above its issue cost (profiles/r02_fe_asm_check.jsonl: ~5.2 cycles per
+instruction against ~4.1); the group formulas have four independent products
+per stage (doubling: X^2, Y^2, Z^2, (X+Y)^2; additions: four, then three or
+four), so they use 3- and 4-chain blocks.
 
 The arithmetic is exactly fe25519.hpp's carry-chained fe_mul / fe_sq (same
 column terms in the same order, same masks and shifts), so the results are
@@ -28,8 +32,8 @@ MASK = {0: "0x3ffffff", 1: "0x1ffffff"}  # even limbs 26 bits, odd 25
 # the limb mask reads the pair's low register, which an operand constraint
 # cannot name (FE_ASM_ACC_CLOBBERS in the header); the compiler allocates
 # everything else around them.
-ACC = ("v[160:161]", "v[162:163]")
-ACC_LO = ("v160", "v162")
+ACC = ("v[160:161]", "v[162:163]", "v[164:165]", "v[166:167]")
+ACC_LO = ("v160", "v162", "v164", "v166")
 
 
 def bits(k):
@@ -61,13 +65,14 @@ def sq_terms(k):
     return out
 
 
-def gen(kind):
-    """One asm statement for two products; operand names carry a product suffix."""
+def gen(kind, n):
+    """One asm statement for n products; operand names carry a product suffix."""
     terms = [mul_terms(k) if kind == "mul" else sq_terms(k) for k in range(10)]
     need = sorted({x for col in terms for t in col for x in t})
     lines = []
-    # scaled operands: f2 = f << 1, f4 = f << 2, g19 / f19 = 19 x
-    for p in (0, 1):
+    P = range(n)
+    # scaled operands: f2 = 2 f, f4 = 4 f, g19 / f19 = 19 x
+    for p in P:
         for nm in need:
             base, idx = nm.split("_")
             src = ("g_%s" % idx) if base == "g19" else ("f_%s" % idx)
@@ -84,78 +89,91 @@ def gen(kind):
     for k in range(10):
         col = terms[k]
         for t, (a, b) in enumerate(col):
-            for p in (0, 1):
+            for p in P:
                 addend = ("0" if k == 0 else "%%[c%d]" % p) if t == 0 else ACC[p]
                 lines.append("v_mad_u64_u32 %s, vcc, %%[%s%d], %%[%s%d], %s" % (ACC[p], a, p, b, p, addend))
-        for p in (0, 1):
+        for p in P:
             lines.append("v_and_b32 %%[r%d_%d], %s, %s" % (p, k, MASK[k & 1], ACC_LO[p]))
             lines.append("v_lshrrev_b64 %%[c%d], %d, %s" % (p, bits(k), ACC[p]))
-    scaled = [n for n in need if n.split("_")[0] in ("f2", "f4", "g19", "f19")]
+    scaled = [nm for nm in need if nm.split("_")[0] in ("f2", "f4", "g19", "f19")]
     return lines, scaled
 
 
-def asm_block(kind):
-    lines, scaled = gen(kind)
+def asm_block(kind, n):
+    lines, scaled = gen(kind, n)
     body = "\n".join('        "%s\\n"' % l for l in lines)
     outs = []
-    for p in (0, 1):
+    for p in range(n):
         outs += ['[r%d_%d] "=&v"(o%d.v[%d])' % (p, k, p, k) for k in range(10)]
         outs += ['[c%d] "=&v"(c%d)' % (p, p)]
-        outs += ['[%s%d] "=&v"(t%d_%s)' % (n, p, p, n) for n in scaled]
+        outs += ['[%s%d] "=&v"(t%d_%s)' % (nm, p, p, nm) for nm in scaled]
     ins = []
-    for p in (0, 1):
+    for p in range(n):
         ins += ['[f_%d%d] "v"(f%d.v[%d])' % (k, p, p, k) for k in range(10)]
         if kind == "mul":
             ins += ['[g_%d%d] "v"(g%d.v[%d])' % (k, p, p, k) for k in range(10)]
-    decl = "\n".join("  uint32_t %s;" % ", ".join("t%d_%s" % (p, n) for n in scaled) for p in (0, 1))
+    decl = "\n".join("  uint32_t %s;" % ", ".join("t%d_%s" % (p, nm) for nm in scaled) for p in range(n))
     return body, ",\n        ".join(outs), ",\n        ".join(ins), decl
 
 
 HEADER = '''// GENERATED by tools/gen_fe_asm.py -- do not edit; re-run the script.
 //
-// GF(2^255-19) products of two independent operand pairs, each as ONE gfx950
-// inline-asm block: carry-chained columns (the incoming carry is the addend of
-// the column's first v_mad_u64_u32, so carries cost no add), the two products'
-// chains interleaved instruction by instruction (a dependent v_mad_u64_u32
-// waits ~12 cycles; two chains per wave and two waves per SIMD keep it issuing
-// every ~4). Bit-identical to fe25519.hpp's carry-chained fe_mul / fe_sq
+// GF(2^255-19) products of two, three or four independent operand pairs, each
+// as ONE gfx950 inline-asm block: carry-chained columns (the incoming carry is
+// the addend of the column's first v_mad_u64_u32, so carries cost no add), the
+// products' chains interleaved instruction by instruction (a dependent
+// v_mad_u64_u32 waits for its predecessor; more chains per wave hide more of
+// that latency). Bit-identical to fe25519.hpp's carry-chained fe_mul / fe_sq
 // (checked by tools/microbench/fe_asm_check.hip); same operand bounds.
 #pragma once
 #include "fe25519.hpp"
 
-// the accumulators' fixed VGPRs (v160..v163): see tools/gen_fe_asm.py
+// the accumulators' fixed VGPRs (v160..v167): see tools/gen_fe_asm.py
 #define FE_ASM_ACC_CLOBBERS "v160", "v161", "v162", "v163"
+#define FE_ASM_ACC_CLOBBERS3 FE_ASM_ACC_CLOBBERS, "v164", "v165"
+#define FE_ASM_ACC_CLOBBERS4 FE_ASM_ACC_CLOBBERS3, "v166", "v167"
 
 namespace cordahip {
 '''
 
+CLOBBERS = {2: "FE_ASM_ACC_CLOBBERS", 3: "FE_ASM_ACC_CLOBBERS3", 4: "FE_ASM_ACC_CLOBBERS4"}
 
-def main():
+
+def signature(kind, n):
+    if kind == "mul":
+        args = ", ".join("fe& r%d, const fe& f%d, const fe& g%d" % (p, p, p) for p in range(n))
+    else:
+        args = ", ".join("fe& r%d, const fe& f%d" % (p, p) for p in range(n))
+    return "CDEV void fe_%s%d(%s)" % (kind, n, args)
+
+
+def render():
     parts = [HEADER]
-    for kind in ("mul", "sq"):
-        body, outs, ins, decl = asm_block(kind)
-        if kind == "mul":
-            sig = "CDEV void fe_mul2(fe& r0, const fe& f0, const fe& g0, fe& r1, const fe& f1, const fe& g1)"
-        else:
-            sig = "CDEV void fe_sq2(fe& r0, const fe& f0, fe& r1, const fe& f1)"
+    for kind, n in (("mul", 2), ("sq", 2), ("mul", 3), ("mul", 4), ("sq", 4)):
+        body, outs, ins, decl = asm_block(kind, n)
         parts.append('''%s {
-  fe o0, o1;
-  uint64_t c0, c1;
+  fe %s;
+  uint64_t %s;
 %s
   asm(
 %s
       : %s
       : %s
-      : "vcc", FE_ASM_ACC_CLOBBERS);
-  fe_fold_top(o0, c0);
-  fe_fold_top(o1, c1);
-  r0 = o0;
-  r1 = o1;
+      : "vcc", %s);
+%s
+%s
 }
-''' % (sig, decl, body, outs, ins))
+''' % (signature(kind, n), ", ".join("o%d" % p for p in range(n)), ", ".join("c%d" % p for p in range(n)),
+       decl, body, outs, ins, CLOBBERS[n],
+       "\n".join("  fe_fold_top(o%d, c%d);" % (p, p) for p in range(n)),
+       "\n".join("  r%d = o%d;" % (p, p) for p in range(n))))
     parts.append("}  // namespace cordahip\n")
+    return "\n".join(parts)
+
+
+def main():
     with open(OUT, "w") as f:
-        f.write("\n".join(parts))
+        f.write(render())
     print("wrote", OUT)
 
 

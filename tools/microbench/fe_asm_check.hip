@@ -1,7 +1,7 @@
-// GPU check + timing of the generated two-product field multiplies
-// (corda_amd/csrc/fe25519_asm.hpp) against fe25519.hpp's carry-chained C
-// versions: identical limbs for random loose operands (limbs < 2^27, the
-// group formulas' bound), then the issue cost of a long chain of each form.
+// GPU check + timing of the generated multi-product field multiplies
+// (corda_amd/csrc/fe25519_asm.hpp: fe_mul2/3/4, fe_sq2/4) against fe25519.hpp's
+// carry-chained C versions: identical limbs for random loose operands (limbs
+// < 2^27, the group formulas' bound), then the issue cost of long chains.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -23,7 +23,7 @@ __device__ void rnd(fe& a, uint32_t& s, int lbits) {
   for (int i = 0; i < 10; i++) a.v[i] = xs(s) & ((1u << lbits) - 1);
 }
 
-__global__ void check(uint32_t* bad, uint32_t seed) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) check(uint32_t* bad, uint32_t seed) {
   uint32_t s = seed ^ (blockIdx.x * 256 + threadIdx.x) * 2654435761u;
   for (int it = 0; it < 64; it++) {
     fe f0, g0, f1, g1, a0, a1, b0, b1;
@@ -39,23 +39,40 @@ __global__ void check(uint32_t* bad, uint32_t seed) {
     fe_sq(a1, f1);
     fe_sq2(b0, f0, b1, f1);
     for (int i = 0; i < 10; i++) d |= ((a0.v[i] ^ b0.v[i]) | (a1.v[i] ^ b1.v[i])) << 1;
+    // 3- and 4-chain blocks
+    fe f2, g2, f3, g3, a2, a3, b2, b3;
+    rnd(f0, s, lb); rnd(g0, s, 26); rnd(f1, s, 26); rnd(g1, s, 27);
+    rnd(f2, s, 27); rnd(g2, s, 25); rnd(f3, s, 26); rnd(g3, s, 26);
+    fe_mul(a0, f0, g0); fe_mul(a1, f1, g1); fe_mul(a2, f2, g2); fe_mul(a3, f3, g3);
+    fe_mul4(b0, f0, g0, b1, f1, g1, b2, f2, g2, b3, f3, g3);
+    for (int i = 0; i < 10; i++)
+      d |= ((a0.v[i] ^ b0.v[i]) | (a1.v[i] ^ b1.v[i]) | (a2.v[i] ^ b2.v[i]) | (a3.v[i] ^ b3.v[i])) ? 4u : 0u;
+    fe_mul3(b0, f0, g0, b1, f1, g1, b2, f2, g2);
+    for (int i = 0; i < 10; i++) d |= ((a0.v[i] ^ b0.v[i]) | (a1.v[i] ^ b1.v[i]) | (a2.v[i] ^ b2.v[i])) ? 8u : 0u;
+    fe_sq(a0, f0); fe_sq(a1, f1); fe_sq(a2, f2); fe_sq(a3, f3);
+    fe_sq4(b0, f0, b1, f1, b2, f2, b3, f3);
+    for (int i = 0; i < 10; i++)
+      d |= ((a0.v[i] ^ b0.v[i]) | (a1.v[i] ^ b1.v[i]) | (a2.v[i] ^ b2.v[i]) | (a3.v[i] ^ b3.v[i])) ? 16u : 0u;
     if (d) atomicOr(bad, d);
   }
 }
 
-template <int MODE>  // 0: fe_mul x2 (C), 1: fe_mul2 (asm), 2: fe_sq x2, 3: fe_sq2
-__global__ void __launch_bounds__(256) chain(uint32_t* out, uint32_t seed, int iters) {
+// 0: fe_mul x4 (C), 1: 2 x fe_mul2, 2: fe_mul4, 3: 2 x fe_sq2, 4: fe_sq4 (four products per iteration)
+template <int MODE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) chain(uint32_t* out, uint32_t seed,
+                                                                                   int iters) {
   uint32_t s = seed ^ (blockIdx.x * 256 + threadIdx.x);
-  fe x, y, z, w;
-  rnd(x, s, 26); rnd(y, s, 26); rnd(z, s, 26); rnd(w, s, 26);
+  fe x, y, z, w, u, v;
+  rnd(x, s, 26); rnd(y, s, 26); rnd(z, s, 26); rnd(w, s, 26); rnd(u, s, 26); rnd(v, s, 26);
   for (int it = 0; it < iters; it++) {
-    if (MODE == 0) { fe_mul(x, x, y); fe_mul(z, z, w); }
-    if (MODE == 1) fe_mul2(x, x, y, z, z, w);
-    if (MODE == 2) { fe_sq(x, x); fe_sq(z, z); }
-    if (MODE == 3) fe_sq2(x, x, z, z);
+    if (MODE == 0) { fe_mul(x, x, y); fe_mul(z, z, w); fe_mul(u, u, y); fe_mul(v, v, w); }
+    if (MODE == 1) { fe_mul2(x, x, y, z, z, w); fe_mul2(u, u, y, v, v, w); }
+    if (MODE == 2) fe_mul4(x, x, y, z, z, w, u, u, y, v, v, w);
+    if (MODE == 3) { fe_sq2(x, x, z, z); fe_sq2(u, u, v, v); }
+    if (MODE == 4) fe_sq4(x, x, z, z, u, u, v, v);
   }
   uint32_t a = 0;
-  for (int i = 0; i < 10; i++) a ^= x.v[i] ^ z.v[i];
+  for (int i = 0; i < 10; i++) a ^= x.v[i] ^ z.v[i] ^ u.v[i] ^ v.v[i];
   out[blockIdx.x * 256 + threadIdx.x] = a;
 }
 
@@ -74,8 +91,8 @@ static int time_chain(const char* name, uint32_t* dout, int ncu, int per_simd_wa
   CHECK(hipEventSynchronize(b));
   float ms;
   CHECK(hipEventElapsedTime(&ms, a, b));
-  // per SIMD: per_simd_waves waves x iters x 2 products
-  const double ns_per_product = ms * 1e6 / ((double)per_simd_waves * iters * 2);
+  // per SIMD: per_simd_waves waves x iters x 4 products
+  const double ns_per_product = ms * 1e6 / ((double)per_simd_waves * iters * 4);
   printf("{\"form\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"ns_per_product_per_simd\": %.2f}\n", name,
          per_simd_waves, ms, ns_per_product);
   return 0;
@@ -91,13 +108,15 @@ int main() {
   hipLaunchKernelGGL(check, dim3(4096), dim3(256), 0, 0, dbad, 12345u);
   uint32_t bad = 0;
   CHECK(hipMemcpy(&bad, dbad, 4, hipMemcpyDeviceToHost));
-  printf("{\"check\": \"fe_mul2/fe_sq2 vs fe_mul/fe_sq\", \"lanes\": %d, \"mul_mismatch\": %d, \"sq_mismatch\": %d}\n",
-         4096 * 256 * 64, bad & 1, (bad >> 1) & 1);
+  printf("{\"check\": \"fe_mul2/3/4, fe_sq2/4 vs fe_mul/fe_sq\", \"lanes\": %d, \"mul2_mismatch\": %d, "
+         "\"sq2_mismatch\": %d, \"mul4_mismatch\": %d, \"mul3_mismatch\": %d, \"sq4_mismatch\": %d}\n",
+         4096 * 256 * 64, bad & 1, (bad >> 1) & 1, (bad >> 2) & 1, (bad >> 3) & 1, (bad >> 4) & 1);
   for (int w : {2, 4}) {
-    if (time_chain<0>("fe_mul x2 (C)", dout, p.multiProcessorCount, w)) return 1;
-    if (time_chain<1>("fe_mul2 (asm)", dout, p.multiProcessorCount, w)) return 1;
-    if (time_chain<2>("fe_sq x2 (C)", dout, p.multiProcessorCount, w)) return 1;
-    if (time_chain<3>("fe_sq2 (asm)", dout, p.multiProcessorCount, w)) return 1;
+    if (time_chain<0>("fe_mul x4 (C)", dout, p.multiProcessorCount, w)) return 1;
+    if (time_chain<1>("2 x fe_mul2 (asm)", dout, p.multiProcessorCount, w)) return 1;
+    if (time_chain<2>("fe_mul4 (asm)", dout, p.multiProcessorCount, w)) return 1;
+    if (time_chain<3>("2 x fe_sq2 (asm)", dout, p.multiProcessorCount, w)) return 1;
+    if (time_chain<4>("fe_sq4 (asm)", dout, p.multiProcessorCount, w)) return 1;
   }
   return bad ? 2 : 0;
 }
