@@ -255,6 +255,32 @@ CDEV void euclid_divstep(uint32_t rp[8], const uint32_t rc[8], uint32_t tp[8], c
   }
 }
 
+// floor(a / 2^s) as a double, exact for a < 2^(s+53)
+CDEV double mp8_top(const uint32_t a[8], int s) {
+  const int w = s >> 5, b = s & 31;
+  const uint64_t lo = ((uint64_t)word_sel(a, w + 1) << 32) | word_sel(a, w);
+  const uint64_t hi = word_sel(a, w + 2);
+  return (double)((lo >> b) | (b ? hi << (64 - b) : 0ull));
+}
+// o = a*x + b*y (mod 2^256) for |a|, |b| < 2^31 of opposite signs (or one of
+// them zero), as |a|x - |b|y, negated when the positive factor is b
+CDEV void mp8_lincomb(uint32_t o[8], const uint32_t x[8], int a, const uint32_t y[8], int b) {
+  const uint32_t ua = (uint32_t)(a < 0 ? -a : a), ub = (uint32_t)(b < 0 ? -b : b);
+  uint64_t pc = 0, qc = 0;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t p = (uint64_t)ua * x[i] + pc;
+    pc = p >> 32;
+    const uint64_t q = (uint64_t)ub * y[i] + qc;
+    qc = q >> 32;
+    const uint64_t d = (uint64_t)(uint32_t)p - (uint32_t)q - br;
+    o[i] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  if (b > 0 || (b == 0 && a < 0)) mp8_neg(o);
+}
+
 // (c0, c1): c0 == c1*h (mod 8L), c1 odd and positive; returns |c0| and its sign
 CDEV void half_scalars(uint32_t c0abs[8], bool& c0neg, uint32_t c1[8], const uint32_t h[8]) {
   const uint32_t kM[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0u, 0u, 0u, 0x80000000u};  // 8L
@@ -267,23 +293,66 @@ CDEV void half_scalars(uint32_t c0abs[8], bool& c0neg, uint32_t c1[8], const uin
     tp[i] = 0;
     tc[i] = i == 0;
   }
-  // Euclid, unrolled by two so the remainders never move between registers:
-  // stop at the first remainder below sqrt(8L); (rc, tc) <- that remainder's
-  // vector, (rp, tp) <- the previous one.
+  // Euclid on (8L, h) until the first remainder below sqrt(8L), run as Lehmer
+  // rounds (Knuth TAOCP 4.5.2, Algorithm L): Euclid on the 52-bit leading
+  // parts of rp, rc (exact in doubles) while both bracketing quotients agree,
+  // so every quotient is Euclid's own, then the round's 2x2 cofactor matrix
+  // is applied to the 256-bit remainders and cofactors once. A step is taken
+  // only while the remainder it produces provably stays >= sqrt(8L) (its
+  // true value is within max(|C|,|D|) units of the leading part), so one
+  // exact step below finishes. ~6 rounds of ~12 double-precision steps replace
+  // ~73 multiprecision steps; the state handed over is Euclid's exactly
+  // (tools/proto/lehmer.py checks that on 5e4 random h).
+  for (;;) {
+    const int s = max(mp8_bitlen(rp) - 52, 0);
+    double uh = mp8_top(rp, s), vh = mp8_top(rc, s);
+    const double th = mp8_top(kS, s) + 1.0;
+    double A = 1.0, B = 0.0, C = 0.0, D = 1.0;
+    int n = 0;
+    for (;;) {
+      const double d1 = vh + C, d2 = vh + D;
+      if (!(d1 > 0.0 && d2 > 0.0)) break;
+      const double n1 = uh + A;
+      double q = floor(n1 / d1);
+      const double r1 = fma(-q, d1, n1);  // exact: |r1| < 2^53
+      q = r1 < 0.0 ? q - 1.0 : (r1 >= d1 ? q + 1.0 : q);
+      const double r2 = fma(-q, d2, uh + B);
+      if (!(r2 >= 0.0 && r2 < d2)) break;  // the other bracket's quotient differs
+      const double nC = fma(-q, C, A), nD = fma(-q, D, B), nv = fma(-q, vh, uh);
+      const double mc = fmax(fabs(nC), fabs(nD));
+      if (nv - mc < th || mc >= 0x1p30) break;
+      A = C;
+      B = D;
+      C = nC;
+      D = nD;
+      uh = vh;
+      vh = nv;
+      n++;
+    }
+    if (n == 0) break;
+    const int a = (int)A, b = (int)B, c = (int)C, d = (int)D;
+    uint32_t x[8], y[8];
+    mp8_lincomb(x, rp, a, rc, b);
+    mp8_lincomb(y, rp, c, rc, d);
+    mp8_copy(rp, x);
+    mp8_copy(rc, y);
+    mp8_lincomb(x, tp, a, tc, b);
+    mp8_lincomb(y, tp, c, tc, d);
+    mp8_copy(tp, x);
+    mp8_copy(tc, y);
+  }
+  // the remaining exact step(s): (rc, tc) <- the first remainder below
+  // sqrt(8L) and its cofactor, (rp, tp) <- the previous one
   while (mp8_ge(rc, kS)) {
     euclid_divstep(rp, rc, tp, tc);  // rp <- rp mod rc
-    if (!mp8_ge(rp, kS)) {
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const uint32_t a = rp[i], b = tp[i];
-        rp[i] = rc[i];
-        rc[i] = a;
-        tp[i] = tc[i];
-        tc[i] = b;
-      }
-      break;
+    for (int i = 0; i < 8; i++) {
+      const uint32_t a = rp[i], b = tp[i];
+      rp[i] = rc[i];
+      rc[i] = a;
+      tp[i] = tc[i];
+      tc[i] = b;
     }
-    euclid_divstep(rc, rp, tc, tp);  // rc <- rc mod rp
   }
   uint32_t a0[8], a1[8];  // chosen (c0, c1), two's complement
   mp8_copy(a0, rc);
