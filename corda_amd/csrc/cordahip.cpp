@@ -165,9 +165,9 @@ thread_local std::unordered_map<uint64_t, int> tl_last_call;
 // Launch-pair sizes of the split kernels = the largest workspace per device.
 // Bigger launches pay fewer end-of-grid tails (C2, measured: 2^18 91.5, 2^20
 // 93.2, 2^22 96.4, 2^24 97.2 M verifs/s): a 2^24-lane batch runs as ONE
-// prep/ladder pair over 50 GB of HBM (17% of the MI355X's 288 GB). Smaller
+// prep/ladder pair over 54 GB of HBM (19% of the MI355X's 288 GB). Smaller
 // batches allocate only what they use (grow-only, from 2^18 lanes up).
-constexpr uint64_t kEdWsLanes = 1ull << 24;  // x 2,992 B = 50 GB of Ed25519 workspace at most
+constexpr uint64_t kEdWsLanes = 1ull << 24;  // x 3,200 B = 54 GB of Ed25519 workspace at most
 constexpr uint64_t kEcWsSlots = 1ull << 24;  // x 1,120 B = 18.8 GB of ECDSA workspace at most
 constexpr uint64_t kWsMinLanes = 1ull << 18;
 

@@ -445,24 +445,20 @@ CDEV void load_point(ge_p3& p, const uint32_t* __restrict__ o) {
   fe_set(p.Z, 1);
 }
 
-CDEV void store_table9(uint32_t* __restrict__ rec, const ge_p3& base) {
-  ge_cached c;
-  fe_set(c.YpX, 1);
-  fe_set(c.YmX, 1);
-  fe_set(c.Z, 1);
-  fe_set(c.T2d, 0);
-  store_cached(rec, c);
-  ge_cached c1;
+// entries [1..8]base of a per-lane table (entry 0, the identity, is shared:
+// table_entry in ed25519_ws.hpp)
+CDEV void store_table8(uint32_t* __restrict__ rec, const ge_p3& base) {
+  ge_cached c, c1;
   ge_to_cached(c1, base);
-  store_cached(rec + 40, c1);
+  store_cached(rec, c1);
   ge_p3 Q;
   ge_dbl<true>(Q, base);
   ge_to_cached(c, Q);
-  store_cached(rec + 80, c);
+  store_cached(rec + kWhEntryWords, c);
   for (int k = 3; k <= 8; k++) {
     ge_add<true>(Q, Q, c1);
     ge_to_cached(c, Q);
-    store_cached(rec + 40 * k, c);
+    store_cached(rec + kWhEntryWords * (k - 1), c);
   }
 }
 
@@ -506,14 +502,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
       ge_identity(A);
       ge_identity(R);
     }
-    // -A, -R parked in the last slot of their table (Z = 1: X, Y, T), so the
+    // -A, -R parked in the last entry of their table (Z = 1: X, Y, T), so the
     // table loop below holds one point at a time
     fe_neg(A.X, A.X);
     fe_neg(A.T, A.T);
     fe_neg(R.X, R.X);
     fe_neg(R.T, R.T);
-    store_point(rec + kWhTabA + 40 * 8, A);
-    store_point(rec + kWhTabR + 40 * 8, R);
+    store_point(rec + kWhTabA + kWhEntryWords * 7, A);
+    store_point(rec + kWhTabR + kWhEntryWords * 7, R);
   }
   PHASE_BARRIER();
   // tables [k](-A), [k](-R): one loop body keeps a single copy of the table
@@ -522,8 +518,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) e
   for (int pass = 0; pass < 2; pass++) {
     uint32_t* tab = rec + (pass ? kWhTabR : kWhTabA);
     ge_p3 P;
-    load_point(P, tab + 40 * 8);  // read before store_table9 overwrites slot 8
-    store_table9(tab, P);
+    load_point(P, tab + kWhEntryWords * 7);  // read before store_table8 overwrites slot 8
+    store_table8(tab, P);
     PHASE_BARRIER();
   }
   uint32_t ka[8], kr[8], e[8];

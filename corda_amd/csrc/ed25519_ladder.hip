@@ -23,6 +23,11 @@
 
 namespace cordahip {
 
+__device__ __attribute__((aligned(64))) const uint32_t kIdentityCached[kWhEntryWords] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0,   // Y + X
+                                                            1, 0, 0, 0, 0, 0, 0, 0, 0, 0,   // Y - X
+                                                            1, 0, 0, 0, 0, 0, 0, 0, 0, 0,   // Z
+                                                            0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // 2dT
+
 // booth_digit (sc25519.hpp) over a scalar stored word-major in LDS: word w of
 // this thread's scalar at col[w * 256]
 template <int W>
@@ -82,8 +87,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_LAD
   for (int j = W - 1; j >= 0; j--) {
     const int da = booth_digit_col<4>(ska, j), dr = booth_digit_col<4>(skr, j);
     ge_cached ca, cr;  // issued before the doublings, consumed after them
-    load_cached(ca, rec + kWhTabA + 40 * (da < 0 ? -da : da));
-    load_cached(cr, rec + kWhTabR + 40 * (dr < 0 ? -dr : dr));
+    load_cached(ca, table_entry(rec + kWhTabA, da < 0 ? -da : da));
+    load_cached(cr, table_entry(rec + kWhTabR, dr < 0 ? -dr : dr));
     if (j != W - 1) {
       ge_dbl<false>(P, P);
       ge_dbl<false>(P, P);

@@ -30,14 +30,30 @@ static constexpr int kBTableEntries = (1 << (kBBits - 1)) + 1;
 static constexpr int kBEntryWords = 32;
 static constexpr uint8_t kStatusPending = 0xff;
 
-// Per-lane workspace record (2,992 B, 16-B aligned fields):
-static constexpr int kWhTabA = 0;                // [0..8](-A), cached form, 40 words each
-static constexpr int kWhTabR = 9 * 40;           // [0..8](-R)
-static constexpr int kWhKa = 18 * 40;            // |c0|, c1, e (8 words each)
+// Per-lane workspace record (3,200 B = 50 x 64 B, so every record and every
+// entry starts on a 64-B sector): entries [1..8](-A), [1..8](-R) in cached form
+// (40 words) padded to 48 words, so a gather of one entry reads exactly three
+// 64-B sectors (at 40-word stride an entry straddled 3-4 sectors and 2-3
+// 128-B lines). Digit 0 gathers the shared identity entry kIdentityCached
+// (L2-resident) instead of a per-lane copy.
+static constexpr int kWhEntryWords = 48;
+static constexpr int kWhTabA = 0;                       // [k](-A) at (k - 1) * kWhEntryWords, k = 1..8
+static constexpr int kWhTabR = 8 * kWhEntryWords;       // [k](-R)
+static constexpr int kWhKa = 16 * kWhEntryWords;        // |c0|, c1, e (8 words each)
 static constexpr int kWhKr = kWhKa + 8;
 static constexpr int kWhE = kWhKa + 16;
-static constexpr int kWhFlags = kWhKa + 24;      // bit 0: c0 < 0
-static constexpr int kWhLaneWords = kWhKa + 28;  // 748 words
+static constexpr int kWhFlags = kWhKa + 24;             // bit 0: c0 < 0
+static constexpr int kWhLaneWords = kWhKa + 32;         // 800 words
+static_assert(kWhLaneWords % 16 == 0, "records must start on 64-B sectors");
+
+// the identity in cached form (Y+X, Y-X, Z, 2dT) = (1, 1, 1, 0), entry 0 of
+// every per-lane table (defined in ed25519_ladder.hip)
+extern __device__ const uint32_t kIdentityCached[kWhEntryWords];
+
+// entry |d| of a per-lane table (tab = rec + kWhTabA or kWhTabR)
+CDEV const uint32_t* table_entry(const uint32_t* tab, int absd) {
+  return absd == 0 ? kIdentityCached : tab + (absd - 1) * kWhEntryWords;
+}
 
 CDEV void load_niels(ge_niels& n, const uint32_t* __restrict__ tab, int idx) {
   const uint4* e = reinterpret_cast<const uint4*>(tab + idx * kBEntryWords);
@@ -94,6 +110,8 @@ CDEV void store_cached(uint32_t* __restrict__ o, const ge_cached& c) {
   }
 #pragma unroll
   for (int q = 0; q < 10; q++) o4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  // the pad too: whole 64-B sectors, no partial-sector writes
+  o4[10] = o4[11] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 CDEV void load_cached(ge_cached& c, const uint32_t* __restrict__ p) {

@@ -76,6 +76,22 @@ CDEV void fe_mul_quad(fe& r0, const fe& f0, const fe& g0, fe& r1, const fe& f1, 
   r3 = o3;
 #endif
 }
+// The formulas' output stage X = F E, Y = H G, Z = F G (, T = H E): F and H
+// as f-operands, E and G as g-operands (F' may reach 5x, so it is never
+// 19-scaled), as ONE outer-product block whose scaled operand copies are
+// shared (fe25519_asm.hpp fe_mul3x / fe_mul4x; Y = H G and T = H E are
+// bit-identical to G H and E H).
+template <bool WANT_T, class P>
+CDEV void ge_out_stage(P& r, const fe& f, const fe& e, const fe& g, const fe& h) {
+#if FE_USE_ASM2 && FE_QUAD
+  if (WANT_T) fe_mul4x(r.X, r.Y, r.Z, r.T, f, h, e, g);
+  else fe_mul3x(r.X, r.Y, r.Z, f, h, e, g);
+#else
+  if (WANT_T) fe_mul_quad(r.X, f, e, r.Y, g, h, r.Z, f, g, r.T, e, h);
+  else fe_mul_triple(r.X, f, e, r.Y, g, h, r.Z, f, g);
+#endif
+}
+
 struct ge_p3 {      // x = X/Z, y = Y/Z, x*y = T/Z
   fe X, Y, Z, T;
 };
@@ -117,8 +133,7 @@ CDEV void ge_dbl(ge_p3& r, const ge_p3& p) {
   fe_sub_loose(g, a, b);   // G' = A - B          (= -G), <= 3x
   fe_add(f, c, c);
   fe_add(f, f, g);         // F' = 2Z^2 + G'      (= -F), <= 5x: f-operand only
-  if (WANT_T) fe_mul_quad(r.X, f, e, r.Y, g, h, r.Z, f, g, r.T, e, h);
-  else fe_mul_triple(r.X, f, e, r.Y, g, h, r.Z, f, g);
+  ge_out_stage<WANT_T>(r, f, e, g, h);
 }
 
 // r = p + q (q cached). WANT_T as above.
@@ -133,8 +148,7 @@ CDEV void ge_add(ge_p3& r, const ge_p3& p, const ge_cached& q) {
   fe_sub_loose(f, d, c);      // <= 4x: f-operand only
   fe_add(g, d, c);            // <= 3x
   fe_add(h, b, a);            // 2x
-  if (WANT_T) fe_mul_quad(r.X, f, e, r.Y, g, h, r.Z, f, g, r.T, e, h);
-  else fe_mul_triple(r.X, f, e, r.Y, g, h, r.Z, f, g);
+  ge_out_stage<WANT_T>(r, f, e, g, h);
 }
 
 // r = p + q (q affine niels: saves the Z multiplication)
@@ -149,8 +163,7 @@ CDEV void ge_madd(ge_p3& r, const ge_p3& p, const ge_niels& q) {
   fe_sub_loose(f, d, c);
   fe_add(g, d, c);
   fe_add(h, b, a);
-  if (WANT_T) fe_mul_quad(r.X, f, e, r.Y, g, h, r.Z, f, g, r.T, e, h);
-  else fe_mul_triple(r.X, f, e, r.Y, g, h, r.Z, f, g);
+  ge_out_stage<WANT_T>(r, f, e, g, h);
 }
 
 // Canonical encoding (i2p GroupElement.toByteArray / ref10 ge_tobytes):

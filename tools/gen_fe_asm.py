@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Generate corda_amd/csrc/fe25519_asm.hpp: GF(2^255-19) products of TWO,
 THREE or FOUR independent operand pairs as one gfx950 inline-asm block each
-(fe_mul2, fe_sq2, fe_mul3, fe_mul4, fe_sq4), in the radix-2^25.5
+(fe_mul2, fe_sq2, fe_mul3, fe_mul4, fe_sq4), plus the outer-product blocks
+fe_mul3x / fe_mul4x of the formulas' output stage, in the radix-2^25.5
 representation of fe25519.hpp.
 
 Why asm: the column accumulation wants the incoming carry as the addend of the
@@ -116,6 +117,80 @@ def asm_block(kind, n):
     return body, ",\n        ".join(outs), ",\n        ".join(ins), decl
 
 
+# Outer-product blocks: the formulas' output stage X = F E, Y = H G, Z = F G,
+# T = H E is {F, H} x {E, G}, so each operand's scaled copies (2x odd limbs of
+# an f-operand, 19x of a g-operand) are made once and shared by the two products
+# that read it: 18 v_mul_lo_u32 + 10 v_add_u32 per block instead of 36 + 20 (4
+# products) or 27 + 15 (3). Product p is F[fi] * G[gi] over column terms
+# mul_terms(k), the same multiset of integer terms as the f/g-swapped product,
+# so every column value and hence the carry-chained result is bit-identical.
+OUTER = ((0, 0), (1, 1), (0, 1), (1, 0))  # (fi, gi): F0 G0, F1 G1, F0 G1, F1 G0
+FSET, GSET = "ab", "cd"
+
+
+def gen_outer(n):
+    terms = [mul_terms(k) for k in range(10)]
+    need = sorted({x for col in terms for t in col for x in t})
+    lines = []
+    scaled = []
+    for nm in need:
+        base, idx = nm.split("_")
+        if base == "f2":
+            for fs in FSET:
+                lines.append("v_add_u32 %%[f2_%s%s], %%[f_%s%s], %%[f_%s%s]" % (idx, fs, idx, fs, idx, fs))
+                scaled.append("f2_%s%s" % (idx, fs))
+        elif base == "g19":
+            for gs in GSET:
+                lines.append("v_mul_lo_u32 %%[g19_%s%s], %%[g_%s%s], 19" % (idx, gs, idx, gs))
+                scaled.append("g19_%s%s" % (idx, gs))
+    P = range(n)
+    for k in range(10):
+        for t, (a, b) in enumerate(terms[k]):
+            for p in P:
+                fi, gi = OUTER[p]
+                addend = ("0" if k == 0 else "%%[c%d]" % p) if t == 0 else ACC[p]
+                lines.append("v_mad_u64_u32 %s, vcc, %%[%s%s], %%[%s%s], %s" % (ACC[p], a, FSET[fi], b, GSET[gi], addend))
+        for p in P:
+            lines.append("v_and_b32 %%[r%d_%d], %s, %s" % (p, k, MASK[k & 1], ACC_LO[p]))
+            lines.append("v_lshrrev_b64 %%[c%d], %d, %s" % (p, bits(k), ACC[p]))
+    return lines, scaled
+
+
+def outer_block(n):
+    lines, scaled = gen_outer(n)
+    body = "\n".join('        "%s\\n"' % l for l in lines)
+    outs = []
+    for p in range(n):
+        outs += ['[r%d_%d] "=&v"(o%d.v[%d])' % (p, k, p, k) for k in range(10)]
+        outs += ['[c%d] "=&v"(c%d)' % (p, p)]
+    outs += ['[%s] "=&v"(t_%s)' % (nm, nm) for nm in scaled]
+    ins = []
+    for j, fs in enumerate(FSET):
+        ins += ['[f_%d%s] "v"(f%d.v[%d])' % (k, fs, j, k) for k in range(10)]
+    for j, gs in enumerate(GSET):
+        ins += ['[g_%d%s] "v"(g%d.v[%d])' % (k, gs, j, k) for k in range(10)]
+    decl = "  uint32_t %s;" % ", ".join("t_%s" % nm for nm in scaled)
+    sig = "CDEV void fe_mul%dx(%s, const fe& f0, const fe& f1, const fe& g0, const fe& g1)" % (
+        n, ", ".join("fe& r%d" % p for p in range(n)))
+    return '''// r0 = f0 g0, r1 = f1 g1, r2 = f0 g1%s (shared scaled operands)
+%s {
+  fe %s;
+  uint64_t %s;
+%s
+  asm(
+%s
+      : %s
+      : %s
+      : "vcc", %s);
+%s
+%s
+}
+''' % (", r3 = f1 g0" if n == 4 else "", sig, ", ".join("o%d" % p for p in range(n)),
+       ", ".join("c%d" % p for p in range(n)), decl, body, ",\n        ".join(outs), ",\n        ".join(ins),
+       CLOBBERS[n], "\n".join("  fe_fold_top(o%d, c%d);" % (p, p) for p in range(n)),
+       "\n".join("  r%d = o%d;" % (p, p) for p in range(n)))
+
+
 HEADER = '''// GENERATED by tools/gen_fe_asm.py -- do not edit; re-run the script.
 //
 // GF(2^255-19) products of two, three or four independent operand pairs, each
@@ -167,6 +242,8 @@ def render():
        decl, body, outs, ins, CLOBBERS[n],
        "\n".join("  fe_fold_top(o%d, c%d);" % (p, p) for p in range(n)),
        "\n".join("  r%d = o%d;" % (p, p) for p in range(n))))
+    for n in (3, 4):
+        parts.append(outer_block(n))
     parts.append("}  // namespace cordahip\n")
     return "\n".join(parts)
 

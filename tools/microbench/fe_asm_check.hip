@@ -1,5 +1,5 @@
 // GPU check + timing of the generated multi-product field multiplies
-// (corda_amd/csrc/fe25519_asm.hpp: fe_mul2/3/4, fe_sq2/4) against fe25519.hpp's
+// (corda_amd/csrc/fe25519_asm.hpp: fe_mul2/3/4, fe_sq2/4, fe_mul3x/4x) against fe25519.hpp's
 // carry-chained C versions: identical limbs for random loose operands (limbs
 // < 2^27, the group formulas' bound), then the issue cost of long chains.
 #include <hip/hip_runtime.h>
@@ -53,6 +53,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) c
     fe_sq4(b0, f0, b1, f1, b2, f2, b3, f3);
     for (int i = 0; i < 10; i++)
       d |= ((a0.v[i] ^ b0.v[i]) | (a1.v[i] ^ b1.v[i]) | (a2.v[i] ^ b2.v[i]) | (a3.v[i] ^ b3.v[i])) ? 16u : 0u;
+    // outer-product blocks (the output stage: F, H up to 5x / 2x; E tight, G <= 3x)
+    rnd(f0, s, 28); rnd(f1, s, 27); rnd(g0, s, 26); rnd(g1, s, 27);
+    fe_mul(a0, f0, g0); fe_mul(a1, f1, g1); fe_mul(a2, f0, g1); fe_mul(a3, f1, g0);
+    fe_mul4x(b0, b1, b2, b3, f0, f1, g0, g1);
+    for (int i = 0; i < 10; i++)
+      d |= ((a0.v[i] ^ b0.v[i]) | (a1.v[i] ^ b1.v[i]) | (a2.v[i] ^ b2.v[i]) | (a3.v[i] ^ b3.v[i])) ? 32u : 0u;
+    fe_mul3x(b0, b1, b2, f0, f1, g0, g1);
+    for (int i = 0; i < 10; i++) d |= ((a0.v[i] ^ b0.v[i]) | (a1.v[i] ^ b1.v[i]) | (a2.v[i] ^ b2.v[i])) ? 64u : 0u;
+    // the swapped operand order of Y = H G, T = H E against fe_mul(G, H), fe_mul(E, H)
+    fe_mul(a1, g1, f1); fe_mul(a3, g0, f1);
+    fe_mul4x(b0, b1, b2, b3, f0, f1, g0, g1);
+    for (int i = 0; i < 10; i++) d |= ((a1.v[i] ^ b1.v[i]) | (a3.v[i] ^ b3.v[i])) ? 128u : 0u;
     if (d) atomicOr(bad, d);
   }
 }
@@ -108,9 +120,11 @@ int main() {
   hipLaunchKernelGGL(check, dim3(4096), dim3(256), 0, 0, dbad, 12345u);
   uint32_t bad = 0;
   CHECK(hipMemcpy(&bad, dbad, 4, hipMemcpyDeviceToHost));
-  printf("{\"check\": \"fe_mul2/3/4, fe_sq2/4 vs fe_mul/fe_sq\", \"lanes\": %d, \"mul2_mismatch\": %d, "
-         "\"sq2_mismatch\": %d, \"mul4_mismatch\": %d, \"mul3_mismatch\": %d, \"sq4_mismatch\": %d}\n",
-         4096 * 256 * 64, bad & 1, (bad >> 1) & 1, (bad >> 2) & 1, (bad >> 3) & 1, (bad >> 4) & 1);
+  printf("{\"check\": \"fe_mul2/3/4, fe_sq2/4, fe_mul3x/4x vs fe_mul/fe_sq\", \"lanes\": %d, \"mul2_mismatch\": %d, "
+         "\"sq2_mismatch\": %d, \"mul4_mismatch\": %d, \"mul3_mismatch\": %d, \"sq4_mismatch\": %d, "
+         "\"mul4x_mismatch\": %d, \"mul3x_mismatch\": %d, \"mul4x_swapped_mismatch\": %d}\n",
+         4096 * 256 * 64, bad & 1, (bad >> 1) & 1, (bad >> 2) & 1, (bad >> 3) & 1, (bad >> 4) & 1, (bad >> 5) & 1,
+         (bad >> 6) & 1, (bad >> 7) & 1);
   for (int w : {2, 4}) {
     if (time_chain<0>("fe_mul x4 (C)", dout, p.multiProcessorCount, w)) return 1;
     if (time_chain<1>("2 x fe_mul2 (asm)", dout, p.multiProcessorCount, w)) return 1;
