@@ -392,7 +392,7 @@ class C5:
                          "10%% secp256k1, 1%% corrupted) streamed from pinned host memory, H2D/D2H included"
                          % args.batch_log2)
         self.data = "synthetic: C2 and C3 corpora (GPU-signed), copied to pinned host memory before timing"
-        self.config = {"batch_per_gpu": n * self.passes, "ed25519": n_ed, "ecdsa": n_ec, "chunk": 1 << 22,
+        self.config = {"batch_per_gpu": n * self.passes, "ed25519": n_ed, "ecdsa": n_ec, "chunk": int(os.environ.get("CORDAHIP_STREAM_CHUNK", 1 << 23)),
                        "stages": 3}
         if args.global_log2:
             self.workload += "; strong scaling: a fixed 2^%d global batch, this rank's share = %d passes" % (

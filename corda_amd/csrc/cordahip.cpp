@@ -100,14 +100,20 @@ struct Stage {  // one pipeline slot: device buffers + its stream
   DevBuf keys, sigs, msgs, pre, status, verdict;
 };
 
-// one stage of the C5 streaming pipeline (cordahip_stream_verify)
+// one stage of the C5 streaming pipeline (cordahip_stream_verify): a stream
+// per section, so a chunk's ECDSA kernels (small, partly latency-bound: the
+// batch inversion) run beside its Ed25519 kernels instead of after them
 struct StreamStage {
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;     // Ed25519 section: H2D -> kernels -> D2H
+  hipStream_t ec_stream = nullptr;  // ECDSA section
+  hipEvent_t ed_copied = nullptr, ec_copied = nullptr;  // this stage's H2D done (PCIe order across chunks)
   DevBuf ed_keys, ed_sigs, ed_msgs, ed_status;
   DevBuf ec_scheme, ec_keys, ec_key_len, ec_sigs, ec_sig_len, ec_msgs, ec_status;
 };
 constexpr int kStreamStages = 3;
-constexpr uint64_t kStreamChunk = 1ull << 22;  // lanes per chunk, both sections together
+// lanes per chunk, both sections together (C5 A/B on one box, profiles/r02_c5_stream_ab.json:
+// 2^21 76.7, 2^22 82.4, 2^23 84.9, 2^24 84.6 M verifs/s with the single-stream stages)
+constexpr uint64_t kStreamChunk = 1ull << 23;
 
 struct TxWork {  // device buffers of the transaction paths (grow-only)
   DevBuf leaf_bytes, leaf_off, tx_leaf_off, hashes, txid, tx_status, tx_sig_off, msgs;
@@ -662,7 +668,12 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
 // [c0, c1) ECDSA lanes, streamed in chunks through kStreamStages stages. A
 // stage is reused only after its previous chunk (copies and kernels) is done,
 // so up to kStreamStages chunks are in flight: while one computes, the next
-// one's inputs and the previous one's statuses cross PCIe.
+// one's inputs and the previous one's statuses cross PCIe. Within a chunk the
+// two sections run on their own streams (the shared workspaces' events order
+// each section's kernels across chunks); the host-to-device copies are chained
+// in chunk order (each chunk's copies wait for the previous chunk's), so the
+// first chunk's inputs arrive at full PCIe rate instead of sharing it with
+// the copies of the chunks queued behind it.
 int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_t e1, uint64_t c0, uint64_t c1) {
   std::lock_guard<std::mutex> g(d.stream_mu);
   if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
@@ -672,7 +683,7 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
   // Chunk boundaries over the combined lane count T = ne + nc, each section cut
   // at the same fraction of its length (64-aligned). The first chunks ramp up
   // (chunk/16, chunk/4, then chunk): the GPU starts after a short first copy
-  // instead of a full chunk's H2D (~0.6 GB for C5), and PCIe (~4x faster than
+  // instead of a full chunk's H2D (~1.2 GB for C5), and PCIe (~4x faster than
   // the kernels per lane) stays ahead while the sizes grow.
   const uint64_t T = ne + nc;
   std::vector<uint64_t> bound(1, 0);  // cumulative combined lanes at chunk ends
@@ -693,8 +704,10 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
   }
   const uint64_t eml = b->ed_msg_len, cml = b->ec_msg_len;
   for (StreamStage& st : d.sstage) {
-    if (!st.stream && hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)
-      return CORDAHIP_ERR_HIP;
+    for (hipStream_t* ps : {&st.stream, &st.ec_stream})
+      if (!*ps && hipStreamCreateWithFlags(ps, hipStreamNonBlocking) != hipSuccess) return CORDAHIP_ERR_HIP;
+    for (hipEvent_t* pe : {&st.ed_copied, &st.ec_copied})
+      if (!*pe && hipEventCreateWithFlags(pe, hipEventDisableTiming) != hipSuccess) return CORDAHIP_ERR_HIP;
     if ((ce && (st.ed_keys.ensure(ce * 32) || st.ed_sigs.ensure(ce * 64) ||
                 st.ed_msgs.ensure(std::max<uint64_t>(ce * eml, 16)) || st.ed_status.ensure(ce))) ||
         (cc && (st.ec_scheme.ensure(cc) || st.ec_keys.ensure(cc * 65) || st.ec_key_len.ensure(cc) ||
@@ -703,26 +716,35 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
       return CORDAHIP_ERR_OUT_OF_MEMORY;
   }
   const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
+  hipEvent_t prev_copied = nullptr;  // the previous chunk's last H2D
   for (uint64_t k = 0; k < nchunks; k++) {
     StreamStage& st = d.sstage[k % kStreamStages];
-    hipStream_t s = st.stream;
-    if (k >= (uint64_t)kStreamStages && hipStreamSynchronize(s) != hipSuccess) return CORDAHIP_ERR_HIP;
+    hipStream_t s = st.stream, sc = st.ec_stream;
+    if (k >= (uint64_t)kStreamStages &&
+        (hipStreamSynchronize(s) != hipSuccess || hipStreamSynchronize(sc) != hipSuccess))
+      return CORDAHIP_ERR_HIP;
     const uint64_t a = e0 + cut(ne, k), ma = cut(ne, k + 1) - cut(ne, k);
     const uint64_t c = c0 + cut(nc, k), mc = cut(nc, k + 1) - cut(nc, k);
     hipError_t e = hipSuccess;
+    // copies: Ed25519 section on s, then the ECDSA section on sc, after the previous chunk's
+    if (prev_copied) e = hipStreamWaitEvent(s, prev_copied, 0);
     if (ma) {
       e = e ? e : hipMemcpyAsync(st.ed_keys.p, b->ed_keys + a * 32, ma * 32, h2d, s);
       e = e ? e : hipMemcpyAsync(st.ed_sigs.p, b->ed_sigs + a * 64, ma * 64, h2d, s);
       if (eml) e = e ? e : hipMemcpyAsync(st.ed_msgs.p, b->ed_msgs + a * eml, ma * eml, h2d, s);
     }
+    e = e ? e : hipEventRecord(st.ed_copied, s);
+    e = e ? e : hipStreamWaitEvent(sc, st.ed_copied, 0);
     if (mc) {
-      e = e ? e : hipMemcpyAsync(st.ec_scheme.p, b->ec_scheme + c, mc, h2d, s);
-      e = e ? e : hipMemcpyAsync(st.ec_keys.p, b->ec_keys + c * 65, mc * 65, h2d, s);
-      e = e ? e : hipMemcpyAsync(st.ec_key_len.p, b->ec_key_len + c, mc, h2d, s);
-      e = e ? e : hipMemcpyAsync(st.ec_sigs.p, b->ec_sigs + c * 72, mc * 72, h2d, s);
-      e = e ? e : hipMemcpyAsync(st.ec_sig_len.p, b->ec_sig_len + c, mc, h2d, s);
-      if (cml) e = e ? e : hipMemcpyAsync(st.ec_msgs.p, b->ec_msgs + c * cml, mc * cml, h2d, s);
+      e = e ? e : hipMemcpyAsync(st.ec_scheme.p, b->ec_scheme + c, mc, h2d, sc);
+      e = e ? e : hipMemcpyAsync(st.ec_keys.p, b->ec_keys + c * 65, mc * 65, h2d, sc);
+      e = e ? e : hipMemcpyAsync(st.ec_key_len.p, b->ec_key_len + c, mc, h2d, sc);
+      e = e ? e : hipMemcpyAsync(st.ec_sigs.p, b->ec_sigs + c * 72, mc * 72, h2d, sc);
+      e = e ? e : hipMemcpyAsync(st.ec_sig_len.p, b->ec_sig_len + c, mc, h2d, sc);
+      if (cml) e = e ? e : hipMemcpyAsync(st.ec_msgs.p, b->ec_msgs + c * cml, mc * cml, h2d, sc);
     }
+    e = e ? e : hipEventRecord(st.ec_copied, sc);
+    prev_copied = st.ec_copied;
     if (ma)
       e = e ? e
             : ed_verify_enqueue(d, st.ed_keys.as<uint8_t>(), st.ed_sigs.as<uint8_t>(), st.ed_msgs.as<uint8_t>(),
@@ -731,14 +753,15 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
       std::lock_guard<std::mutex> ge(d.ec_mu);
       e = ec_verify_enqueue(d, st.ec_scheme.as<uint8_t>(), st.ec_keys.as<uint8_t>(), st.ec_key_len.as<uint8_t>(),
                             st.ec_sigs.as<uint8_t>(), st.ec_sig_len.as<uint8_t>(), st.ec_msgs.as<uint8_t>(), nullptr,
-                            (uint32_t)cml, mc, nullptr, st.ec_status.as<uint8_t>(), nullptr, 0u, s);
+                            (uint32_t)cml, mc, nullptr, st.ec_status.as<uint8_t>(), nullptr, 0u, sc);
     }
     if (ma) e = e ? e : hipMemcpyAsync(b->ed_status + a, st.ed_status.p, ma, d2h, s);
-    if (mc) e = e ? e : hipMemcpyAsync(b->ec_status + c, st.ec_status.p, mc, d2h, s);
+    if (mc) e = e ? e : hipMemcpyAsync(b->ec_status + c, st.ec_status.p, mc, d2h, sc);
     if (e != hipSuccess) return CORDAHIP_ERR_HIP;
   }
   for (StreamStage& st : d.sstage)
-    if (hipStreamSynchronize(st.stream) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (hipStreamSynchronize(st.stream) != hipSuccess || hipStreamSynchronize(st.ec_stream) != hipSuccess)
+      return CORDAHIP_ERR_HIP;
   return CORDAHIP_SUCCESS;
 }
 
@@ -834,7 +857,10 @@ void free_device(Device& d) {
     for (DevBuf* b : {&st.ed_keys, &st.ed_sigs, &st.ed_msgs, &st.ed_status, &st.ec_scheme, &st.ec_keys,
                       &st.ec_key_len, &st.ec_sigs, &st.ec_sig_len, &st.ec_msgs, &st.ec_status})
       b->release();
-    if (st.stream) (void)hipStreamDestroy(st.stream);
+    for (hipStream_t ss : {st.stream, st.ec_stream})
+      if (ss) (void)hipStreamDestroy(ss);
+    for (hipEvent_t ev : {st.ed_copied, st.ec_copied})
+      if (ev) (void)hipEventDestroy(ev);
   }
   for (DevBuf* b : {&d.tx.leaf_bytes, &d.tx.leaf_off, &d.tx.tx_leaf_off, &d.tx.hashes, &d.tx.txid, &d.tx.tx_status,
                     &d.tx.tx_sig_off, &d.tx.msgs, &d.tx.tok, &d.tx.tok_hash, &d.tx.tx_tok_off, &d.tx.root,

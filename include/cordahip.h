@@ -159,7 +159,8 @@ int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_sc
  * asynchronous): an Ed25519 section (as cordahip_ed25519_verify_host) and an
  * ECDSA section (as cordahip_ecdsa_verify_device, 65/72-byte slots). Each
  * context device takes a contiguous shard of both sections and streams it in
- * chunks of up to 2^22 lanes through 3 stages (one HIP stream each), so the
+ * chunks of up to 2^23 lanes through 3 stages (two HIP streams each: one per
+ * section, so a chunk's ECDSA kernels run beside its Ed25519 kernels), so the
  * H2D copy of chunk k+1, the kernels of chunk k and the status D2H of chunk
  * k-1 overlap. Synchronous; statuses land in ed_status / ec_status.          */
 typedef struct {
