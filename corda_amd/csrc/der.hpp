@@ -55,15 +55,24 @@ CHD bool der_decode_sig(const uint8_t* sig, uint32_t n, DerInt& r, DerInt& s) {
     const uint8_t* body = sig + i;
     if (l > 1 && ((body[0] == 0 && body[1] < 0x80) || (body[0] == 0xff && body[1] >= 0x80))) return false;
     d.neg = body[0] >= 0x80;
-    uint32_t start = 0;
-    while (start < l && body[start] == 0) start++;
-    d.big = (l - start) > 32;
+    // more than 32 significant bytes: a nonzero byte above significance 31
+    uint32_t hi = 0;
+    for (uint32_t t = 0; t + 32 < l; t++) hi |= body[t];
+    d.big = hi != 0;
+    // the low 32 bytes by significance k (unrolled: every limb index is a
+    // compile-time constant, so the limbs stay in registers on the GPU instead
+    // of a scratch-memory array written byte by byte)
+#pragma unroll
     for (int q = 0; q < 8; q++) d.v[q] = 0;
-    if (!d.big) {
-      for (uint32_t t = start; t < l; t++) {
-        const uint32_t pos = l - 1 - t;  // byte significance
-        d.v[pos >> 2] |= (uint32_t)body[t] << (8 * (pos & 3));
-      }
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+      const bool in = (uint32_t)k < l;
+      const uint32_t b = body[in ? l - 1 - k : 0] & (in ? 0xffu : 0u);  // address always inside the body
+      d.v[k >> 2] |= b << (8 * (k & 3));
+    }
+    if (d.big) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) d.v[q] = 0;
     }
     i += l;
   }
