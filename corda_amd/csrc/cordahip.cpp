@@ -100,13 +100,11 @@ struct Stage {  // one pipeline slot: device buffers + its stream
   DevBuf keys, sigs, msgs, pre, status, verdict;
 };
 
-// one stage of the C5 streaming pipeline (cordahip_stream_verify): a stream
-// per section, so a chunk's ECDSA kernels (small, partly latency-bound: the
-// batch inversion) run beside its Ed25519 kernels instead of after them
+// one stage (buffer set) of the C5 streaming pipeline (cordahip_stream_verify);
+// its events order the reuse of the buffers, so the host never waits per chunk
 struct StreamStage {
-  hipStream_t stream = nullptr;     // Ed25519 section: H2D -> kernels -> D2H
-  hipStream_t ec_stream = nullptr;  // ECDSA section
-  hipEvent_t ed_copied = nullptr, ec_copied = nullptr;  // this stage's H2D done (PCIe order across chunks)
+  hipEvent_t ed_copied = nullptr, ec_copied = nullptr;  // this chunk's H2D of each section done
+  hipEvent_t ed_done = nullptr, ec_done = nullptr;      // its kernels and status D2H done: buffers free
   DevBuf ed_keys, ed_sigs, ed_msgs, ed_status;
   DevBuf ec_scheme, ec_keys, ec_key_len, ec_sigs, ec_sig_len, ec_msgs, ec_status;
 };
@@ -161,8 +159,14 @@ struct Device {
   std::mutex ed_mu;
   DevBuf ed_ws;
   hipEvent_t ed_ev = nullptr;
-  std::mutex stream_mu;  // serialises use of sstage
+  std::mutex stream_mu;  // serialises use of sstage and the drain streams
   StreamStage sstage[kStreamStages];
+  // the drain's three streams, created together: every H2D on s_copy (PCIe in
+  // chunk order), each section's kernels + status D2H on its own stream. Three
+  // active streams, not one per stage and section: HIP maps streams onto
+  // GPU_MAX_HW_QUEUES (4) hardware queues, and streams sharing a queue
+  // serialise (with 6 stage streams C5 ran 90.6 M/s at 4 queues, 93.4 at 8).
+  hipStream_t s_copy = nullptr, s_ed = nullptr, s_ec = nullptr;
 };
 
 // device uid -> ring slot of this thread's most recent timed call
@@ -665,15 +669,14 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
 }
 
 // C5: one device's contiguous shard of both sections, [e0, e1) Ed25519 and
-// [c0, c1) ECDSA lanes, streamed in chunks through kStreamStages stages. A
-// stage is reused only after its previous chunk (copies and kernels) is done,
-// so up to kStreamStages chunks are in flight: while one computes, the next
-// one's inputs and the previous one's statuses cross PCIe. Within a chunk the
-// two sections run on their own streams (the shared workspaces' events order
-// each section's kernels across chunks); the host-to-device copies are chained
-// in chunk order (each chunk's copies wait for the previous chunk's), so the
-// first chunk's inputs arrive at full PCIe rate instead of sharing it with
-// the copies of the chunks queued behind it.
+// [c0, c1) ECDSA lanes, streamed in chunks through kStreamStages buffer sets.
+// The host enqueues every chunk at once; events do the ordering: a chunk's H2D
+// (on s_copy, so PCIe serves the chunks in order and the first one arrives at
+// full rate) waits until its stage's previous chunk has finished with the
+// buffers; each section's kernels wait for that section's copies. While one
+// chunk computes, the next chunks' inputs and the previous chunk's statuses
+// cross PCIe, and a chunk's ECDSA kernels (small, the batch inversion
+// latency-bound) run beside its Ed25519 ladder on their own stream.
 int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_t e1, uint64_t c0, uint64_t c1) {
   std::lock_guard<std::mutex> g(d.stream_mu);
   if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
@@ -703,11 +706,22 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
     cc = std::max(cc, cut(nc, k + 1) - cut(nc, k));
   }
   const uint64_t eml = b->ed_msg_len, cml = b->ec_msg_len;
+  if (!d.s_copy) {
+    // the ECDSA stream at the higher priority: HIP gives it a hardware queue
+    // of its own (at normal priority it shared one with s_ed, and the two
+    // sections' kernels ran one after the other)
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithFlags(&d.s_copy, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&d.s_ed, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&d.s_ec, hipStreamNonBlocking, hi) != hipSuccess)
+      return CORDAHIP_ERR_HIP;
+  }
   for (StreamStage& st : d.sstage) {
-    for (hipStream_t* ps : {&st.stream, &st.ec_stream})
-      if (!*ps && hipStreamCreateWithFlags(ps, hipStreamNonBlocking) != hipSuccess) return CORDAHIP_ERR_HIP;
-    for (hipEvent_t* pe : {&st.ed_copied, &st.ec_copied})
+    for (hipEvent_t* pe : {&st.ed_copied, &st.ec_copied, &st.ed_done, &st.ec_done})
       if (!*pe && hipEventCreateWithFlags(pe, hipEventDisableTiming) != hipSuccess) return CORDAHIP_ERR_HIP;
+    // a grow replaces buffers: the previous call's work on them is finished
+    // (every call synchronises its streams before returning)
     if ((ce && (st.ed_keys.ensure(ce * 32) || st.ed_sigs.ensure(ce * 64) ||
                 st.ed_msgs.ensure(std::max<uint64_t>(ce * eml, 16)) || st.ed_status.ensure(ce))) ||
         (cc && (st.ec_scheme.ensure(cc) || st.ec_keys.ensure(cc * 65) || st.ec_key_len.ensure(cc) ||
@@ -716,52 +730,51 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
       return CORDAHIP_ERR_OUT_OF_MEMORY;
   }
   const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
-  hipEvent_t prev_copied = nullptr;  // the previous chunk's last H2D
-  for (uint64_t k = 0; k < nchunks; k++) {
+  hipStream_t cs = d.s_copy, es = d.s_ed, xs = d.s_ec;
+  hipError_t e = hipSuccess;
+  for (uint64_t k = 0; k < nchunks && e == hipSuccess; k++) {
     StreamStage& st = d.sstage[k % kStreamStages];
-    hipStream_t s = st.stream, sc = st.ec_stream;
-    if (k >= (uint64_t)kStreamStages &&
-        (hipStreamSynchronize(s) != hipSuccess || hipStreamSynchronize(sc) != hipSuccess))
-      return CORDAHIP_ERR_HIP;
     const uint64_t a = e0 + cut(ne, k), ma = cut(ne, k + 1) - cut(ne, k);
     const uint64_t c = c0 + cut(nc, k), mc = cut(nc, k + 1) - cut(nc, k);
-    hipError_t e = hipSuccess;
-    // copies: Ed25519 section on s, then the ECDSA section on sc, after the previous chunk's
-    if (prev_copied) e = hipStreamWaitEvent(s, prev_copied, 0);
+    if (k >= (uint64_t)kStreamStages) {  // the stage's buffers: chunk k-3 must be done with them
+      e = hipStreamWaitEvent(cs, st.ed_done, 0);
+      e = e ? e : hipStreamWaitEvent(cs, st.ec_done, 0);
+    }
     if (ma) {
-      e = e ? e : hipMemcpyAsync(st.ed_keys.p, b->ed_keys + a * 32, ma * 32, h2d, s);
-      e = e ? e : hipMemcpyAsync(st.ed_sigs.p, b->ed_sigs + a * 64, ma * 64, h2d, s);
-      if (eml) e = e ? e : hipMemcpyAsync(st.ed_msgs.p, b->ed_msgs + a * eml, ma * eml, h2d, s);
+      e = e ? e : hipMemcpyAsync(st.ed_keys.p, b->ed_keys + a * 32, ma * 32, h2d, cs);
+      e = e ? e : hipMemcpyAsync(st.ed_sigs.p, b->ed_sigs + a * 64, ma * 64, h2d, cs);
+      if (eml) e = e ? e : hipMemcpyAsync(st.ed_msgs.p, b->ed_msgs + a * eml, ma * eml, h2d, cs);
     }
-    e = e ? e : hipEventRecord(st.ed_copied, s);
-    e = e ? e : hipStreamWaitEvent(sc, st.ed_copied, 0);
+    e = e ? e : hipEventRecord(st.ed_copied, cs);
     if (mc) {
-      e = e ? e : hipMemcpyAsync(st.ec_scheme.p, b->ec_scheme + c, mc, h2d, sc);
-      e = e ? e : hipMemcpyAsync(st.ec_keys.p, b->ec_keys + c * 65, mc * 65, h2d, sc);
-      e = e ? e : hipMemcpyAsync(st.ec_key_len.p, b->ec_key_len + c, mc, h2d, sc);
-      e = e ? e : hipMemcpyAsync(st.ec_sigs.p, b->ec_sigs + c * 72, mc * 72, h2d, sc);
-      e = e ? e : hipMemcpyAsync(st.ec_sig_len.p, b->ec_sig_len + c, mc, h2d, sc);
-      if (cml) e = e ? e : hipMemcpyAsync(st.ec_msgs.p, b->ec_msgs + c * cml, mc * cml, h2d, sc);
+      e = e ? e : hipMemcpyAsync(st.ec_scheme.p, b->ec_scheme + c, mc, h2d, cs);
+      e = e ? e : hipMemcpyAsync(st.ec_keys.p, b->ec_keys + c * 65, mc * 65, h2d, cs);
+      e = e ? e : hipMemcpyAsync(st.ec_key_len.p, b->ec_key_len + c, mc, h2d, cs);
+      e = e ? e : hipMemcpyAsync(st.ec_sigs.p, b->ec_sigs + c * 72, mc * 72, h2d, cs);
+      e = e ? e : hipMemcpyAsync(st.ec_sig_len.p, b->ec_sig_len + c, mc, h2d, cs);
+      if (cml) e = e ? e : hipMemcpyAsync(st.ec_msgs.p, b->ec_msgs + c * cml, mc * cml, h2d, cs);
     }
-    e = e ? e : hipEventRecord(st.ec_copied, sc);
-    prev_copied = st.ec_copied;
+    e = e ? e : hipEventRecord(st.ec_copied, cs);
+    e = e ? e : hipStreamWaitEvent(es, st.ed_copied, 0);
     if (ma)
       e = e ? e
             : ed_verify_enqueue(d, st.ed_keys.as<uint8_t>(), st.ed_sigs.as<uint8_t>(), st.ed_msgs.as<uint8_t>(),
-                                (uint32_t)eml, ma, nullptr, st.ed_status.as<uint8_t>(), nullptr, 0u, s);
+                                (uint32_t)eml, ma, nullptr, st.ed_status.as<uint8_t>(), nullptr, 0u, es);
+    if (ma) e = e ? e : hipMemcpyAsync(b->ed_status + a, st.ed_status.p, ma, d2h, es);
+    e = e ? e : hipEventRecord(st.ed_done, es);
+    e = e ? e : hipStreamWaitEvent(xs, st.ec_copied, 0);
     if (mc && e == hipSuccess) {
       std::lock_guard<std::mutex> ge(d.ec_mu);
       e = ec_verify_enqueue(d, st.ec_scheme.as<uint8_t>(), st.ec_keys.as<uint8_t>(), st.ec_key_len.as<uint8_t>(),
                             st.ec_sigs.as<uint8_t>(), st.ec_sig_len.as<uint8_t>(), st.ec_msgs.as<uint8_t>(), nullptr,
-                            (uint32_t)cml, mc, nullptr, st.ec_status.as<uint8_t>(), nullptr, 0u, sc);
+                            (uint32_t)cml, mc, nullptr, st.ec_status.as<uint8_t>(), nullptr, 0u, xs);
     }
-    if (ma) e = e ? e : hipMemcpyAsync(b->ed_status + a, st.ed_status.p, ma, d2h, s);
-    if (mc) e = e ? e : hipMemcpyAsync(b->ec_status + c, st.ec_status.p, mc, d2h, sc);
-    if (e != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (mc) e = e ? e : hipMemcpyAsync(b->ec_status + c, st.ec_status.p, mc, d2h, xs);
+    e = e ? e : hipEventRecord(st.ec_done, xs);
   }
-  for (StreamStage& st : d.sstage)
-    if (hipStreamSynchronize(st.stream) != hipSuccess || hipStreamSynchronize(st.ec_stream) != hipSuccess)
-      return CORDAHIP_ERR_HIP;
+  // drain all three streams even after an error, so no queued work outlives the call
+  const hipError_t e1s = hipStreamSynchronize(cs), e2s = hipStreamSynchronize(es), e3s = hipStreamSynchronize(xs);
+  if (e != hipSuccess || e1s != hipSuccess || e2s != hipSuccess || e3s != hipSuccess) return CORDAHIP_ERR_HIP;
   return CORDAHIP_SUCCESS;
 }
 
@@ -857,11 +870,11 @@ void free_device(Device& d) {
     for (DevBuf* b : {&st.ed_keys, &st.ed_sigs, &st.ed_msgs, &st.ed_status, &st.ec_scheme, &st.ec_keys,
                       &st.ec_key_len, &st.ec_sigs, &st.ec_sig_len, &st.ec_msgs, &st.ec_status})
       b->release();
-    for (hipStream_t ss : {st.stream, st.ec_stream})
-      if (ss) (void)hipStreamDestroy(ss);
-    for (hipEvent_t ev : {st.ed_copied, st.ec_copied})
+    for (hipEvent_t ev : {st.ed_copied, st.ec_copied, st.ed_done, st.ec_done})
       if (ev) (void)hipEventDestroy(ev);
   }
+  for (hipStream_t ss : {d.s_copy, d.s_ed, d.s_ec})
+    if (ss) (void)hipStreamDestroy(ss);
   for (DevBuf* b : {&d.tx.leaf_bytes, &d.tx.leaf_off, &d.tx.tx_leaf_off, &d.tx.hashes, &d.tx.txid, &d.tx.tx_status,
                     &d.tx.tx_sig_off, &d.tx.msgs, &d.tx.tok, &d.tx.tok_hash, &d.tx.tx_tok_off, &d.tx.root,
                     &d.tx.stack})

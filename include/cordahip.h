@@ -159,10 +159,13 @@ int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_sc
  * asynchronous): an Ed25519 section (as cordahip_ed25519_verify_host) and an
  * ECDSA section (as cordahip_ecdsa_verify_device, 65/72-byte slots). Each
  * context device takes a contiguous shard of both sections and streams it in
- * chunks of up to 2^23 lanes through 3 stages (two HIP streams each: one per
- * section, so a chunk's ECDSA kernels run beside its Ed25519 kernels), so the
- * H2D copy of chunk k+1, the kernels of chunk k and the status D2H of chunk
- * k-1 overlap. Synchronous; statuses land in ed_status / ec_status.          */
+ * chunks of up to 2^23 lanes through 3 device buffer sets on three HIP
+ * streams (every H2D on one copy stream; each section's kernels and status
+ * D2H on its own stream, so a chunk's ECDSA kernels run beside its Ed25519
+ * kernels), so the H2D copy of chunk k+1, the kernels of chunk k and the
+ * status D2H of chunk k-1 overlap. All of the batch's host buffers, statuses
+ * included, must be pinned. Synchronous; statuses land in ed_status /
+ * ec_status.                                                                  */
 typedef struct {
   uint64_t n_ed;
   const uint8_t* ed_keys; /* [n_ed*32] */
