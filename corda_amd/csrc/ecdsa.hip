@@ -296,8 +296,8 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
   f29_mul_pair<F>(u2, x2, z1z1, s2, t, z1z1);
   f29_sub_red<F>(h, u2, p.X);
   f29_sub_red<F>(rr, s2, p.Y);
-  if (f29_iszero<F>(h)) {
-    if (f29_iszero<F>(rr)) {
+  if (f29_iszero_norm<F>(h)) {  // h, rr norm (f29_sub_red outputs)
+    if (f29_iszero_norm<F>(rr)) {
       jdbl<C>(r, p);
     } else {
       r.inf = true;

@@ -296,6 +296,27 @@ CDEV bool f29_iszero(const f29& a) {
   return x == 0;
 }
 
+// a == 0 (mod p) for a NORM a (value < 2p, as every f29_*_red output): one
+// carry pass gives the unique radix-2^29 limbs of the value, which is then 0
+// or p. No fold and no conditional subtraction (f29_iszero canonicalises any
+// a < 2^260): the additions' exceptional-case test on H runs once per addition.
+template <class F>
+CDEV bool f29_iszero_norm(const f29& a) {
+  uint32_t c = 0, z = 0, dp = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t s = a.v[i] + c;
+    const uint32_t l = s & kMask29;
+    c = s >> 29;
+    z |= l;
+    dp |= l ^ F::m(i);
+  }
+  const uint32_t top = a.v[8] + c;
+  z |= top;
+  dp |= top ^ F::m(8);
+  return z == 0 || dp == 0;
+}
+
 template <class F>
 CDEV bool f29_eq(const f29& a, const f29& b) {
   f29 x, y;

@@ -170,6 +170,20 @@ class Fp29:
     def iszero(self, a):
         return not any(self.canon(a))
 
+    def iszero_norm(self, a):
+        """fp29.hpp f29_iszero_norm: one carry pass, compare with 0 and p (a norm)."""
+        assert self.val(a) < 2 * self.p and all(0 <= x < U32 for x in a)
+        c, limbs = 0, []
+        for i in range(8):
+            s = a[i] + c
+            assert s < U32
+            limbs.append(s & M29)
+            c = s >> 29
+        limbs.append(a[8] + c)
+        r = limbs == [0] * 9 or limbs == list(self.m)
+        assert r == self.iszero(a)
+        return r
+
     def neg(self, a):
         return self.sub([0] * 9, a)
 
@@ -251,8 +265,8 @@ def jmadd(F, am3, P, x2, y2):
     z1z1, t = F.sqr(Z1), F.mul(y2, Z1)
     u2, s2 = F.mul(x2, z1z1), F.mul(t, z1z1)
     h, rr = F.subs_red(u2, X1), F.subs_red(s2, Y1)
-    if F.iszero(h):
-        return jdbl(F, am3, P) if F.iszero(rr) else None
+    if F.iszero_norm(h):
+        return jdbl(F, am3, P) if F.iszero_norm(rr) else None
     rr = F.add(rr, rr)
     hh, x3 = F.sqr(h), F.sqr(rr)
     i = F.add(hh, hh)
@@ -350,6 +364,34 @@ def test_exceptional_additions(scheme):
     assert jadd(F, am3, JP, jacobian(F, negP, rng)) is None                 # P - P -> infinity
     assert affine(F, jmadd(F, am3, JP, high(F, P[0], rng), high(F, P[1], rng))) == ec._add(c, P, P)
     assert jmadd(F, am3, JP, high(F, P[0], rng), F.neg(high(F, P[1], rng))) is None
+
+
+@pytest.mark.parametrize("scheme", [2, 3])
+def test_iszero_norm_on_sub_red_outputs(scheme):
+    """f29_iszero_norm agrees with the canonicalising test on every norm value
+    a sub_red can produce near 0 and p, including non-normalised limbs 0, 1
+    (fold outputs) and the two representatives 0 and p of zero."""
+    F = FIELDS[scheme]
+    rng = random.Random(30 + scheme)
+    p = F.p
+    vals = [0, 1, 2, p - 2, p - 1, p, p + 1, p + 2, 2 * p - 1] + [rng.randrange(2 * p) for _ in range(300)]
+    hits = 0
+    for a in vals:
+        for b in [0, 1, p - 1, p, a % p, (a + 1) % p] + [rng.randrange(2 * p) for _ in range(6)]:
+            m = F.mul(gen.limbs29(a), F.r2)             # a norm product output
+            bb = F.mul(gen.limbs29(b), F.r2)
+            h = F.subs_red(m, bb)                       # the addition's H = U2 - X1, as the kernel makes it
+            hits += F.iszero_norm(h)
+            F.iszero_norm(gen.limbs29(a))               # normalised limbs
+    assert hits > 0
+    # explicit non-normalised limbs: limb 0 carrying into limb 1 (fold excess)
+    for v in (0, p):
+        l = gen.limbs29(v)
+        if l[1] > 0:
+            l2 = list(l)
+            l2[1] -= 1
+            l2[0] += 1 << 29
+            assert F.iszero_norm(l2)
 
 
 def test_glv_split_bound():
