@@ -286,7 +286,7 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
   using F = typename C::F;
   if (p.inf) {
     r.X = x2;
-    r.Y = y2;
+    f29_red<F>(r.Y, y2);  // y2 may be f29_cneg_loose's 4p - y: back to norm
     f29_const_one<F>(r.Z);
     r.inf = false;
     return;
@@ -726,12 +726,12 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
         jdbl<C>(acc, acc);
       }
       if (e1) {
-        f29_cneg<F>(y1, (d1 < 0) != nb1);
+        f29_cneg_loose<F>(y1, (d1 < 0) != nb1);
         jmadd<C>(acc, acc, x1, y1);
       }
       if (e2) {
         f29_mul<F>(x2, x2, beta);  // phi([e2]Q)
-        f29_cneg<F>(y2, (d2 < 0) != nb2);
+        f29_cneg_loose<F>(y2, (d2 < 0) != nb2);
         jmadd<C>(acc, acc, x2, y2);
       }
       if (j % (kGBits / 4) == 0) {
@@ -739,12 +739,12 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
         f29 gx, gy;
         if (g1) {
           load_g(gx, gy, gtab, g1 < 0 ? -g1 : g1);
-          f29_cneg<F>(gy, (g1 < 0) != na1);
+          f29_cneg_loose<F>(gy, (g1 < 0) != na1);
           jmadd<C>(acc, acc, gx, gy);
         }
         if (g2) {
           load_g(gx, gy, gtab2, g2 < 0 ? -g2 : g2);
-          f29_cneg<F>(gy, (g2 < 0) != na2);
+          f29_cneg_loose<F>(gy, (g2 < 0) != na2);
           jmadd<C>(acc, acc, gx, gy);
         }
       }
@@ -765,7 +765,7 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
         jdbl<C>(acc, acc);
       }
       if (aq) {
-        f29_cneg<F>(ty, (dq < 0) != neg2);
+        f29_cneg_loose<F>(ty, (dq < 0) != neg2);
         jmadd<C>(acc, acc, tx, ty);
       }
       if (j % (kGBits / 4) == 0) {
@@ -773,7 +773,7 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
         if (dg) {
           f29 gx, gy;
           load_g(gx, gy, gtab, dg < 0 ? -dg : dg);
-          f29_cneg<F>(gy, (dg < 0) != neg1);
+          f29_cneg_loose<F>(gy, (dg < 0) != neg1);
           jmadd<C>(acc, acc, gx, gy);
         }
       }
@@ -799,7 +799,7 @@ CDEV void fixed_base_g(jpt& acc, const u256& k, const uint32_t* __restrict__ gta
     if (d != 0) {
       f29 gx, gy;
       load_g(gx, gy, gtab, d < 0 ? -d : d);
-      f29_cneg<F>(gy, (d < 0) != neg);
+      f29_cneg_loose<F>(gy, (d < 0) != neg);
       jmadd<C>(acc, acc, gx, gy);
     }
   }

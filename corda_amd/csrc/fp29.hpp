@@ -167,6 +167,18 @@ CDEV void f29_cneg(f29& r, bool neg) {
   for (int i = 0; i < 9; i++) r.v[i] = neg ? n.v[i] : r.v[i];
 }
 
+// The y of a mixed addition's affine point, conditionally negated without a
+// carry pass: 4p - a limb by limb (F::sub4p's limbs exceed those of any norm a,
+// so none goes negative). The result (value < 4p, limbs < 2^31.4) is only ever
+// the first operand of jmadd's y2 * Z1 product, whose column sums stay below
+// 2^64 (checked exactly by tests/test_fp29_model.py). 18 instructions instead
+// of f29_cneg's carry pass + select (~50).
+template <class F>
+CDEV void f29_cneg_loose(f29& r, bool neg) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = neg ? F::sub4p(i) - r.v[i] : r.v[i];
+}
+
 // limbs 0..7 of r normalised (< 2^29), top = the value's bits >= 2^232 (value
 // < 2^260)  ->  r norm, value < 2p: folds the bits >= 2^256.
 template <class F>

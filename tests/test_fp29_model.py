@@ -187,6 +187,15 @@ class Fp29:
     def neg(self, a):
         return self.sub([0] * 9, a)
 
+    def cneg_loose(self, a):
+        """fp29.hpp f29_cneg_loose (negating case): 4p - a limb by limb, no carry."""
+        s4 = self.skp[4]
+        assert self.val(a) < 2 * self.p and all(x < (1 << 29) + (1 << 15) for x in a[:8])
+        r = [s4[i] - a[i] for i in range(9)]
+        assert all(0 <= x < U32 for x in r)
+        assert self.val(r) == 4 * self.p - self.val(a)
+        return r
+
     def to_mont(self, x):
         return self.mul(gen.limbs29(x), self.r2)
 
@@ -260,7 +269,7 @@ def jadd(F, am3, P, Q):
 
 def jmadd(F, am3, P, x2, y2):
     if P is None:
-        return (x2, y2, list(F.one))
+        return (x2, F.red(y2), list(F.one))
     X1, Y1, Z1 = P
     z1z1, t = F.sqr(Z1), F.mul(y2, Z1)
     u2, s2 = F.mul(x2, z1z1), F.mul(t, z1z1)
@@ -392,6 +401,28 @@ def test_iszero_norm_on_sub_red_outputs(scheme):
             l2[1] -= 1
             l2[0] += 1 << 29
             assert F.iszero_norm(l2)
+
+
+@pytest.mark.parametrize("scheme", [2, 3])
+def test_mixed_addition_with_loose_negated_y(scheme):
+    """The ladder's table and fixed-base y, negated by f29_cneg_loose (4p - y,
+    no carry), into jmadd: every product column stays < 2^64 (F.mul asserts it),
+    the sum is P - Q, and the infinity branch returns a norm Y."""
+    F, c, am3 = FIELDS[scheme], ec.CURVES[scheme], AM3[scheme]
+    rng = random.Random(40 + scheme)
+    for _ in range(25):
+        P, Q = rand_point(c, rng), rand_point(c, rng)
+        JP = jacobian(F, P, rng)
+        xq, yq = high(F, Q[0], rng), high(F, Q[1], rng)
+        negQ = (Q[0], (-Q[1]) % F.p)
+        assert affine(F, jmadd(F, am3, JP, xq, F.cneg_loose(yq))) == ec._add(c, P, negQ)
+        S = jmadd(F, am3, None, xq, F.cneg_loose(yq))     # accumulator at infinity
+        assert F.val(S[1]) < 2 * F.p and affine(F, S) == negQ
+        assert affine(F, jdbl(F, am3, S)) == ec._add(c, negQ, negQ)
+    # extreme limbs: y = 0 (4p - 0) and y just below 2p
+    for yv in (0, 2 * F.p - 1):
+        y = gen.limbs29(yv)
+        F.mul(F.cneg_loose(y), gen.limbs29(2 * F.p - 1))
 
 
 def test_glv_split_bound():
