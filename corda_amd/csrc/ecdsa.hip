@@ -182,13 +182,14 @@ CDEV void jdbl(jpt& r, const jpt& p) {
   }
   f29 x3, y3, z3, t, u;
   if constexpr (C::kAm3) {
-    f29 delta, gamma, beta, a3, b4, yz;
+    f29 delta, gamma, x4, a3, b4, yz;
     f29_sqr_pair<F>(delta, p.Z, gamma, p.Y);
     f29_sub<F>(t, p.X, delta);  // < 4p
     f29_add(u, p.X, delta);     // < 4p
-    f29_mul_pair<F>(beta, p.X, gamma, a3, t, u);
+    f29_add(x4, p.X, p.X);
+    f29_add(x4, x4, x4);        // 4X < 8p, limbs < 2^31: (4X) gamma < 16 p^2 < R p
+    f29_mul_pair<F>(b4, x4, gamma, a3, t, u);  // 4 beta directly (no f29_mulk_red pass)
     f29_mulk_red<F, 3>(a3, a3);  // alpha = 3 (X - delta)(X + delta)
-    f29_mulk_red<F, 4>(b4, beta);
     f29_add(yz, p.Y, p.Z);
     f29_sqr_pair<F>(x3, a3, yz, yz);
     f29_sub2_red<F>(x3, x3, b4, b4);       // X3 = alpha^2 - 8 beta

@@ -215,9 +215,9 @@ def jdbl(F, am3, P):
     if am3:
         delta, gamma = F.sqr(Z), F.sqr(Y)
         t, u = F.sub(X, delta), F.add(X, delta)
-        beta, a3 = F.mul(X, gamma), F.mul(t, u)
+        x4 = F.add(F.add(X, X), F.add(X, X))
+        b4, a3 = F.mul(x4, gamma), F.mul(t, u)      # 4 beta = (4 X) gamma: no mulk_red pass
         a3 = F.mulk_red(a3, 3)
-        b4 = F.mulk_red(beta, 4)
         yz = F.add(Y, Z)
         x3, yz = F.sqr(a3), F.sqr(yz)
         x3 = F.subs_red(x3, b4, b4)
