@@ -167,7 +167,8 @@ CDEV void f29_sqr_mul_pair(f29& r0, const f29& a0, f29& r1, const f29& a1, const
 #endif
 }
 
-// 2P. a = -3: dbl-2001-b (3M + 5S); a = 0: dbl-2009-l (2M + 5S). Prime-order
+// 2P. a = -3: dbl-2001-b (3M + 5S); a = 0: dbl-2009-l (2M + 5S) with
+// D = 4XB as one product (3M + 4S). Prime-order
 // curves have no 2-torsion, so only the point at infinity is exceptional.
 // Every f29_sub / f29_red below respects fp29.hpp's operand bounds (value
 // bounds in units of p in the comments; modelled in tests/test_fp29_model.py).
@@ -199,12 +200,13 @@ CDEV void jdbl(jpt& r, const jpt& p) {
     f29_sqr_mul_pair<F>(t, t, y3, a3, u);  // 4 gamma^2, alpha (4 beta - X3)
     f29_sub2_red<F>(y3, y3, t, t);          // Y3 = alpha (4 beta - X3) - 8 gamma^2
   } else {
-    f29 A, B, Cc, D, E;
+    f29 A, B, Cc, D, E, x4;
     f29_sqr_pair<F>(A, p.X, B, p.Y);
-    f29_add(t, p.X, B);
-    f29_sqr_pair<F>(Cc, B, t, t);
-    f29_sub2_red<F>(t, t, A, Cc);
-    f29_mulk_red<F, 2>(D, t);    // D = 2 ((X + B)^2 - A - C)
+    f29_add(x4, p.X, p.X);
+    f29_add(x4, x4, x4);         // 4X < 8p, limbs < 2^31: (4X) B < 16 p^2 < R p
+    // D = 2 ((X + B)^2 - A - C) = 4 X B as one product: cheaper than the
+    // square, the subtract pass and the doubling pass it replaces
+    f29_sqr_mul_pair<F>(Cc, B, D, x4, B);
     f29_mulk_red<F, 3>(E, A);    // E = 3 A
     f29_add(t, p.Y, p.Y);
     f29_sqr_mul_pair<F>(x3, E, z3, t, p.Z);  // E^2, Z3 = 2 Y Z

@@ -228,10 +228,8 @@ def jdbl(F, am3, P):
         y3 = F.subs_red(y3, t, t)
     else:
         A, B = F.sqr(X), F.sqr(Y)
-        t = F.add(X, B)
-        C, t = F.sqr(B), F.sqr(t)
-        t = F.subs_red(t, A, C)
-        D = F.mulk_red(t, 2)
+        x4 = F.add(F.add(X, X), F.add(X, X))
+        C, D = F.sqr(B), F.mul(x4, B)           # D = 2((X + B)^2 - A - C) = 4 X B, one product
         E = F.mulk_red(A, 3)
         t = F.add(Y, Y)
         x3, z3 = F.sqr(E), F.mul(t, Z)
