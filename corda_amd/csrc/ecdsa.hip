@@ -195,7 +195,7 @@ CDEV void jdbl(jpt& r, const jpt& p) {
     f29_sqr_pair<F>(x3, a3, yz, yz);
     f29_sub2_red<F>(x3, x3, b4, b4);       // X3 = alpha^2 - 8 beta
     f29_sub2_red<F>(z3, yz, gamma, delta);  // Z3 = (Y + Z)^2 - gamma - delta
-    f29_sub<F>(u, b4, x3);
+    f29_sub_loose<F>(u, b4, x3);  // < 6p, only the operand of alpha * u
     f29_add(t, gamma, gamma);
     f29_sqr_mul_pair<F>(t, t, y3, a3, u);  // 4 gamma^2, alpha (4 beta - X3)
     f29_sub2_red<F>(y3, y3, t, t);          // Y3 = alpha (4 beta - X3) - 8 gamma^2
@@ -211,7 +211,7 @@ CDEV void jdbl(jpt& r, const jpt& p) {
     f29_add(t, p.Y, p.Y);
     f29_sqr_mul_pair<F>(x3, E, z3, t, p.Z);  // E^2, Z3 = 2 Y Z
     f29_sub2_red<F>(x3, x3, D, D);           // X3 = E^2 - 2 D
-    f29_sub<F>(t, D, x3);
+    f29_sub_loose<F>(t, D, x3);  // < 6p, only the operand of E * t
     f29_mul<F>(y3, E, t);
     f29_mulk_red<F, 4>(u, Cc);   // 4 C
     f29_sub2_red<F>(y3, y3, u, u);  // Y3 = E (D - X3) - 8 C

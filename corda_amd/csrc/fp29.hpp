@@ -167,6 +167,16 @@ CDEV void f29_cneg(f29& r, bool neg) {
   for (int i = 0; i < 9; i++) r.v[i] = neg ? n.v[i] : r.v[i];
 }
 
+// a - b + 4p limb by limb, no carry pass (F::sub4p's limbs exceed a norm b's):
+// value < a + 4p, limbs < a's + 2^31.4. Only as the operand of a product whose
+// other operand is norm (columns < 2^63.9; tests/test_fp29_model.py): the
+// doublings' 4 beta - X3 (P-256) and D - X3 (secp256k1).
+template <class F>
+CDEV void f29_sub_loose(f29& r, const f29& a, const f29& b) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = a.v[i] + F::sub4p(i) - b.v[i];
+}
+
 // The y of a mixed addition's affine point, conditionally negated without a
 // carry pass: 4p - a limb by limb (F::sub4p's limbs exceed those of any norm a,
 // so none goes negative). The result (value < 4p, limbs < 2^31.4) is only ever

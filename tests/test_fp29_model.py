@@ -187,6 +187,15 @@ class Fp29:
     def neg(self, a):
         return self.sub([0] * 9, a)
 
+    def sub_loose(self, a, b):
+        """fp29.hpp f29_sub_loose: a + 4p - b limb by limb, no carry."""
+        s4 = self.skp[4]
+        assert self.val(b) <= 2 * self.p and all(x < (1 << 29) + (1 << 15) for x in b[:8])
+        r = [a[i] + s4[i] - b[i] for i in range(9)]
+        assert all(0 <= x < U32 for x in r)
+        assert self.val(r) == self.val(a) + 4 * self.p - self.val(b)
+        return r
+
     def cneg_loose(self, a):
         """fp29.hpp f29_cneg_loose (negating case): 4p - a limb by limb, no carry."""
         s4 = self.skp[4]
@@ -222,7 +231,7 @@ def jdbl(F, am3, P):
         x3, yz = F.sqr(a3), F.sqr(yz)
         x3 = F.subs_red(x3, b4, b4)
         z3 = F.subs_red(yz, gamma, delta)
-        u = F.sub(b4, x3)
+        u = F.sub_loose(b4, x3)
         t = F.add(gamma, gamma)
         t, y3 = F.sqr(t), F.mul(a3, u)
         y3 = F.subs_red(y3, t, t)
@@ -234,7 +243,7 @@ def jdbl(F, am3, P):
         t = F.add(Y, Y)
         x3, z3 = F.sqr(E), F.mul(t, Z)
         x3 = F.subs_red(x3, D, D)
-        y3 = F.mul(E, F.sub(D, x3))
+        y3 = F.mul(E, F.sub_loose(D, x3))
         u = F.mulk_red(C, 4)
         y3 = F.subs_red(y3, u, u)
     return (x3, y3, z3)
