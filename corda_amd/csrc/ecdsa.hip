@@ -127,6 +127,25 @@ struct jpt {
 #ifndef EC_USE_ASM2
 #define EC_USE_ASM2 1
 #endif
+// single products of the ladder's formulas (no partner): one asm chain each
+template <class F>
+CDEV void f29_mul1(f29& r, const f29& a, const f29& b) {
+#if EC_USE_ASM2
+  if constexpr (F::kRed == 1) f29a_mul_k1(r, a, b);
+  else f29a_mul_r1(r, a, b);
+#else
+  f29_mul<F>(r, a, b);
+#endif
+}
+template <class F>
+CDEV void f29_sqr1(f29& r, const f29& a) {
+#if EC_USE_ASM2
+  if constexpr (F::kRed == 1) f29a_sqr_k1(r, a);
+  else f29a_sqr_r1(r, a);
+#else
+  f29_sqr<F>(r, a);
+#endif
+}
 template <class F>
 CDEV void f29_mul_pair(f29& r0, const f29& a0, const f29& b0, f29& r1, const f29& a1, const f29& b1) {
 #if EC_USE_ASM2
@@ -212,7 +231,7 @@ CDEV void jdbl(jpt& r, const jpt& p) {
     f29_sqr_mul_pair<F>(x3, E, z3, t, p.Z);  // E^2, Z3 = 2 Y Z
     f29_sub2_red<F>(x3, x3, D, D);           // X3 = E^2 - 2 D
     f29_sub_loose<F>(t, D, x3);  // < 6p, only the operand of E * t
-    f29_mul<F>(y3, E, t);
+    f29_mul1<F>(y3, E, t);
     f29_mulk_red<F, 4>(u, Cc);   // 4 C
     f29_sub2_red<F>(y3, y3, u, u);  // Y3 = E (D - X3) - 8 C
   }
@@ -317,7 +336,7 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
   f29_mul_pair<F>(y3, rr, t, t, p.Y, j);
   f29_sub2_red<F>(y3, y3, t, t);     // Y3 = r (V - X3) - 2 Y1 J
   f29_add(t, p.Z, h);
-  f29_sqr<F>(t, t);
+  f29_sqr1<F>(t, t);
   f29_sub2_red<F>(z3, t, z1z1, hh);  // Z3 = (Z1 + H)^2 - Z1Z1 - HH
   r.X = x3;
   r.Y = y3;
@@ -733,7 +752,7 @@ CDEV uint8_t ecdsa_ladder_lane(const uint32_t* __restrict__ rec, const uint32_t*
         jmadd<C>(acc, acc, x1, y1);
       }
       if (e2) {
-        f29_mul<F>(x2, x2, beta);  // phi([e2]Q)
+        f29_mul1<F>(x2, x2, beta);  // phi([e2]Q)
         f29_cneg_loose<F>(y2, (d2 < 0) != nb2);
         jmadd<C>(acc, acc, x2, y2);
       }

@@ -2,7 +2,7 @@
 """Generate corda_amd/csrc/fp29_asm.hpp: radix-2^29 Montgomery products
 (fp29.hpp f29_mul / f29_sqr, R = 2^261) of TWO independent operand pairs as one
 gfx950 inline-asm block, per curve (secp256k1 "k1", P-256 "r1") and per pair
-shape (mul+mul, sqr+sqr, sqr+mul).
+shape (mul+mul, sqr+sqr, sqr+mul), plus single mul / sqr blocks.
 
 Same reason as tools/gen_fe_asm.py: product scanning keeps ONE running 64-bit
 accumulator per product (column k's sum continues from column k-1's, shifted
@@ -152,7 +152,7 @@ def gen(curve, kinds):
             # 2a as an add: v_add_u32 issues at ~2.3 cycles, v_lshlrev_b32 at ~4.0
             cols[0] = ["v_add_u32 %%[a2_%d_%d], %%[a%d_%d], %%[a%d_%d]" % (j, p, j, p, j, p) for j in range(8)] + cols[0]
         per.append(cols)
-    lines = interleave(per[0], per[1])
+    lines = interleave(per[0], per[1]) if len(per) == 2 else [l for col in per[0] for l in col]
     body = "\n".join('        "%s\\n"' % l for l in lines)
     outs, ins = [], []
     decl = []
@@ -199,6 +199,10 @@ FUNCS = (
     (("mul", "mul"), "mul_mul", "f29& r0, const f29& a0, const f29& b0, f29& r1, const f29& a1, const f29& b1"),
     (("sqr", "sqr"), "sqr_sqr", "f29& r0, const f29& a0, f29& r1, const f29& a1"),
     (("sqr", "mul"), "sqr_mul", "f29& r0, const f29& a0, f29& r1, const f29& a1, const f29& b1"),
+    # single products (no partner in the formula): still one asm chain, so the
+    # accumulator stays the mad addend (LLVM's version re-associates: +17 adds)
+    (("mul",), "mul", "f29& r0, const f29& a0, const f29& b0"),
+    (("sqr",), "sqr", "f29& r0, const f29& a0"),
 )
 
 
@@ -208,18 +212,19 @@ def render():
     for curve in ("k1", "r1"):
         for kinds, name, sig in FUNCS:
             body, outs, ins, decl = gen(curve, kinds)
+            n = len(kinds)
             parts.append('''CDEV void f29a_%s_%s(%s) {
-  f29 o0, o1;
+  f29 %s;
   %s
   asm(
 %s
       : %s
       : %s
       : "vcc", FE_ASM_ACC_CLOBBERS);
-  r0 = o0;
-  r1 = o1;
+%s
 }
-''' % (name, curve, sig, decl, body, outs, ins))
+''' % (name, curve, sig, ", ".join("o%d" % p for p in range(n)), decl, body, outs, ins,
+       "\n".join("  r%d = o%d;" % (p, p) for p in range(n))))
     parts.append("}  // namespace cordahip\n")
     return "\n".join(parts)
 
