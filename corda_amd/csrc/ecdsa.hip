@@ -1200,7 +1200,7 @@ CDEV void ecdsa_affine_lane(uint32_t* __restrict__ rec) {
 // One kernel per curve (launched over the whole chunk; the other curve's lanes
 // exit at once, and the partition makes them whole waves): the register
 // allocations differ (P-256 fits 164 VGPRs = 3 waves per SIMD, secp256k1's
-// GLV ladder needs ~214 = 2 waves), and a combined kernel runs both at the
+// GLV ladder needs ~221 = 2 waves), and a combined kernel runs both at the
 // larger one.
 template <int S>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ecdsa_ladder_kernel(
