@@ -48,14 +48,99 @@ def _oracle():
     return load_oracle()
 
 
+def _cgroup_cpus():
+    """CPUs granted by the cgroup's CPU quota (cgroup v2 cpu.max, v1 cfs files), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else max(1, -(-q // per))
+    except (OSError, ValueError):
+        return None
+
+
 def _cores():
-    return max(1, min(16, os.cpu_count() or 1))
+    """Host threads for the CPU legs: every CPU this process may run on
+    (sched_getaffinity), capped by the cgroup CPU quota when one is set (more
+    threads than the quota only time-slice), shared evenly by the ranks."""
+    n = len(os.sched_getaffinity(0))
+    q = _cgroup_cpus()
+    if q:
+        n = min(n, q)
+    return max(1, n // int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+
+
+def _cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": _cgroup_cpus(),
+            "os_cpu_count": os.cpu_count()}
+
+
+def _ed_oracle_check(eng_status, keys, sigs, msgs, idx):
+    """Oracle statuses for the lanes idx of a device Ed25519 batch vs the GPU's
+    (oracle/c, the checker: construction-open lanes, e.g. slide()-dependent S)."""
+    import numpy as np
+    orc = _oracle()
+    m = int(idx.numel())
+    if m == 0:
+        return {"lanes": 0, "mismatches": 0}
+    k = keys[idx].cpu().numpy().copy()
+    s = sigs[idx].cpu().numpy().copy()
+    g = msgs[idx].cpu().numpy().copy()
+    out = np.zeros(m, np.uint8)
+    orc.oracle_ed25519_verify_batch(m, k.ctypes.data, s.ctypes.data, g.ctypes.data, g.shape[1], out.ctypes.data,
+                                    _cores())
+    got = eng_status[idx].cpu().numpy()
+    return {"lanes": m, "mismatches": int((out != got).sum()), "oracle_accepted": int((out == 0).sum())}
+
+
+def _ec_oracle_check(status, scheme, keys, key_len, sigs, sig_len, msgs, idx):
+    """Oracle statuses for lanes idx of a slot-layout ECDSA batch vs the GPU's."""
+    import numpy as np
+    orc = _oracle()
+    m = int(idx.numel())
+    if m == 0:
+        return {"lanes": 0, "mismatches": 0}
+    sc = scheme[idx].cpu().numpy().copy()
+    kl = key_len[idx].cpu().numpy().astype(np.uint64)
+    sl = sig_len[idx].cpu().numpy().astype(np.uint64)
+    K = keys[idx].cpu().numpy()
+    S = sigs[idx].cpu().numpy()
+    M = np.ascontiguousarray(msgs[idx].cpu().numpy())
+    kb = np.ascontiguousarray(np.concatenate([K[i, :kl[i]] for i in range(m)]))
+    sb = np.ascontiguousarray(np.concatenate([S[i, :sl[i]] for i in range(m)]))
+    ko = np.zeros(m + 1, np.uint64)
+    so = np.zeros(m + 1, np.uint64)
+    ko[1:] = np.cumsum(kl)
+    so[1:] = np.cumsum(sl)
+    mo = np.arange(m + 1, dtype=np.uint64) * M.shape[1]
+    out = np.zeros(m, np.uint8)
+    orc.oracle_ecdsa_verify_batch(m, sc.ctypes.data, kb.ctypes.data, ko.ctypes.data, sb.ctypes.data, so.ctypes.data,
+                                  M.ctypes.data, mo.ctypes.data, out.ctypes.data, _cores())
+    got = status[idx].cpu().numpy()
+    return {"lanes": m, "mismatches": int((out != got).sum()), "oracle_accepted": int((out == 0).sum())}
 
 
 # ---- C2: Ed25519 ---------------------------------------------------------------
 class C2:
     # one step = the split verification pass: prep (decode A/R, SHA-512, lattice
-    # reduction -> per-lane workspace) + ladder, one launch pair per 2^20 lanes
+    # reduction -> per-lane workspace) + ladder, one launch pair for the whole
+    # 2^24-lane batch (the workspace holds 2^24 lanes, cordahip.cpp kEdWsLanes)
     kernel = "ed25519_prep_half_kernel + ed25519_ladder_half_kernel"
     pmc = "r02_pmc_ed25519_split.json"
 
@@ -81,11 +166,17 @@ class C2:
                                        stream=self.stream)
 
     def check(self):
-        # vs the corpus construction (slide-dependent lanes excluded; full bit-exact
-        # parity vs the oracle is tests/test_gpu_ed25519.py's job and the sample below)
+        # every lane is checked: lanes whose status the corpus construction fixes
+        # against it, the construction-open ones (S + kL, slide()-dependent) against
+        # the C oracle, so the whole 2^24-lane status vector is bit-exact attested
         known = self.expected >= 0
+        open_ = (self.expected < 0).nonzero().flatten()
+        orc = _ed_oracle_check(self.status, self.pubs, self.sigs, self.msgs, open_)
         return {"mismatches_vs_construction": int((self.status[known].to(self.torch.int16)
                                                    != self.expected[known]).sum()),
+                "construction_lanes": int(known.sum()),
+                "mismatches_vs_oracle_open_lanes": orc["mismatches"], "open_lanes_oracle_checked": orc["lanes"],
+                "lanes_checked": int(known.sum()) + orc["lanes"], "lanes": self.n,
                 "accepted": int((self.status == 0).sum()), "corrupted": int((self.expected != 0).sum())}
 
     def cpu_baseline(self, sample):
@@ -213,12 +304,17 @@ class C3:
                                      self.status, self.verdict, device=0, stream=self.stream)
 
     def check(self):
-        from corda_amd.corpus import REJECT_ANY
+        # exact-status lanes vs the construction; REJECT_ANY lanes (bit flips whose
+        # status -- BAD_SIG or MALFORMED_SIG -- the flip decides) vs the C oracle
         st = self.status.to(self.torch.int16)
         exact = self.expected >= 0
-        anyrej = self.expected == REJECT_ANY
-        return {"mismatches_vs_construction": int((st[exact] != self.expected[exact]).sum())
-                + int((st[anyrej] == 0).sum()),
+        open_ = (self.expected < 0).nonzero().flatten()
+        orc = _ec_oracle_check(self.status, self.scheme, self.keys, self.key_len, self.sigs, self.sig_len, self.msgs,
+                               open_)
+        return {"mismatches_vs_construction": int((st[exact] != self.expected[exact]).sum()),
+                "construction_lanes": int(exact.sum()),
+                "mismatches_vs_oracle_open_lanes": orc["mismatches"], "open_lanes_oracle_checked": orc["lanes"],
+                "lanes_checked": int(exact.sum()) + orc["lanes"], "lanes": self.n,
                 "accepted": int((self.status == 0).sum()), "corrupted": int((self.expected != 0).sum()),
                 "compressed_valid": int(self.cats["compressed_valid"].numel())}
 
@@ -404,14 +500,20 @@ class C5:
             self.eng.stream_verify(self.ed, self.ec)
 
     def check(self):
-        from corda_amd.corpus import REJECT_ANY
         t = self.torch
         st_ed = self.ed[3].to(t.int16)
         st_ec = self.ec[6].to(t.int16)
         k = self.exp_ed >= 0
         ex = self.exp_ec >= 0
+        o_ed = _ed_oracle_check(self.ed[3], self.ed[0], self.ed[1], self.ed[2], (self.exp_ed < 0).nonzero().flatten())
+        o_ec = _ec_oracle_check(self.ec[6], *self.ec[:6], (self.exp_ec < 0).nonzero().flatten())
         return {"mismatches_vs_construction": int((st_ed[k] != self.exp_ed[k]).sum())
-                + int((st_ec[ex] != self.exp_ec[ex]).sum()) + int((st_ec[self.exp_ec == REJECT_ANY] == 0).sum()),
+                + int((st_ec[ex] != self.exp_ec[ex]).sum()),
+                "construction_lanes": int(k.sum()) + int(ex.sum()),
+                "mismatches_vs_oracle_open_lanes": o_ed["mismatches"] + o_ec["mismatches"],
+                "open_lanes_oracle_checked": o_ed["lanes"] + o_ec["lanes"],
+                "lanes_checked": int(k.sum()) + int(ex.sum()) + o_ed["lanes"] + o_ec["lanes"],
+                "lanes": self.n_ed + self.n_ec,
                 "accepted": int((st_ed == 0).sum()) + int((st_ec == 0).sum())}
 
     def cpu_baseline(self, sample):
@@ -521,7 +623,9 @@ def main():
         kernel_ms = elapsed * 1e3 / args.steps  # synchronous host-buffer drain: the wall clock is the measure
     chk = wl.check()
     elapsed = max_over_ranks(elapsed, device)
-    chk["mismatches_vs_construction"] = int(max_over_ranks(float(chk["mismatches_vs_construction"]), device))
+    for key in ("mismatches_vs_construction", "mismatches_vs_oracle_open_lanes"):
+        if key in chk:
+            chk[key] = int(max_over_ranks(float(chk[key]), device))
 
     if rank == 0:
         value = world * wl.units * args.steps / elapsed
@@ -562,6 +666,7 @@ def main():
             # bounded samples sized for ~10 s of 16-thread CPU work each (C1: its whole 2^20 set)
             sample = args.cpu_sample or {"c1": 1 << 20, "c2": 1 << 22, "c3": 1 << 20, "c4": 1 << 20, "c5": 1 << 21}[args.workload]
             out["cpu_baseline"] = wl.cpu_baseline(min(sample, wl.units))
+            out["cpu_baseline"].update(_cpu_info())
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

@@ -104,3 +104,40 @@ def test_device_path_and_signer(engine, oracle):
     torch.cuda.synchronize()
     assert int(status.sum()) == 0
     assert bool((verdict == -1).all())
+
+
+def test_reference_made_keys(engine, oracle):
+    """The two Ed25519 keys the reference itself serialised (samples/irs-demo/
+    .../trade.json:3,25, tests/golden/kryo_key_vectors.json): A5 decode succeeds
+    on the GPU, so every arbitrary signature is BAD_SIG (not BAD_KEY), as in the
+    oracle, through the generic batch, the dense host path and the device path."""
+    import json
+    import os
+    import torch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    vs = json.load(open(os.path.join(root, "tests", "golden", "kryo_key_vectors.json")))["vectors"]
+    rows = [(bytes.fromhex(v["A"]), bytes.fromhex(s["sig"]), bytes.fromhex(s["msg"]), s["status"])
+            for v in vs for s in v["signatures"]]
+    # each key also with 60 more arbitrary signatures
+    for v in vs:
+        for j in range(60):
+            sig = hashlib.sha512(b"more%d" % j + bytes.fromhex(v["A"])).digest()
+            msg = hashlib.sha256(b"msg%d" % j).digest()
+            rows.append((bytes.fromhex(v["A"]), sig, msg, None))
+    n = len(rows)
+    keys = np.frombuffer(b"".join(r[0] for r in rows), np.uint8).copy()
+    sigs = np.frombuffer(b"".join(r[1] for r in rows), np.uint8).copy()
+    msgs = np.frombuffer(b"".join(r[2] for r in rows), np.uint8).copy()
+    want = _oracle_status(oracle, keys, sigs, msgs, n)
+    assert (want == 1).all()
+    assert [int(w) for w, r in zip(want, rows) if r[3] is not None] == [r[3] for r in rows if r[3] is not None]
+    st, _ = engine.verify_batch([ED] * n, [r[0] for r in rows], [r[1] for r in rows], [r[2] for r in rows])
+    assert np.array_equal(st, want)
+    st2, _ = engine.ed25519_verify_host(keys, sigs, msgs)
+    assert np.array_equal(st2, want)
+    dev = torch.device("cuda:0")
+    tk, ts, tm = (torch.from_numpy(x.reshape(n, -1)).to(dev) for x in (keys, sigs, msgs))
+    st3 = torch.empty(n, dtype=torch.uint8, device=dev)
+    engine.ed25519_verify_device(tk, ts, tm, st3, None, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(st3.cpu().numpy(), want)

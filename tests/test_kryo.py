@@ -92,3 +92,48 @@ def test_bad_items_are_rejected():
         _lib.kryo_encode([("ed25519_key", b"short", 3)])
     with pytest.raises(_lib.EngineError):
         _lib.kryo_encode([("public_key", b"", 3)])
+
+
+def _key_vectors():
+    with open(os.path.join(ROOT, "tests", "golden", "kryo_key_vectors.json")) as f:
+        return json.load(f)["vectors"]
+
+
+def test_reference_ed25519_key_serialisations_pin_the_key_leaf():
+    """The two Base58 party keys of samples/irs-demo/.../trade.json:3,25 are the
+    reference's own p2p Kryo bytes of an EdDSAPublicKey (PublicKey.toBase58String,
+    EncodingUtils.kt:67; tests/golden/make_kryo_key_vectors.py). With references
+    on they read header || varint(45+2) || 01 || varint(32) || A; the Merkle
+    leaf of the same key is hashed withoutReferences (Kryo.kt:550), i.e. without
+    the 01 marker, which is what CORDAHIP_KRYO_ED25519_KEY with class id 45 writes."""
+    vs = _key_vectors()
+    assert len(vs) == 2
+    alphabet = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"  # Base58.java:31
+    for v in vs:
+        raw = bytes.fromhex(v["serialized"])
+        # the fixture's bytes are the Base58 string's: re-encode them
+        x, s = int.from_bytes(raw, "big"), ""
+        while x:
+            x, r = divmod(x, 58)
+            s = alphabet[r] + s
+        assert s == v["base58"]
+        A = bytes.fromhex(v["A"])
+        assert raw == K.HEADER + bytes([v["class_id"] + 2, 0x01, 32]) + A
+        leaf = _lib.kryo_encode([("ed25519_key", A, v["class_id"])])[0]
+        assert leaf.hex() == v["leaf_without_references"]
+        assert leaf == K.leaf("ed25519_key", A, v["class_id"])
+        assert leaf == raw[:9] + raw[10:]  # the same bytes minus the reference marker
+
+
+def test_reference_ed25519_keys_decode_in_both_oracles(oracle):
+    """A5 on two reference-made keys: they decode under the i2p 0.2.0 rules (so
+    arbitrary signatures are BAD_SIG, not BAD_KEY) in the C and Python oracles."""
+    import i2p_ed25519 as E
+    for v in _key_vectors():
+        A = bytes.fromhex(v["A"])
+        assert E.decode_i2p(A) is not None and E.encode(E.decode_i2p(A)) == A
+        for s in v["signatures"]:
+            sig, msg = bytes.fromhex(s["sig"]), bytes.fromhex(s["msg"])
+            assert s["status"] == 1
+            assert oracle.oracle_ed25519_verify(A, 32, sig, 64, msg, 32) == s["status"]
+            assert E.verify_status(A, sig, msg) == s["status"]
