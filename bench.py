@@ -29,6 +29,8 @@ import subprocess
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -376,7 +378,7 @@ class C4:
         self.tx_status = torch.empty(ntx, dtype=torch.uint8, device=device)
         self.first_bad = torch.empty(ntx, dtype=torch.int64, device=device)
         self.sig_status = torch.empty(ns, dtype=torch.uint8, device=device)
-        self.step()  # computes the ids (signatures still blank)
+        C4.step(self)  # computes the ids (signatures still blank)
         torch.cuda.synchronize(device)
         tx_of_sig = torch.repeat_interleave(torch.arange(ntx, device=device), nsig)
         seeds = torch.randint(0, 256, (ns, 32), dtype=torch.uint8, device=device, generator=g)
@@ -547,7 +549,178 @@ class C5:
                 "wall_s": t_ed + t_ec, "gpu_vs_port_mismatches_on_sample": mism}
 
 
-WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c4": C4, "c5": C5}
+# ---- the JVM's boundary: generic CSR batches in host memory ------------------
+def _pinned(a):
+    """numpy array -> page-locked CPU tensor (the JVM's direct ByteBuffers from
+    cordahip_alloc_pinned are the same hipHostMalloc memory)."""
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
+
+
+def _csr_rows(rows, lens):
+    """[n, W] slots + per-lane lengths -> (blob, off[n+1]) with the bytes in lane order."""
+    lens = lens.astype(np.int64)
+    mask = np.arange(rows.shape[1])[None, :] < lens[:, None]
+    off = np.zeros(rows.shape[0] + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    return rows[mask], off
+
+
+class _HostSigBatch:
+    """A cordahip_sig_batch over pinned host CSR arrays (scheme, key/sig/msg blobs + offsets)."""
+
+    def __init__(self, scheme, kb, ko, sb, so, mb, mo):
+        from corda_amd import _lib
+        n = len(scheme)
+        self.t = [_pinned(x) for x in (scheme, kb, ko, sb, so, mb, mo)]
+        self.status = _pinned(np.zeros(n, np.uint8))
+        self.verdict = _pinned(np.zeros((n + 63) // 64, np.uint64))
+        p = [x.data_ptr() for x in self.t]
+        self.b = _lib.SigBatch(n, *p, self.status.data_ptr(), self.verdict.data_ptr(), 0)
+
+    def run(self, eng):
+        import ctypes
+        from corda_amd._lib import check, lib
+        check(lib().cordahip_sig_verify(eng.ctx, ctypes.byref(self.b)), "cordahip_sig_verify")
+
+
+class C2H(C2):
+    """C2's corpus through the boundary the JVM calls: `Crypto.isValid` batches
+    (Crypto.kt:534-541, doVerify semantics) as ONE cordahip_sig_verify over a
+    2^24-lane CSR batch in pinned host memory. Timed region =
+    the whole call: lane classification, host packing into pinned staging, PCIe
+    both ways, the kernels, status scatter and verdict words."""
+    kernel = "cordahip_sig_verify (host CSR batch): pack + H2D + ed25519 prep/ladder + D2H, pipelined"
+    host_timed = True
+
+    def __init__(self, eng, device, stream, rank, args):
+        super().__init__(eng, device, stream, rank, args)
+        n = self.n
+        k, s, m = (x.cpu().numpy() for x in (self.pubs, self.sigs, self.msgs))
+        ar = np.arange(n + 1, dtype=np.uint64)
+        self.hb = _HostSigBatch(np.full(n, 4, np.uint8), k.reshape(-1), ar * 32, s.reshape(-1), ar * 64,
+                                m.reshape(-1), ar * 32)
+        self.workload = ("C2 via the JVM boundary: cordahip_sig_verify over a 2^%d-lane Ed25519 CSR batch in pinned "
+                         "host memory (PCIe and host packing included), 1%% corrupted" % args.batch_log2)
+        self.config = dict(self.config, boundary="cordahip_sig_verify", host_memory="pinned CSR")
+
+    def step(self):
+        self.hb.run(self.eng)
+
+    def check(self):
+        import torch
+        st = self.hb.status
+        self.status = st
+        exp = self.expected.cpu()
+        known = exp >= 0
+        open_ = (exp < 0).nonzero().flatten()
+        orc = _ed_oracle_check(st, self.pubs.cpu(), self.sigs.cpu(), self.msgs.cpu(), open_)
+        ok = (st == 0)
+        words = np.zeros((self.n + 63) // 64, np.uint64)
+        bits = ok.numpy().reshape(-1, 64).astype(np.uint64) << np.arange(64, dtype=np.uint64)
+        words[:] = bits.sum(axis=1, dtype=np.uint64)
+        return {"mismatches_vs_construction": int((st[known].to(torch.int16) != exp[known]).sum()),
+                "construction_lanes": int(known.sum()),
+                "mismatches_vs_oracle_open_lanes": orc["mismatches"], "open_lanes_oracle_checked": orc["lanes"],
+                "lanes_checked": int(known.sum()) + orc["lanes"], "lanes": self.n,
+                "verdict_word_mismatches": int((words != self.hb.verdict.numpy()).sum()),
+                "accepted": int(ok.sum()), "corrupted": int((exp != 0).sum())}
+
+    def cpu_baseline(self, sample):
+        self.status = self.hb.status
+        return C2.cpu_baseline(self, sample)
+
+
+class C3H(C3):
+    """C3's corpus (mixed secp256k1 / P-256, DER signatures of 8-73 bytes, 33- or
+    65-byte keys) through cordahip_sig_verify as a pinned host CSR batch."""
+    kernel = "cordahip_sig_verify (host CSR batch): pack + H2D + ecdsa partition/prep/inv/ladders + D2H, pipelined"
+    host_timed = True
+
+    def __init__(self, eng, device, stream, rank, args):
+        super().__init__(eng, device, stream, rank, args)
+        n = self.n
+        kb, ko = _csr_rows(self.keys.cpu().numpy(), self.key_len.cpu().numpy())
+        sb, so = _csr_rows(self.sigs.cpu().numpy(), self.sig_len.cpu().numpy())
+        ar = np.arange(n + 1, dtype=np.uint64)
+        self.hb = _HostSigBatch(self.scheme.cpu().numpy(), kb, ko, sb, so, self.msgs.cpu().numpy().reshape(-1), ar * 32)
+        self.workload = ("C3 via the JVM boundary: cordahip_sig_verify over a 2^%d-lane mixed secp256k1 / P-256 CSR "
+                         "batch in pinned host memory (PCIe and host packing included), 1%% corrupted" % args.batch_log2)
+        self.config = dict(self.config, boundary="cordahip_sig_verify", host_memory="pinned CSR")
+
+    def step(self):
+        self.hb.run(self.eng)
+
+    def check(self):
+        self.status = self.hb.status
+        dev = (self.scheme, self.keys, self.key_len, self.sigs, self.sig_len, self.msgs, self.expected)
+        self.scheme, self.keys, self.key_len, self.sigs, self.sig_len, self.msgs, self.expected = (x.cpu() for x in dev)
+        try:
+            return C3.check(self)
+        finally:
+            self.scheme, self.keys, self.key_len, self.sigs, self.sig_len, self.msgs, self.expected = dev
+
+    def cpu_baseline(self, sample):
+        self.status = self.hb.status
+        return C3.cpu_baseline(self, sample)
+
+
+class C4H(C4):
+    """C4's transactions through the boundary SignedTransaction.checkSignaturesAreValid
+    maps to (SignedTransaction.kt:95-100): cordahip_tx_submit +
+    cordahip_wait over pinned host CSR arrays (leaf bytes, per-tx leaves and
+    signatures, CSR keys/sigs with scheme bytes). Timed: tx ids (leaf SHA-256 +
+    Merkle) then every signature over its tx's id, PCIe both ways included."""
+    kernel = "cordahip_tx_submit (host CSR): tx ids (sha256_leaves + merkle_root) then cordahip_sig_verify lanes"
+    host_timed = True
+
+    def __init__(self, eng, device, stream, rank, args):
+        from corda_amd import _lib
+        super().__init__(eng, device, stream, rank, args)
+        ntx, ns = self.ntx, self.ns
+        ar = np.arange(ns + 1, dtype=np.uint64)
+        self.t = [_pinned(x) for x in (
+            self.leaf_bytes.cpu().numpy(), self.leaf_off.cpu().numpy().astype(np.uint64),
+            self.tx_leaf_off.cpu().numpy().astype(np.uint64), self.tx_sig_off.cpu().numpy().astype(np.uint64),
+            np.full(ns, 4, np.uint8), self.keys.cpu().numpy().reshape(-1), ar * 32,
+            self.sigs.cpu().numpy().reshape(-1), ar * 64)]
+        self.h_txid = _pinned(np.zeros((ntx, 32), np.uint8))
+        self.h_txst = _pinned(np.zeros(ntx, np.uint8))
+        self.h_sst = _pinned(np.zeros(ns, np.uint8))
+        self.h_fb = _pinned(np.zeros(ntx, np.int64))
+        p = [x.data_ptr() for x in self.t]
+        tb = _lib.TxidBatch(ntx, p[0], p[1], p[2], self.h_txid.data_ptr(), self.h_txst.data_ptr())
+        self.b = _lib.SignedTxBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], self.h_sst.data_ptr(),
+                                    self.h_fb.data_ptr())
+        self.workload = ("C4 via the JVM boundary: cordahip_tx_submit over %d synthetic cash-issue txs per GPU in pinned "
+                         "host CSR memory (5 leaves of %s B, 1-3 Ed25519 signers; PCIe included)"
+                         % (ntx, list(C4_LEAF_LENS)))
+        self.config = dict(self.config, boundary="cordahip_tx_submit + cordahip_wait", host_memory="pinned CSR")
+
+    def step(self):
+        import ctypes
+        from corda_amd._lib import check, lib
+        t = ctypes.c_uint64()
+        check(lib().cordahip_tx_submit(self.eng.ctx, ctypes.byref(self.b), ctypes.byref(t)), "cordahip_tx_submit")
+        check(lib().cordahip_wait(self.eng.ctx, t.value, -1), "cordahip_wait")
+
+    def check(self):
+        import torch
+        exp_st = self.exp_status.cpu()
+        exp_bad = self.exp_bad.cpu()
+        C4.step(self)  # the device-resident path over the same bytes: its ids
+        self.torch.cuda.synchronize(self.device)
+        txid = self.txid.cpu()
+        return {"mismatches_vs_construction": int((self.h_txst != exp_st).sum()) + int((self.h_fb != exp_bad).sum()),
+                "txid_mismatches_vs_device_path": int((self.h_txid != txid).any(dim=1).sum()),
+                "accepted_txs": int((self.h_txst == 0).sum()), "txs": self.ntx, "sigs": self.ns}
+
+    def cpu_baseline(self, sample):
+        self.sig_status = self.h_sst
+        return C4.cpu_baseline(self, sample)
+
+
+WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c4": C4, "c5": C5, "c2h": C2H, "c3h": C3H, "c4h": C4H}
 
 
 def main():
@@ -664,7 +837,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             # bounded samples sized for ~10 s of 16-thread CPU work each (C1: its whole 2^20 set)
-            sample = args.cpu_sample or {"c1": 1 << 20, "c2": 1 << 22, "c3": 1 << 20, "c4": 1 << 20, "c5": 1 << 21}[args.workload]
+            sample = args.cpu_sample or {"c1": 1 << 20, "c2": 1 << 22, "c3": 1 << 20, "c4": 1 << 20, "c5": 1 << 21,
+                                         "c2h": 1 << 22, "c3h": 1 << 20, "c4h": 1 << 20}[args.workload]
             out["cpu_baseline"] = wl.cpu_baseline(min(sample, wl.units))
             out["cpu_baseline"].update(_cpu_info())
         print(json.dumps(out), flush=True)

@@ -10,167 +10,174 @@
 // stream waits on the last user's completion). Tickets run on a per-context
 // worker pool. The fixed-base tables are built once per device at init by a
 // kernel. There is no CPU verification fallback: a HIP failure is returned to
-// the caller as CORDAHIP_ERR_HIP.
+// the caller as CORDAHIP_ERR_HIP. The generic CSR signature batch lives in
+// host_batch.cpp; the shared runtime types in runtime.hpp.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
-#include <atomic>
 #include <chrono>
-#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
-#include <deque>
-#include <functional>
-#include <future>
-#include <map>
-#include <memory>
-#include <mutex>
-#include <thread>
-#include <unordered_map>
-#include <vector>
 
-#include "../../include/cordahip.h"
 #include "der.hpp"
+#include "runtime.hpp"
 #include "status.hpp"
 
-namespace cordahip {
-hipError_t launch_ed25519_btable(uint32_t* tab, hipStream_t s);
-size_t ed25519_btable_bytes();
-hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
-                                 uint64_t n, const uint32_t* btab, const uint8_t* pre_status, uint8_t* status,
-                                 unsigned long long* verdict, uint32_t* ws, uint64_t ws_lanes, uint32_t flags,
-                                 hipStream_t s);
-size_t ed25519_ws_lane_bytes();
-hipError_t launch_ed25519_sign(const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len, uint64_t n,
-                               const uint32_t* btab, uint8_t* pubs, uint8_t* sigs, hipStream_t s);
-hipError_t launch_sha256_leaves(const uint8_t* bytes, const uint64_t* off, uint64_t nleaves, uint32_t* hashes,
-                                hipStream_t s);
-hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uint64_t ntx, uint8_t* txid,
-                              uint8_t* tx_status, hipStream_t s);
-hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
-                              hipStream_t s);
-hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
-                            uint8_t* tx_status, hipStream_t s);
-hipError_t launch_pmt_verify(const uint32_t* leaf_hashes, const uint64_t* tx_leaf_off, const uint8_t* tok,
-                             const uint8_t* tok_hash, const uint64_t* tx_tok_off, const uint8_t* root, uint64_t ntx,
-                             uint32_t* stack, uint8_t* tx_status, hipStream_t s);
-size_t ecdsa_gtable_bytes();
-hipError_t launch_ecdsa_gtables(uint32_t* k1, uint32_t* r1, hipStream_t s);
-hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
-                               const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs,
-                               const uint64_t* msg_off, uint32_t msg_len, uint64_t n, const uint32_t* gk1,
-                               const uint32_t* gr1, const uint8_t* pre_status, uint8_t* status,
-                               unsigned long long* verdict, unsigned int* counters6, unsigned int* perm,
-                               uint32_t* ws, uint64_t ws_slots, uint32_t flags, hipStream_t s);
-size_t ecdsa_ws_slot_bytes();
-hipError_t launch_ecdsa_sign(const uint8_t* scheme, const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len,
-                             uint64_t n, const uint32_t* gk1, const uint32_t* gr1, uint8_t* keys, uint8_t* key_len,
-                             uint8_t* sigs, uint8_t* sig_len, hipStream_t s);
-}  // namespace cordahip
-
 using namespace cordahip;
+using namespace cordahip::rt;
 
-namespace {
+namespace cordahip {
+namespace rt {
 
-constexpr uint64_t kChunk = 1ull << 20;  // lanes per pipelined chunk (128 MiB of Ed25519 input)
+// ---- host fork-join pool -----------------------------------------------------
+HostPool::HostPool(int nthreads) {
+  for (int i = 1; i < nthreads; i++) threads_.emplace_back([this] { worker(); });
+}
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    hipError_t e = hipMalloc(&p, bytes);
-    if (e == hipSuccess) cap = bytes;
+HostPool::~HostPool() {
+  {
+    std::lock_guard<std::mutex> g(m_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();
+}
+
+void HostPool::run_pieces(Job& j) {
+  for (;;) {
+    const uint64_t k = j.next.fetch_add(1);
+    if (k >= j.npieces) return;
+    const uint64_t lo = k * j.piece, hi = std::min(j.n, lo + j.piece);
+    (*j.fn)(lo, hi);
+    if (j.done.fetch_add(1) + 1 == j.npieces) {
+      std::lock_guard<std::mutex> g(j.m);
+      j.cv.notify_all();
+    }
+  }
+}
+
+void HostPool::worker() {
+  for (;;) {
+    std::shared_ptr<Job> j;
+    {
+      std::unique_lock<std::mutex> g(m_);
+      for (;;) {
+        while (!q_.empty() && q_.front()->next.load() >= q_.front()->npieces) q_.pop_front();  // exhausted
+        if (!q_.empty()) {
+          j = q_.front();
+          break;
+        }
+        if (stop_) return;
+        cv_.wait(g);
+      }
+    }
+    run_pieces(*j);
+  }
+}
+
+void HostPool::parallel_for(uint64_t n, uint64_t grain, const std::function<void(uint64_t, uint64_t)>& fn) {
+  if (n == 0) return;
+  grain = std::max<uint64_t>(grain, 1);
+  const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>((n + grain - 1) / grain, 4 * (uint64_t)threads()));
+  if (want == 1 || threads_.empty()) {
+    fn(0, n);
+    return;
+  }
+  auto j = std::make_shared<Job>();
+  j->fn = &fn;
+  j->n = n;
+  j->piece = (n + want - 1) / want;
+  j->npieces = (n + j->piece - 1) / j->piece;
+  {
+    std::lock_guard<std::mutex> g(m_);
+    q_.push_back(j);
+  }
+  cv_.notify_all();
+  run_pieces(*j);
+  {
+    std::unique_lock<std::mutex> g(j->m);
+    j->cv.wait(g, [&] { return j->done.load() == j->npieces; });
+  }
+  std::lock_guard<std::mutex> g(m_);  // drop it if no worker got to pop it
+  for (auto it = q_.begin(); it != q_.end(); ++it)
+    if (*it == j) {
+      q_.erase(it);
+      break;
+    }
+}
+
+// ---- ticket pool ---------------------------------------------------------------
+WorkerPool::WorkerPool(int nthreads) {
+  for (int i = 0; i < nthreads; i++) threads_.emplace_back([this] { run(); });
+}
+
+WorkerPool::~WorkerPool() {
+  {
+    std::lock_guard<std::mutex> g(m_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();
+}
+
+void WorkerPool::push(std::shared_ptr<JobState> st, std::function<int()> fn) {
+  {
+    std::lock_guard<std::mutex> g(m_);
+    q_.emplace_back(std::move(st), std::move(fn));
+  }
+  cv_.notify_one();
+}
+
+void WorkerPool::run() {
+  for (;;) {
+    std::pair<std::shared_ptr<JobState>, std::function<int()>> job;
+    {
+      std::unique_lock<std::mutex> g(m_);
+      cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;  // stop_ and drained: queued jobs always run
+      job = std::move(q_.front());
+      q_.pop_front();
+    }
+    int rc;
+    try {
+      rc = job.second();
+    } catch (...) {
+      rc = CORDAHIP_ERR_OUT_OF_MEMORY;  // std::bad_alloc from host staging vectors
+    }
+    {
+      std::lock_guard<std::mutex> g(job.first->m);
+      job.first->rc = rc;
+      job.first->done = true;
+    }
+    job.first->cv.notify_all();
+  }
+}
+
+int hip_err(hipError_t e) { return e == hipSuccess ? CORDAHIP_SUCCESS : CORDAHIP_ERR_HIP; }
+
+hipError_t ensure_streams(Device& d) {
+  std::lock_guard<std::mutex> g(d.streams_mu);
+  if (d.s_copy) return hipSuccess;
+  // the ECDSA stream at the higher priority: HIP gives it a hardware queue of
+  // its own (at normal priority it shared one with s_ed, and the two sections'
+  // kernels ran one after the other)
+  int lo = 0, hi = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  hipStream_t c = nullptr, x = nullptr, y = nullptr;
+  e = e ? e : hipStreamCreateWithFlags(&c, hipStreamNonBlocking);
+  e = e ? e : hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
+  e = e ? e : hipStreamCreateWithPriority(&y, hipStreamNonBlocking, hi);
+  if (e != hipSuccess) {
+    for (hipStream_t s : {c, x, y})
+      if (s) (void)hipStreamDestroy(s);
     return e;
   }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-  template <class T>
-  T* as() const { return static_cast<T*>(p); }
-};
-
-struct Stage {  // one pipeline slot: device buffers + its stream
-  hipStream_t stream = nullptr;
-  DevBuf keys, sigs, msgs, pre, status, verdict;
-};
-
-// one stage (buffer set) of the C5 streaming pipeline (cordahip_stream_verify);
-// its events order the reuse of the buffers, so the host never waits per chunk
-struct StreamStage {
-  hipEvent_t ed_copied = nullptr, ec_copied = nullptr;  // this chunk's H2D of each section done
-  hipEvent_t ed_done = nullptr, ec_done = nullptr;      // its kernels and status D2H done: buffers free
-  DevBuf ed_keys, ed_sigs, ed_msgs, ed_status;
-  DevBuf ec_scheme, ec_keys, ec_key_len, ec_sigs, ec_sig_len, ec_msgs, ec_status;
-};
-constexpr int kStreamStages = 3;
-// lanes per chunk, both sections together (C5 A/B on one box, profiles/r02_c5_stream_ab.json:
-// 2^21 76.7, 2^22 82.4, 2^23 84.9, 2^24 84.6 M verifs/s with the single-stream stages)
-constexpr uint64_t kStreamChunk = 1ull << 23;
-
-struct TxWork {  // device buffers of the transaction paths (grow-only)
-  DevBuf leaf_bytes, leaf_off, tx_leaf_off, hashes, txid, tx_status, tx_sig_off, msgs;
-  DevBuf tok, tok_hash, tx_tok_off, root, stack;  // filtered-tx (partial Merkle tree) path
-};
-
-struct EcWork {  // device buffers of the ECDSA paths (grow-only)
-  DevBuf scheme, keys, key_len, sigs, sig_len, msgs, msg_off, pre, status, counters, perm;
-  DevBuf ws;                 // split-kernel workspace (kEcWsSlots records)
-  hipEvent_t ev = nullptr;   // last enqueued user of counters/perm/ws (cross-stream reuse)
-};
-
-// Per-call timing of the *_device entry points: a ring of event pairs per
-// device, one pair per call, so concurrent callers never share events.
-constexpr int kTimingRing = 64;
-struct TimedCall {
-  hipEvent_t a = nullptr, b = nullptr;
-};
-
-std::atomic<uint64_t> g_device_uid{1};
-
-struct Device {
-  int id = 0;
-  uint64_t uid = 0;  // process-unique: keys the per-thread timing slot
-  uint32_t* btab = nullptr;
-  uint32_t* gtab_k1 = nullptr;  // [k]G tables, k = 0..128, secp256k1 / P-256
-  uint32_t* gtab_r1 = nullptr;
-  std::mutex ec_mu;
-  EcWork ec;
-  hipStream_t stream = nullptr;  // context stream (init-time work and host tx paths)
-  std::mutex tmu;
-  TimedCall ring[kTimingRing];
-  uint32_t ring_next = 0;
-  std::mutex mu;  // serialises host-path use of the stages
-  Stage stage[2];
-  // tx buffers: tx_mu orders the enqueues of every user (host tx paths, the
-  // device signed-tx path), tx_ev marks the last enqueued user's completion;
-  // each user's stream waits on it before touching the buffers.
-  std::mutex tx_mu;
-  TxWork tx;
-  hipEvent_t tx_ev = nullptr;
-  // Ed25519 split-kernel workspace, shared by every stream that verifies on
-  // this device: ed_mu orders the enqueues, ed_ev makes each user's stream
-  // wait for the previous user's kernels before it reuses the buffer.
-  std::mutex ed_mu;
-  DevBuf ed_ws;
-  hipEvent_t ed_ev = nullptr;
-  std::mutex stream_mu;  // serialises use of sstage and the drain streams
-  StreamStage sstage[kStreamStages];
-  // the drain's three streams, created together: every H2D on s_copy (PCIe in
-  // chunk order), each section's kernels + status D2H on its own stream. Three
-  // active streams, not one per stage and section: HIP maps streams onto
-  // GPU_MAX_HW_QUEUES (4) hardware queues, and streams sharing a queue
-  // serialise (with 6 stage streams C5 ran 90.6 M/s at 4 queues, 93.4 at 8).
-  hipStream_t s_copy = nullptr, s_ed = nullptr, s_ec = nullptr;
-};
-
-// device uid -> ring slot of this thread's most recent timed call
-thread_local std::unordered_map<uint64_t, int> tl_last_call;
+  d.s_ed = x;
+  d.s_ec = y;
+  d.s_copy = c;
+  return hipSuccess;
+}
 
 // Launch-pair sizes of the split kernels = the largest workspace per device.
 // Bigger launches pay fewer end-of-grid tails (C2, measured: 2^18 91.5, 2^20
@@ -241,8 +248,6 @@ hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs
   return e;
 }
 
-int hip_err(hipError_t e) { return e == hipSuccess ? CORDAHIP_SUCCESS : CORDAHIP_ERR_HIP; }
-
 // the in-process partition rule (cordahip_shard_range)
 void shard_range(uint64_t n, uint64_t nshards, uint64_t shard, uint64_t align, uint64_t& lo, uint64_t& hi) {
   if (nshards == 0 || shard >= nshards) {
@@ -255,100 +260,15 @@ void shard_range(uint64_t n, uint64_t nshards, uint64_t shard, uint64_t align, u
   hi = std::min(n, lo + per);
 }
 
-// Run fn(device, lo, hi) for every non-empty shard of n lanes, one host thread
-// per device; returns the first failure.
-template <class F>
-int for_shards(std::vector<std::unique_ptr<Device>>& devs, uint64_t n, uint64_t align, F fn) {
-  const uint64_t nd = devs.size();
-  std::vector<std::future<int>> fs;
-  for (uint64_t i = 0; i < nd; i++) {
-    uint64_t lo, hi;
-    shard_range(n, nd, i, align, lo, hi);
-    if (lo >= hi) break;
-    Device* d = devs[i].get();
-    if (nd == 1) return fn(*d, lo, hi);
-    fs.push_back(std::async(std::launch::async, [=, &fn] { return fn(*d, lo, hi); }));
-  }
-  int rc = CORDAHIP_SUCCESS;
-  for (auto& f : fs) {
-    const int r = f.get();
-    if (r != CORDAHIP_SUCCESS && rc == CORDAHIP_SUCCESS) rc = r;
-  }
-  return rc;
-}
-
-// ---- ticket pool -------------------------------------------------------------
-struct JobState {
-  std::mutex m;
-  std::condition_variable cv;
-  bool done = false;
-  int rc = CORDAHIP_SUCCESS;
-};
-
-class WorkerPool {
- public:
-  explicit WorkerPool(int nthreads) {
-    for (int i = 0; i < nthreads; i++) threads_.emplace_back([this] { run(); });
-  }
-  ~WorkerPool() {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : threads_) t.join();
-  }
-  void push(std::shared_ptr<JobState> st, std::function<int()> fn) {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      q_.emplace_back(std::move(st), std::move(fn));
-    }
-    cv_.notify_one();
-  }
-
- private:
-  void run() {
-    for (;;) {
-      std::pair<std::shared_ptr<JobState>, std::function<int()>> job;
-      {
-        std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [this] { return stop_ || !q_.empty(); });
-        if (q_.empty()) return;  // stop_ and drained: queued jobs always run
-        job = std::move(q_.front());
-        q_.pop_front();
-      }
-      int rc;
-      try {
-        rc = job.second();
-      } catch (...) {
-        rc = CORDAHIP_ERR_OUT_OF_MEMORY;  // std::bad_alloc from host staging vectors
-      }
-      {
-        std::lock_guard<std::mutex> g(job.first->m);
-        job.first->rc = rc;
-        job.first->done = true;
-      }
-      job.first->cv.notify_all();
-    }
-  }
-  std::mutex m_;
-  std::condition_variable cv_;
-  std::deque<std::pair<std::shared_ptr<JobState>, std::function<int()>>> q_;
-  std::vector<std::thread> threads_;
-  bool stop_ = false;
-};
-
-}  // namespace
-
-struct cordahip_ctx {
-  std::vector<std::unique_ptr<Device>> devs;
-  std::mutex mu;  // guards next_ticket and jobs
-  uint64_t next_ticket = 1;
-  std::unordered_map<uint64_t, std::shared_ptr<JobState>> jobs;
-  std::unique_ptr<WorkerPool> pool;
-};
+}  // namespace rt
+}  // namespace cordahip
 
 namespace {
+
+std::atomic<uint64_t> g_device_uid{1};
+
+// device uid -> (ring slot, generation) of this thread's most recent timed call
+thread_local std::unordered_map<uint64_t, std::pair<int, uint64_t>> tl_last_call;
 
 uint64_t submit_job(cordahip_ctx* ctx, std::function<int()> fn) {
   auto st = std::make_shared<JobState>();
@@ -362,222 +282,18 @@ uint64_t submit_job(cordahip_ctx* ctx, std::function<int()> fn) {
   return t;
 }
 
-// timing slot for one *_device call (records `a` now on stream s)
+// timing slot for one *_device call (records `a` now on stream s); the slot's
+// generation is the call's sequence number, so a reader whose slot was reused
+// by a later call (more than kTimingRing calls in between) can tell
 TimedCall* timed_begin(Device& d, hipStream_t s) {
-  int idx;
-  {
-    std::lock_guard<std::mutex> g(d.tmu);
-    idx = (int)(d.ring_next++ % kTimingRing);
-  }
+  std::lock_guard<std::mutex> g(d.tmu);
+  const uint64_t seq = ++d.ring_next;
+  const int idx = (int)(seq % kTimingRing);
   TimedCall* tc = &d.ring[idx];
+  tc->gen = seq;
   if (hipEventRecord(tc->a, s) != hipSuccess) return nullptr;
-  tl_last_call[d.uid] = idx;
+  tl_last_call[d.uid] = {idx, seq};
   return tc;
-}
-
-// Dense Ed25519 shard on one device: [lo, hi) of the caller's host arrays.
-int verify_shard_host(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
-                      const uint8_t* pre, uint64_t lo, uint64_t hi, uint8_t* status, uint64_t* verdict,
-                      uint32_t flags) {
-  std::lock_guard<std::mutex> g(d.mu);
-  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
-  const uint64_t chunk = kChunk;
-  for (int s = 0; s < 2; s++) {
-    Stage& st = d.stage[s];
-    if (!st.stream && hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess)
-      return CORDAHIP_ERR_HIP;
-    const uint64_t c = std::min<uint64_t>(chunk, hi - lo);
-    if (st.keys.ensure(c * 32) || st.sigs.ensure(c * 64) || st.msgs.ensure(std::max<uint64_t>(c * msg_len, 16)) ||
-        st.pre.ensure(c) || st.status.ensure(c) || st.verdict.ensure(((c + 63) / 64) * 8))
-      return CORDAHIP_ERR_OUT_OF_MEMORY;
-  }
-  int k = 0;
-  for (uint64_t off = lo; off < hi; off += chunk, k ^= 1) {
-    Stage& st = d.stage[k];
-    const uint64_t c = std::min<uint64_t>(chunk, hi - off);
-    hipStream_t s = st.stream;
-    hipError_t e = hipSuccess;
-    e = e ? e : hipMemcpyAsync(st.keys.p, keys + off * 32, c * 32, hipMemcpyHostToDevice, s);
-    e = e ? e : hipMemcpyAsync(st.sigs.p, sigs + off * 64, c * 64, hipMemcpyHostToDevice, s);
-    if (msg_len) e = e ? e : hipMemcpyAsync(st.msgs.p, msgs + off * msg_len, c * msg_len, hipMemcpyHostToDevice, s);
-    if (pre) e = e ? e : hipMemcpyAsync(st.pre.p, pre + off, c, hipMemcpyHostToDevice, s);
-    const bool aligned = (off % 64) == 0;
-    e = e ? e
-          : ed_verify_enqueue(d, st.keys.as<uint8_t>(), st.sigs.as<uint8_t>(), st.msgs.as<uint8_t>(), msg_len, c,
-                              pre ? st.pre.as<uint8_t>() : nullptr, st.status.as<uint8_t>(),
-                              st.verdict.as<unsigned long long>(), flags, s);
-    e = e ? e : hipMemcpyAsync(status + off, st.status.p, c, hipMemcpyDeviceToHost, s);
-    if (verdict && aligned)
-      e = e ? e : hipMemcpyAsync(verdict + off / 64, st.verdict.p, ((c + 63) / 64) * 8, hipMemcpyDeviceToHost, s);
-    if (e != hipSuccess) return CORDAHIP_ERR_HIP;
-    // the other stage may be reused next iteration: make sure it is idle
-    if (hipStreamSynchronize(d.stage[k ^ 1].stream) != hipSuccess) return CORDAHIP_ERR_HIP;
-  }
-  for (int s = 0; s < 2; s++)
-    if (hipStreamSynchronize(d.stage[s].stream) != hipSuccess) return CORDAHIP_ERR_HIP;
-  return CORDAHIP_SUCCESS;
-}
-
-void verdict_from_status(const uint8_t* status, uint64_t n, uint64_t* verdict) {
-  for (uint64_t w = 0; w < (n + 63) / 64; w++) {
-    uint64_t m = 0;
-    for (uint64_t b = 0; b < 64 && w * 64 + b < n; b++)
-      if (status[w * 64 + b] == CORDAHIP_STATUS_OK) m |= 1ull << b;
-    verdict[w] = m;
-  }
-}
-
-int ed25519_dense_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
-                       uint32_t msg_len, const uint8_t* pre, uint64_t n, uint8_t* status, uint64_t* verdict,
-                       uint32_t flags) {
-  if (n == 0) return CORDAHIP_SUCCESS;
-  // contiguous 64-aligned shards: no cross-device dependency
-  const int rc = for_shards(ctx->devs, n, 64, [&](Device& d, uint64_t lo, uint64_t hi) {
-    return verify_shard_host(d, keys, sigs, msgs, msg_len, pre, lo, hi, status, verdict, flags);
-  });
-  // chunk boundaries are 64-aligned except possibly a shard tail; recompute
-  // the verdict words from status so every word is exact
-  if (rc == CORDAHIP_SUCCESS && verdict) verdict_from_status(status, n, verdict);
-  return rc;
-}
-
-// One device's shard [lo, hi) of packed ECDSA slot-layout lanes (host arrays).
-int ecdsa_shard_host(Device& d, const uint8_t* sch, const uint8_t* keys, const uint8_t* klen, const uint8_t* sigs,
-                     const uint8_t* slen, const uint8_t* msgs, const uint64_t* moff, const uint8_t* pre, uint64_t lo,
-                     uint64_t hi, uint8_t* st, uint32_t flags) {
-  const uint64_t m = hi - lo;
-  std::vector<uint64_t> off(m + 1);  // message offsets rebased to the shard
-  for (uint64_t j = 0; j <= m; j++) off[j] = moff[lo + j] - moff[lo];
-  const uint64_t mbytes = off[m];
-  std::lock_guard<std::mutex> g(d.ec_mu);
-  if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
-  EcWork& w = d.ec;
-  hipStream_t s = d.stream;
-  if (w.ev && hipEventSynchronize(w.ev) != hipSuccess) return CORDAHIP_ERR_HIP;  // staging buffers below are shared
-  if (w.scheme.ensure(m) || w.keys.ensure(m * 65) || w.key_len.ensure(m) || w.sigs.ensure(m * 72) ||
-      w.sig_len.ensure(m) || w.msgs.ensure(std::max<uint64_t>(mbytes, 16)) || w.msg_off.ensure((m + 1) * 8) ||
-      w.pre.ensure(m) || w.status.ensure(m))
-    return CORDAHIP_ERR_OUT_OF_MEMORY;
-  const hipMemcpyKind h2d = hipMemcpyHostToDevice;
-  hipError_t e = hipMemcpyAsync(w.scheme.p, sch + lo, m, h2d, s);
-  e = e ? e : hipMemcpyAsync(w.keys.p, keys + lo * 65, m * 65, h2d, s);
-  e = e ? e : hipMemcpyAsync(w.key_len.p, klen + lo, m, h2d, s);
-  e = e ? e : hipMemcpyAsync(w.sigs.p, sigs + lo * 72, m * 72, h2d, s);
-  e = e ? e : hipMemcpyAsync(w.sig_len.p, slen + lo, m, h2d, s);
-  if (mbytes) e = e ? e : hipMemcpyAsync(w.msgs.p, msgs + moff[lo], mbytes, h2d, s);
-  e = e ? e : hipMemcpyAsync(w.msg_off.p, off.data(), (m + 1) * 8, h2d, s);
-  e = e ? e : hipMemcpyAsync(w.pre.p, pre + lo, m, h2d, s);
-  e = e ? e
-        : ec_verify_enqueue(d, w.scheme.as<uint8_t>(), w.keys.as<uint8_t>(), w.key_len.as<uint8_t>(),
-                            w.sigs.as<uint8_t>(), w.sig_len.as<uint8_t>(), w.msgs.as<uint8_t>(), w.msg_off.as<uint64_t>(),
-                            0, m, w.pre.as<uint8_t>(), w.status.as<uint8_t>(), nullptr, flags, s);
-  e = e ? e : hipMemcpyAsync(st + lo, w.status.p, m, hipMemcpyDeviceToHost, s);
-  e = e ? e : hipStreamSynchronize(s);
-  return hip_err(e);
-}
-
-// ECDSA lanes of a generic batch: pack into the kernel's slot layout (65-byte
-// keys, 72-byte DER slots, CSR messages) and run K2 on contiguous 64-aligned
-// shards, one per context device. Signatures longer than 72 bytes cannot hold
-// r, s < n (some INTEGER needs > 33 bytes): the host decides them with the same
-// DER rules (der.hpp); the kernel still decodes the key first so key errors
-// keep precedence.
-int ecdsa_host_lanes(cordahip_ctx* ctx, const cordahip_sig_batch* b, const std::vector<uint64_t>& lanes) {
-  const uint64_t m = lanes.size();
-  const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
-  std::vector<uint8_t> sch(m), keys(m * 65, 0), klen(m), sigs(m * 72, 0), slen(m), pre(m, 0), st(m);
-  std::vector<uint64_t> moff(m + 1, 0);
-  for (uint64_t j = 0; j < m; j++) moff[j + 1] = moff[j] + (b->msg_off[lanes[j] + 1] - b->msg_off[lanes[j]]);
-  std::vector<uint8_t> msgs(std::max<uint64_t>(moff[m], 1));
-  for (uint64_t j = 0; j < m; j++) {
-    const uint64_t i = lanes[j];
-    sch[j] = b->scheme[i];
-    const uint64_t kl = b->key_off[i + 1] - b->key_off[i];
-    std::memcpy(&keys[j * 65], b->key + b->key_off[i], kl);
-    klen[j] = (uint8_t)kl;
-    const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
-    const uint64_t ml = b->msg_off[i + 1] - b->msg_off[i];
-    if (sl <= 72) {
-      std::memcpy(&sigs[j * 72], b->sig + b->sig_off[i], sl);
-      slen[j] = (uint8_t)sl;
-    } else {
-      DerInt r, s;
-      pre[j] = (ml == 0 && do_verify) ? CORDAHIP_STATUS_EMPTY
-               : der_decode_sig(b->sig + b->sig_off[i], (uint32_t)std::min<uint64_t>(sl, 0xffffffffu), r, s)
-                   ? CORDAHIP_STATUS_BAD_SIG
-                   : CORDAHIP_STATUS_MALFORMED_SIG;
-      slen[j] = 72;
-    }
-    std::memcpy(&msgs[moff[j]], b->msg + b->msg_off[i], ml);
-  }
-  const int rc = for_shards(ctx->devs, m, 64, [&](Device& d, uint64_t lo, uint64_t hi) {
-    return ecdsa_shard_host(d, sch.data(), keys.data(), klen.data(), sigs.data(), slen.data(), msgs.data(),
-                            moff.data(), pre.data(), lo, hi, st.data(), b->flags);
-  });
-  if (rc != CORDAHIP_SUCCESS) return rc;
-  for (uint64_t j = 0; j < m; j++) b->status[lanes[j]] = st[j];
-  return CORDAHIP_SUCCESS;
-}
-
-// Generic CSR batch: host-side scheme partition and length checks (the
-// Crypto.doVerify require() checks, or none under CORDAHIP_FLAG_IS_VALID), then
-// one dense device launch set per (scheme, message length) group.
-int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
-  const uint64_t n = b->n;
-  if (n == 0) return CORDAHIP_SUCCESS;
-  if (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off || !b->msg || !b->msg_off || !b->status ||
-      (b->flags & ~CORDAHIP_FLAG_IS_VALID))
-    return CORDAHIP_ERR_INVALID_ARG;
-  const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
-  std::map<uint64_t, std::vector<uint64_t>> ed_groups;  // msg length -> lanes
-  std::vector<uint64_t> ec_lanes;
-  for (uint64_t i = 0; i < n; i++) {
-    const uint8_t sch = b->scheme[i];
-    if (sch == CORDAHIP_SCHEME_ECDSA_SECP256K1_SHA256 || sch == CORDAHIP_SCHEME_ECDSA_SECP256R1_SHA256) {
-      const uint64_t kl = b->key_off[i + 1] - b->key_off[i];
-      if (kl != 33 && kl != 65) {
-        b->status[i] = CORDAHIP_STATUS_BAD_KEY;  // ECCurve.decodePoint: invalid point encoding
-        continue;
-      }
-      ec_lanes.push_back(i);
-      continue;
-    }
-    if (sch != CORDAHIP_SCHEME_EDDSA_ED25519_SHA512) {
-      b->status[i] = CORDAHIP_STATUS_UNSUPPORTED;  // Crypto.kt:474 require(isSupportedSignatureScheme)
-      continue;
-    }
-    if (b->key_off[i + 1] - b->key_off[i] != 32) {
-      b->status[i] = CORDAHIP_STATUS_BAD_KEY;  // EdDSAPublicKeySpec: "public-key length is wrong"
-      continue;
-    }
-    ed_groups[b->msg_off[i + 1] - b->msg_off[i]].push_back(i);
-  }
-  for (auto& kv : ed_groups) {
-    const uint64_t mlen = kv.first;
-    const auto& idx = kv.second;
-    const uint64_t m = idx.size();
-    if (mlen > 0xffffffffull) return CORDAHIP_ERR_INVALID_ARG;
-    std::vector<uint8_t> keys(m * 32), sigs(m * 64, 0), msgs(std::max<uint64_t>(m * mlen, 1)), pre(m, 0), st(m);
-    for (uint64_t j = 0; j < m; j++) {
-      const uint64_t i = idx[j];
-      std::memcpy(&keys[j * 32], b->key + b->key_off[i], 32);
-      const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
-      if (do_verify && (sl == 0 || mlen == 0)) pre[j] = CORDAHIP_STATUS_EMPTY;  // Crypto.kt:475-476
-      else if (sl != 64) pre[j] = CORDAHIP_STATUS_MALFORMED_SIG;                // EdDSAEngine length check
-      else std::memcpy(&sigs[j * 64], b->sig + b->sig_off[i], 64);
-      if (mlen) std::memcpy(&msgs[j * mlen], b->msg + b->msg_off[i], mlen);
-    }
-    const int rc = ed25519_dense_host(ctx, keys.data(), sigs.data(), msgs.data(), (uint32_t)mlen, pre.data(), m,
-                                      st.data(), nullptr, b->flags);
-    if (rc != CORDAHIP_SUCCESS) return rc;
-    for (uint64_t j = 0; j < m; j++) b->status[idx[j]] = st[j];
-  }
-  if (!ec_lanes.empty()) {
-    const int rc = ecdsa_host_lanes(ctx, b, ec_lanes);
-    if (rc != CORDAHIP_SUCCESS) return rc;
-  }
-  if (b->verdict) verdict_from_status(b->status, n, b->verdict);
-  return CORDAHIP_SUCCESS;
 }
 
 // Acquire d.tx for a host tx path (tx_mu held): the last device-path user may
@@ -706,17 +422,7 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
     cc = std::max(cc, cut(nc, k + 1) - cut(nc, k));
   }
   const uint64_t eml = b->ed_msg_len, cml = b->ec_msg_len;
-  if (!d.s_copy) {
-    // the ECDSA stream at the higher priority: HIP gives it a hardware queue
-    // of its own (at normal priority it shared one with s_ed, and the two
-    // sections' kernels ran one after the other)
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-        hipStreamCreateWithFlags(&d.s_copy, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&d.s_ed, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithPriority(&d.s_ec, hipStreamNonBlocking, hi) != hipSuccess)
-      return CORDAHIP_ERR_HIP;
-  }
+  if (ensure_streams(d) != hipSuccess) return CORDAHIP_ERR_HIP;
   for (StreamStage& st : d.sstage) {
     for (hipEvent_t* pe : {&st.ed_copied, &st.ec_copied, &st.ed_done, &st.ec_done})
       if (!*pe && hipEventCreateWithFlags(pe, hipEventDisableTiming) != hipSuccess) return CORDAHIP_ERR_HIP;
@@ -862,10 +568,14 @@ Device* dev_at(cordahip_ctx* ctx, int device) {
 
 void free_device(Device& d) {
   (void)hipSetDevice(d.id);
-  for (auto& st : d.stage) {
-    for (DevBuf* b : {&st.keys, &st.sigs, &st.msgs, &st.pre, &st.status, &st.verdict}) b->release();
-    if (st.stream) (void)hipStreamDestroy(st.stream);
-  }
+  for (PackStage* set : {d.ped, d.pec})
+    for (int k = 0; k < kPackStages; k++) {
+      PackStage& st = set[k];
+      for (auto& b : st.h) b.release();
+      for (auto& b : st.d) b.release();
+      for (hipEvent_t ev : {st.copied, st.done})
+        if (ev) (void)hipEventDestroy(ev);
+    }
   for (auto& st : d.sstage) {
     for (DevBuf* b : {&st.ed_keys, &st.ed_sigs, &st.ed_msgs, &st.ed_status, &st.ec_scheme, &st.ec_keys,
                       &st.ec_key_len, &st.ec_sigs, &st.ec_sig_len, &st.ec_msgs, &st.ec_status})
@@ -879,9 +589,7 @@ void free_device(Device& d) {
                     &d.tx.tx_sig_off, &d.tx.msgs, &d.tx.tok, &d.tx.tok_hash, &d.tx.tx_tok_off, &d.tx.root,
                     &d.tx.stack})
     b->release();
-  for (DevBuf* b : {&d.ec.scheme, &d.ec.keys, &d.ec.key_len, &d.ec.sigs, &d.ec.sig_len, &d.ec.msgs, &d.ec.msg_off,
-                    &d.ec.pre, &d.ec.status, &d.ec.counters, &d.ec.perm, &d.ec.ws})
-    b->release();
+  for (DevBuf* b : {&d.ec.counters, &d.ec.perm, &d.ec.ws}) b->release();
   d.ed_ws.release();
   for (hipEvent_t ev : {d.ec.ev, d.ed_ev, d.tx_ev})
     if (ev) (void)hipEventDestroy(ev);
@@ -928,8 +636,18 @@ int cordahip_init(uint32_t device_mask, cordahip_ctx** out) {
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return CORDAHIP_ERR_NO_DEVICE;
   auto ctx = std::make_unique<cordahip_ctx>();
   int rc = CORDAHIP_SUCCESS;
-  for (int d = 0; d < count && d < 32 && rc == CORDAHIP_SUCCESS; d++) {
-    if (device_mask && !((device_mask >> d) & 1u)) continue;
+  // Test-only: CORDAHIP_TEST_DEVICE_REPLICAS=k gives the context k Device
+  // objects per selected HIP device (each with its own streams, buffers and
+  // tables), so the N-device code -- shard split, per-device workers, tails,
+  // verdict reassembly -- runs on a one-GPU box. Unset in production.
+  int replicas = 1;
+  if (const char* v = getenv("CORDAHIP_TEST_DEVICE_REPLICAS")) replicas = std::max(1, std::min(8, atoi(v)));
+  std::vector<int> ids;
+  for (int d = 0; d < count && d < 32; d++)
+    if (!device_mask || ((device_mask >> d) & 1u))
+      for (int r = 0; r < replicas; r++) ids.push_back(d);
+  for (int d : ids) {
+    if (rc != CORDAHIP_SUCCESS) break;
     ctx->devs.push_back(std::make_unique<Device>());
     Device& dev = *ctx->devs.back();
     dev.id = d;
@@ -959,6 +677,16 @@ int cordahip_init(uint32_t device_mask, cordahip_ctx** out) {
     return rc;
   }
   ctx->pool = std::make_unique<WorkerPool>((int)std::max<size_t>(2, 2 * ctx->devs.size()));
+  // host packing threads: CORDAHIP_HOST_THREADS, else the CPUs this process may
+  // use, at most 16 per device (the pipelines are PCIe/kernel bound beyond that)
+  int ht = 0;
+  if (const char* v = getenv("CORDAHIP_HOST_THREADS")) ht = atoi(v);
+  if (ht <= 0) {
+    cpu_set_t cs;
+    const int ncpu = sched_getaffinity(0, sizeof(cs), &cs) == 0 ? CPU_COUNT(&cs) : (int)std::thread::hardware_concurrency();
+    ht = std::max(1, std::min(ncpu, 16 * (int)ctx->devs.size()));
+  }
+  ctx->host = std::make_unique<HostPool>(std::min(ht, 256));
   *out = ctx.release();
   return CORDAHIP_SUCCESS;
 }
@@ -966,6 +694,7 @@ int cordahip_init(uint32_t device_mask, cordahip_ctx** out) {
 void cordahip_shutdown(cordahip_ctx* ctx) {
   if (!ctx) return;
   ctx->pool.reset();  // runs every queued job to completion, joins the workers
+  ctx->host.reset();
   {
     std::lock_guard<std::mutex> g(ctx->mu);
     ctx->jobs.clear();
@@ -1099,7 +828,11 @@ double cordahip_last_kernel_ms(cordahip_ctx* ctx, int device) {
   if (!d) return -1.0;
   auto it = tl_last_call.find(d->uid);
   if (it == tl_last_call.end()) return -1.0;
-  const TimedCall& tc = d->ring[it->second];
+  const TimedCall& tc = d->ring[it->second.first];
+  {
+    std::lock_guard<std::mutex> g(d->tmu);
+    if (tc.gen != it->second.second) return -1.0;  // the slot was reused: > kTimingRing calls since
+  }
   if (hipEventSynchronize(tc.b) != hipSuccess) return -1.0;
   float ms = -1.f;
   if (hipEventElapsedTime(&ms, tc.a, tc.b) != hipSuccess) return -1.0;
@@ -1109,7 +842,7 @@ double cordahip_last_kernel_ms(cordahip_ctx* ctx, int device) {
 int cordahip_ed25519_verify_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                                  uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict) {
   if (!ctx || (n && (!keys || !sigs || !status || (msg_len && !msgs)))) return CORDAHIP_ERR_INVALID_ARG;
-  return ed25519_dense_host(ctx, keys, sigs, msgs, msg_len, nullptr, n, status, verdict, 0u);
+  return ed25519_dense_host(ctx, keys, sigs, msgs, msg_len, n, status, verdict);
 }
 
 int cordahip_filtered_tx_verify(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch) {

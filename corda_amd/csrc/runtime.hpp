@@ -1,0 +1,293 @@
+// libcordahip's internal runtime types (not ABI): per-device state, buffers,
+// the ticket pool, the host thread pool and the enqueue helpers shared by
+// cordahip.cpp (C-ABI, tx / stream / device paths) and host_batch.cpp (the
+// generic CSR signature batch).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <future>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/cordahip.h"
+
+namespace cordahip {
+hipError_t launch_ed25519_btable(uint32_t* tab, hipStream_t s);
+size_t ed25519_btable_bytes();
+hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
+                                 uint64_t n, const uint32_t* btab, const uint8_t* pre_status, uint8_t* status,
+                                 unsigned long long* verdict, uint32_t* ws, uint64_t ws_lanes, uint32_t flags,
+                                 hipStream_t s);
+size_t ed25519_ws_lane_bytes();
+hipError_t launch_ed25519_sign(const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len, uint64_t n,
+                               const uint32_t* btab, uint8_t* pubs, uint8_t* sigs, hipStream_t s);
+hipError_t launch_sha256_leaves(const uint8_t* bytes, const uint64_t* off, uint64_t nleaves, uint32_t* hashes,
+                                hipStream_t s);
+hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uint64_t ntx, uint8_t* txid,
+                              uint8_t* tx_status, hipStream_t s);
+hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
+                              hipStream_t s);
+hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
+                            uint8_t* tx_status, hipStream_t s);
+hipError_t launch_pmt_verify(const uint32_t* leaf_hashes, const uint64_t* tx_leaf_off, const uint8_t* tok,
+                             const uint8_t* tok_hash, const uint64_t* tx_tok_off, const uint8_t* root, uint64_t ntx,
+                             uint32_t* stack, uint8_t* tx_status, hipStream_t s);
+size_t ecdsa_gtable_bytes();
+hipError_t launch_ecdsa_gtables(uint32_t* k1, uint32_t* r1, hipStream_t s);
+hipError_t launch_ecdsa_verify(const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
+                               const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs,
+                               const uint64_t* msg_off, uint32_t msg_len, uint64_t n, const uint32_t* gk1,
+                               const uint32_t* gr1, const uint8_t* pre_status, uint8_t* status,
+                               unsigned long long* verdict, unsigned int* counters6, unsigned int* perm,
+                               uint32_t* ws, uint64_t ws_slots, uint32_t flags, hipStream_t s);
+size_t ecdsa_ws_slot_bytes();
+hipError_t launch_ecdsa_sign(const uint8_t* scheme, const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len,
+                             uint64_t n, const uint32_t* gk1, const uint32_t* gr1, uint8_t* keys, uint8_t* key_len,
+                             uint8_t* sigs, uint8_t* sig_len, hipStream_t s);
+
+namespace rt {
+
+// grow-only device buffer
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// grow-only page-locked host buffer (staging for the packed host pipelines)
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// one stage (buffer set) of the C5 streaming pipeline (cordahip_stream_verify);
+// its events order the reuse of the buffers, so the host never waits per chunk
+struct StreamStage {
+  hipEvent_t ed_copied = nullptr, ec_copied = nullptr;  // this chunk's H2D of each section done
+  hipEvent_t ed_done = nullptr, ec_done = nullptr;      // its kernels and status D2H done: buffers free
+  DevBuf ed_keys, ed_sigs, ed_msgs, ed_status;
+  DevBuf ec_scheme, ec_keys, ec_key_len, ec_sigs, ec_sig_len, ec_msgs, ec_status;
+};
+constexpr int kStreamStages = 3;
+// lanes per chunk, both sections together (C5 A/B on one box, profiles/r02_c5_stream_ab.json:
+// 2^21 76.7, 2^22 82.4, 2^23 84.9, 2^24 84.6 M verifs/s with the single-stream stages)
+constexpr uint64_t kStreamChunk = 1ull << 23;
+
+// one stage of a packed host pipeline (host_batch.cpp): the host packs a chunk
+// of lanes into the pinned buffers, they cross PCIe into the device buffers,
+// the kernels run, the statuses come back into h_status; `done` marks the
+// stage reusable (the host scatters its statuses first)
+struct PackStage {
+  hipEvent_t copied = nullptr, done = nullptr;
+  PinBuf h[9];
+  DevBuf d[9];
+  bool pending = false;
+  uint64_t tag0 = 0, tag1 = 0, tag2 = 0;  // which chunk is in flight (pipeline-defined)
+};
+constexpr int kPackStages = 3;
+
+struct TxWork {  // device buffers of the transaction paths (grow-only)
+  DevBuf leaf_bytes, leaf_off, tx_leaf_off, hashes, txid, tx_status, tx_sig_off, msgs;
+  DevBuf tok, tok_hash, tx_tok_off, root, stack;  // filtered-tx (partial Merkle tree) path
+};
+
+struct EcWork {  // device buffers of the ECDSA paths (grow-only)
+  DevBuf counters, perm;
+  DevBuf ws;                 // split-kernel workspace (kEcWsSlots records)
+  hipEvent_t ev = nullptr;   // last enqueued user of counters/perm/ws (cross-stream reuse)
+};
+
+// Per-call timing of the *_device entry points: a ring of event pairs per
+// device, one pair per call, so concurrent callers never share events; a
+// slot's generation tells a reader whether its call's events are still there.
+constexpr int kTimingRing = 64;
+struct TimedCall {
+  hipEvent_t a = nullptr, b = nullptr;
+  uint64_t gen = 0;
+};
+
+struct Device {
+  int id = 0;
+  uint64_t uid = 0;  // process-unique: keys the per-thread timing slot
+  uint32_t* btab = nullptr;
+  uint32_t* gtab_k1 = nullptr;  // [k]G tables, k = 0..128, secp256k1 / P-256
+  uint32_t* gtab_r1 = nullptr;
+  std::mutex ec_mu;
+  EcWork ec;
+  hipStream_t stream = nullptr;  // context stream (init-time work and host tx paths)
+  std::mutex tmu;
+  TimedCall ring[kTimingRing];
+  uint64_t ring_next = 0;
+  // tx buffers: tx_mu orders the enqueues of every user (host tx paths, the
+  // device signed-tx path), tx_ev marks the last enqueued user's completion;
+  // each user's stream waits on it before touching the buffers.
+  std::mutex tx_mu;
+  TxWork tx;
+  hipEvent_t tx_ev = nullptr;
+  // Ed25519 split-kernel workspace, shared by every stream that verifies on
+  // this device: ed_mu orders the enqueues, ed_ev makes each user's stream
+  // wait for the previous user's kernels before it reuses the buffer.
+  std::mutex ed_mu;
+  DevBuf ed_ws;
+  hipEvent_t ed_ev = nullptr;
+  // The pipelines' three streams, created together and shared by the C5 drain
+  // and the packed host pipelines: every H2D on s_copy (PCIe in chunk order),
+  // each section's kernels + status D2H on its own stream. Three active
+  // streams, not one per stage and section: HIP maps streams onto
+  // GPU_MAX_HW_QUEUES (4) hardware queues, and streams sharing a queue
+  // serialise (with 6 stage streams C5 ran 90.6 M/s at 4 queues, 93.4 at 8).
+  std::mutex streams_mu;
+  hipStream_t s_copy = nullptr, s_ed = nullptr, s_ec = nullptr;
+  std::mutex stream_mu;  // serialises use of sstage (C5)
+  StreamStage sstage[kStreamStages];
+  // packed host pipelines: one stage set per section, each behind its mutex
+  std::mutex ped_mu, pec_mu;
+  PackStage ped[kPackStages], pec[kPackStages];
+};
+
+// Fork-join pool for host-side packing and scattering. parallel_for splits
+// [0, n) into pieces of at least `grain` lanes; the caller runs pieces too,
+// so concurrent callers (one pipeline per device and section) all progress.
+class HostPool {
+ public:
+  explicit HostPool(int nthreads);
+  ~HostPool();
+  int threads() const { return (int)threads_.size() + 1; }
+  void parallel_for(uint64_t n, uint64_t grain, const std::function<void(uint64_t, uint64_t)>& fn);
+
+ private:
+  struct Job {
+    const std::function<void(uint64_t, uint64_t)>* fn = nullptr;
+    uint64_t n = 0, piece = 0, npieces = 0;
+    std::atomic<uint64_t> next{0}, done{0};
+    std::mutex m;
+    std::condition_variable cv;
+  };
+  static void run_pieces(Job& j);
+  void worker();
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::shared_ptr<Job>> q_;
+  std::vector<std::thread> threads_;
+  bool stop_ = false;
+};
+
+// ---- ticket pool -------------------------------------------------------------
+struct JobState {
+  std::mutex m;
+  std::condition_variable cv;
+  bool done = false;
+  int rc = CORDAHIP_SUCCESS;
+};
+
+class WorkerPool {
+ public:
+  explicit WorkerPool(int nthreads);
+  ~WorkerPool();
+  void push(std::shared_ptr<JobState> st, std::function<int()> fn);
+
+ private:
+  void run();
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::pair<std::shared_ptr<JobState>, std::function<int()>>> q_;
+  std::vector<std::thread> threads_;
+  bool stop_ = false;
+};
+
+int hip_err(hipError_t e);
+hipError_t ensure_streams(Device& d);
+hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
+                             uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
+                             unsigned long long* verdict, uint32_t flags, hipStream_t s);
+// d.ec_mu must be held
+hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
+                             const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs, const uint64_t* msg_off,
+                             uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
+                             unsigned long long* verdict, uint32_t flags, hipStream_t s);
+void shard_range(uint64_t n, uint64_t nshards, uint64_t shard, uint64_t align, uint64_t& lo, uint64_t& hi);
+uint64_t env_lanes(const char* name, uint64_t dflt);
+
+// Run fn(device, lo, hi) for every non-empty shard of n lanes, one host thread
+// per device; returns the first failure.
+template <class F>
+int for_shards(std::vector<std::unique_ptr<Device>>& devs, uint64_t n, uint64_t align, F fn) {
+  const uint64_t nd = devs.size();
+  std::vector<std::future<int>> fs;
+  for (uint64_t i = 0; i < nd; i++) {
+    uint64_t lo, hi;
+    shard_range(n, nd, i, align, lo, hi);
+    if (lo >= hi) break;
+    Device* d = devs[i].get();
+    if (nd == 1) return fn(*d, lo, hi);
+    fs.push_back(std::async(std::launch::async, [=, &fn] { return fn(*d, lo, hi); }));
+  }
+  int rc = CORDAHIP_SUCCESS;
+  for (auto& f : fs) {
+    const int r = f.get();
+    if (r != CORDAHIP_SUCCESS && rc == CORDAHIP_SUCCESS) rc = r;
+  }
+  return rc;
+}
+
+}  // namespace rt
+}  // namespace cordahip
+
+struct cordahip_ctx {
+  std::vector<std::unique_ptr<cordahip::rt::Device>> devs;
+  std::mutex mu;  // guards next_ticket and jobs
+  uint64_t next_ticket = 1;
+  std::unordered_map<uint64_t, std::shared_ptr<cordahip::rt::JobState>> jobs;
+  std::unique_ptr<cordahip::rt::WorkerPool> pool;
+  std::unique_ptr<cordahip::rt::HostPool> host;  // packing / scattering threads
+};
+
+namespace cordahip {
+namespace rt {
+// generic CSR batches (host_batch.cpp)
+int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b);
+// dense Ed25519 rows in host memory through the packed pipeline (host_batch.cpp)
+int ed25519_dense_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
+                       uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict);
+void verdict_from_status(cordahip_ctx* ctx, const uint8_t* status, uint64_t n, uint64_t* verdict);
+}  // namespace rt
+}  // namespace cordahip

@@ -1,0 +1,12 @@
+# round 3: GPU suite (incl. multi-device replicas), then the boundary workloads c2h/c3h/c4h and c2
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r3b
+mkdir -p $O
+cd $R
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+for wl in ${WLS:-c2h c3h c4h}; do
+  timeout -k 10 400 python -u bench.py --workload $wl ${BARGS} > $O/bench_$wl.json 2> $O/bench_$wl.err || { echo "bench $wl failed"; tail -20 $O/bench_$wl.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/bench_$wl.json'));print('$wl', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],2), 'ms', d['verdict_check'])"
+done
