@@ -305,7 +305,7 @@ int tx_acquire_host(Device& d) {
 }
 
 // Transaction ids for txs [t0, t1) on one device (offsets rebased to the shard).
-int tx_ids_shard(Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1) {
+int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1) {
   std::lock_guard<std::mutex> g(d.tx_mu);
   if (int rc = tx_acquire_host(d)) return rc;
   const uint64_t ntx = t1 - t0;
@@ -313,8 +313,12 @@ int tx_ids_shard(Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t 
   const uint64_t nleaves = l1 - l0;
   const uint64_t b0 = b->leaf_off[l0], b1 = b->leaf_off[l1];
   std::vector<uint64_t> loff(nleaves + 1), toff(ntx + 1);
-  for (uint64_t i = 0; i <= nleaves; i++) loff[i] = b->leaf_off[l0 + i] - b0;
-  for (uint64_t i = 0; i <= ntx; i++) toff[i] = b->tx_leaf_off[t0 + i] - l0;
+  ctx->host->parallel_for(nleaves + 1, 1 << 16, [&](uint64_t x, uint64_t y) {
+    for (uint64_t i = x; i < y; i++) loff[i] = b->leaf_off[l0 + i] - b0;
+  });
+  ctx->host->parallel_for(ntx + 1, 1 << 16, [&](uint64_t x, uint64_t y) {
+    for (uint64_t i = x; i < y; i++) toff[i] = b->tx_leaf_off[t0 + i] - l0;
+  });
   TxWork& w = d.tx;
   if (w.leaf_bytes.ensure(std::max<uint64_t>(b1 - b0, 16)) || w.leaf_off.ensure((nleaves + 1) * 8) ||
       w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
@@ -341,7 +345,8 @@ int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
     return CORDAHIP_ERR_INVALID_ARG;
   if (b->ntx == 0) return CORDAHIP_SUCCESS;
   // contiguous tx shards: a transaction's tree stays on one device
-  return for_shards(ctx->devs, b->ntx, 1, [&](Device& d, uint64_t t0, uint64_t t1) { return tx_ids_shard(d, b, t0, t1); });
+  return for_shards(ctx->devs, b->ntx, 1,
+                    [&](Device& d, uint64_t t0, uint64_t t1) { return tx_ids_shard(ctx, d, b, t0, t1); });
 }
 
 int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
@@ -350,37 +355,41 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   int rc = tx_ids_impl(ctx, &b->tx);
   if (rc != CORDAHIP_SUCCESS) return rc;
   const uint64_t nsig = ntx ? b->tx_sig_off[ntx] : 0;
-  // each signature signs its transaction's id (SignedTransaction.kt:98)
-  std::vector<uint8_t> msgs(std::max<uint64_t>(nsig, 1) * 32);
-  std::vector<uint64_t> moff(nsig + 1);
-  for (uint64_t t = 0; t < ntx; t++)
-    for (uint64_t s = b->tx_sig_off[t]; s < b->tx_sig_off[t + 1]; s++) std::memcpy(&msgs[s * 32], b->tx.txid + t * 32, 32);
-  for (uint64_t s = 0; s <= nsig; s++) moff[s] = s * 32;
   if (nsig) {
+    if (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off) return CORDAHIP_ERR_INVALID_ARG;
+    // each signature signs its transaction's id (SignedTransaction.kt:98): the
+    // pipeline reads it from txid through tx_of, no per-signature copies
+    std::vector<uint64_t> tx_of(nsig);
+    ctx->host->parallel_for(ntx, 4096, [&](uint64_t t0, uint64_t t1) {
+      for (uint64_t t = t0; t < t1; t++)
+        for (uint64_t s = b->tx_sig_off[t]; s < b->tx_sig_off[t + 1]; s++) tx_of[s] = t;
+    });
     // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
-    cordahip_sig_batch sb{nsig, b->scheme, b->key, b->key_off, b->sig, b->sig_off, msgs.data(), moff.data(),
+    cordahip_sig_batch sb{nsig, b->scheme, b->key, b->key_off, b->sig, b->sig_off, b->tx.txid, nullptr,
                           b->sig_status, nullptr, 0u};
-    rc = sig_verify_impl(ctx, &sb);
+    rc = sig_verify_msgs(ctx, &sb, MsgView{b->tx.txid, nullptr, tx_of.data()});
     if (rc != CORDAHIP_SUCCESS) return rc;
   }
-  for (uint64_t t = 0; t < ntx; t++) {
-    const uint64_t lo = b->tx_sig_off[t], hi = b->tx_sig_off[t + 1];
-    b->first_bad_sig[t] = -1;
-    if (lo == hi) {  // require(sigs.isNotEmpty()) in the constructor (SignedTransaction.kt:37-39) precedes tx.id
-      b->tx.tx_status[t] = CORDAHIP_TX_NO_SIGNATURES;
-      continue;
-    }
-    if (b->tx.tx_status[t] != CORDAHIP_STATUS_OK) {  // tx.id threw before any signature was checked
-      for (uint64_t s = lo; s < hi; s++) b->sig_status[s] = b->tx.tx_status[t];
-      continue;
-    }
-    for (uint64_t s = lo; s < hi; s++)
-      if (b->sig_status[s] != CORDAHIP_STATUS_OK) {
-        b->first_bad_sig[t] = (int64_t)(s - lo);
-        b->tx.tx_status[t] = b->sig_status[s];
-        break;
+  ctx->host->parallel_for(ntx, 4096, [&](uint64_t t0, uint64_t t1) {
+    for (uint64_t t = t0; t < t1; t++) {
+      const uint64_t lo = b->tx_sig_off[t], hi = b->tx_sig_off[t + 1];
+      b->first_bad_sig[t] = -1;
+      if (lo == hi) {  // require(sigs.isNotEmpty()) in the constructor (SignedTransaction.kt:37-39) precedes tx.id
+        b->tx.tx_status[t] = CORDAHIP_TX_NO_SIGNATURES;
+        continue;
       }
-  }
+      if (b->tx.tx_status[t] != CORDAHIP_STATUS_OK) {  // tx.id threw before any signature was checked
+        for (uint64_t s = lo; s < hi; s++) b->sig_status[s] = b->tx.tx_status[t];
+        continue;
+      }
+      for (uint64_t s = lo; s < hi; s++)
+        if (b->sig_status[s] != CORDAHIP_STATUS_OK) {
+          b->first_bad_sig[t] = (int64_t)(s - lo);
+          b->tx.tx_status[t] = b->sig_status[s];
+          break;
+        }
+    }
+  });
   return CORDAHIP_SUCCESS;
 }
 
@@ -568,14 +577,18 @@ Device* dev_at(cordahip_ctx* ctx, int device) {
 
 void free_device(Device& d) {
   (void)hipSetDevice(d.id);
-  for (PackStage* set : {d.ped, d.pec})
-    for (int k = 0; k < kPackStages; k++) {
-      PackStage& st = set[k];
-      for (auto& b : st.h) b.release();
-      for (auto& b : st.d) b.release();
-      for (hipEvent_t ev : {st.copied, st.done})
-        if (ev) (void)hipEventDestroy(ev);
-    }
+  for (PackStage& st : d.ped) {
+    for (auto& b : st.h) b.release();
+    for (auto& b : st.d) b.release();
+    for (hipEvent_t ev : {st.copied, st.done})
+      if (ev) (void)hipEventDestroy(ev);
+  }
+  for (BatchStage& st : d.pb) {
+    for (auto& b : st.h) b.release();
+    for (auto& b : st.d) b.release();
+    for (hipEvent_t ev : {st.copied, st.ed_done, st.ec_done})
+      if (ev) (void)hipEventDestroy(ev);
+  }
   for (auto& st : d.sstage) {
     for (DevBuf* b : {&st.ed_keys, &st.ed_sigs, &st.ed_msgs, &st.ed_status, &st.ec_scheme, &st.ec_keys,
                       &st.ec_key_len, &st.ec_sigs, &st.ec_sig_len, &st.ec_msgs, &st.ec_status})

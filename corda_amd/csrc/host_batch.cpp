@@ -4,20 +4,18 @@
 // signature at Crypto.kt:537-540) and dense Ed25519 rows in host memory
 // (cordahip_ed25519_verify_host).
 //
-// Shape, MI355X-first:
-//  1. classify every lane on the host pool (parallel counting sort, no per-lane
-//     map): direct statuses (UNSUPPORTED, key-length BAD_KEY), one lane list per
-//     Ed25519 message length, one ECDSA lane list (both curves: the kernels
-//     partition by curve on the device);
-//  2. shard every list over the context devices (cordahip_shard_range: contiguous,
-//     64-aligned); per device, the Ed25519 and ECDSA sections run at once, each a
-//     pipeline over kPackStages stages: the host pool packs chunk k into a stage's
-//     pinned buffers (dense rows / 65- and 72-byte slots, 16-B aligned) while the
-//     GPU verifies chunks k-1, k-2 and PCIe carries their inputs and statuses;
-//     when a stage comes round again its statuses are scattered back to the
-//     caller's lanes. H2D on the device's copy stream, each section's kernels and
-//     status D2H on its own stream (ECDSA at high priority), as in the C5 drain;
-//  3. verdict words from the statuses.
+// Shape, MI355X-first: the batch is split into contiguous 64-aligned input
+// shards, one per context device (cordahip_shard_range); each device streams
+// its shard in chunks through kPackStages stages. Per chunk the host pool
+// classifies every lane (the checks that precede the engines, written as
+// statuses at once; Ed25519 lanes grouped by message length; ECDSA lanes, both
+// curves: the kernels partition by curve on the device) and packs it straight
+// into its row of the stage's pinned buffers (dense 32/64-byte rows, 65/72-byte
+// ECDSA slots, CSR messages), while the GPU verifies the previous chunks and
+// PCIe carries their inputs and statuses. H2D on the device's copy stream, the
+// Ed25519 launches and the ECDSA launch on their own streams (beside each
+// other, ECDSA at high priority) as in the C5 drain; when a stage comes round
+// again its statuses go back to the caller's lanes. Verdict words last.
 // The caller's buffers may be pageable: every PCIe transfer is from/to pinned
 // staging. Per-lane rules are those of the reference call chain (see
 // include/cordahip.h): key length before scheme engine checks before DER/length
@@ -36,10 +34,9 @@ namespace cordahip {
 namespace rt {
 namespace {
 
-// lanes per chunk: Ed25519 rows 2^22 (launches of 2^22 lose ~1% to grid tails
-// against one 2^24 launch, C2 measured), ECDSA slots 2^21
+// lanes per chunk: 2^22 (launches of 2^22 lose ~1% to grid tails against one
+// 2^24 launch, C2 measured)
 constexpr uint64_t kEdChunk = 1ull << 22;
-constexpr uint64_t kEcChunk = 1ull << 21;
 constexpr uint64_t kGrain = 1ull << 14;  // lanes per packing piece
 
 uint64_t chunk_lanes(const char* env, uint64_t dflt) {
@@ -75,31 +72,23 @@ std::vector<Chunk> make_chunks(const std::vector<Unit>& units, uint64_t chunk) {
 }
 
 // ---- the two sources of Ed25519 rows --------------------------------------------
-struct CsrEdSource {  // lanes of a cordahip_sig_batch
-  const cordahip_sig_batch* b;
-  bool do_verify;
-  void pack(const Unit& u, uint64_t a, uint64_t b0, uint64_t b1, uint8_t* keys, uint8_t* sigs, uint8_t* msgs,
-            uint8_t* pre) const {
-    const uint32_t L = u.mlen;
-    for (uint64_t p = b0; p < b1; p++) {
-      const uint64_t i = u.lanes[p], r = p - a;
-      std::memcpy(keys + r * 32, b->key + b->key_off[i], 32);
-      const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
-      uint8_t st = CORDAHIP_STATUS_OK;
-      if (do_verify && (sl == 0 || L == 0)) st = CORDAHIP_STATUS_EMPTY;  // Crypto.kt:475-476
-      else if (sl != 64) st = CORDAHIP_STATUS_MALFORMED_SIG;           // EdDSAEngine: signature length
-      if (st == CORDAHIP_STATUS_OK) std::memcpy(sigs + r * 64, b->sig + b->sig_off[i], 64);
-      else std::memset(sigs + r * 64, 0, 64);
-      pre[r] = st;
-      if (L == 32) std::memcpy(msgs + r * 32, b->msg + b->msg_off[i], 32);
-      else if (L) std::memcpy(msgs + r * (uint64_t)L, b->msg + b->msg_off[i], L);
-    }
-  }
-  void scatter(const Unit& u, uint64_t a, uint64_t b0, uint64_t b1, const uint8_t* st) const {
-    for (uint64_t p = b0; p < b1; p++) b->status[u.lanes[p]] = st[p - a];
-  }
-};
+// Ed25519 row of lane i of a cordahip_sig_batch (message length L): the
+// Crypto.doVerify require()s and the engine's length check as the pre-status
+inline void pack_ed_row(const cordahip_sig_batch* b, const MsgView& mv, bool do_verify, uint64_t i, uint32_t L,
+                        uint8_t* key, uint8_t* sig, uint8_t* msg, uint8_t* pre) {
+  std::memcpy(key, b->key + b->key_off[i], 32);
+  const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
+  uint8_t st = CORDAHIP_STATUS_OK;
+  if (do_verify && (sl == 0 || L == 0)) st = CORDAHIP_STATUS_EMPTY;  // Crypto.kt:475-476
+  else if (sl != 64) st = CORDAHIP_STATUS_MALFORMED_SIG;           // EdDSAEngine: signature length
+  if (st == CORDAHIP_STATUS_OK) std::memcpy(sig, b->sig + b->sig_off[i], 64);
+  else std::memset(sig, 0, 64);
+  *pre = st;
+  if (L == 32) std::memcpy(msg, mv.ptr(i), 32);
+  else if (L) std::memcpy(msg, mv.ptr(i), L);
+}
 
+// ---- dense Ed25519 rows in host memory -------------------------------------------
 struct DenseEdSource {  // cordahip_ed25519_verify_host rows
   const uint8_t *keys, *sigs, *msgs;
   uint8_t* status;
@@ -187,135 +176,14 @@ int ed_pipeline(cordahip_ctx* ctx, Device& d, const std::vector<Unit>& units, co
   return (e || e1 || e2) ? CORDAHIP_ERR_HIP : CORDAHIP_SUCCESS;
 }
 
-// ECDSA section of one device (lanes of a cordahip_sig_batch): slot layout of
-// the K2 kernels. Stage buffers h/d[0] scheme, [1] keys (65-B slots), [2]
-// key_len, [3] sigs (72-B slots), [4] sig_len, [5] msgs (CSR bytes), [6]
-// msg_off (chunk-relative), [7] pre-status, [8] status.
-int ec_pipeline(cordahip_ctx* ctx, Device& d, const Unit& unit, const cordahip_sig_batch* b) {
-  const std::vector<Unit> units{unit};
-  const std::vector<Chunk> chunks = make_chunks(units, chunk_lanes("CORDAHIP_HOST_EC_CHUNK", kEcChunk));
-  if (chunks.empty()) return CORDAHIP_SUCCESS;
-  const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
-  std::lock_guard<std::mutex> g(d.pec_mu);
-  if (hipSetDevice(d.id) != hipSuccess || ensure_streams(d) != hipSuccess || ensure_events(d.pec) != hipSuccess)
-    return CORDAHIP_ERR_HIP;
-  HostPool& pool = *ctx->host;
-  const uint64_t* lanes = unit.lanes;
-  auto finish = [&](PackStage& st) -> hipError_t {
-    if (!st.pending) return hipSuccess;
-    st.pending = false;
-    hipError_t e = hipEventSynchronize(st.done);
-    if (e != hipSuccess) return e;
-    const uint8_t* sts = st.h[8].as<uint8_t>();
-    const uint64_t a = st.tag1;
-    pool.parallel_for(st.tag2 - a, kGrain * 4, [&](uint64_t x, uint64_t y) {
-      for (uint64_t p = a + x; p < a + y; p++) b->status[lanes[p]] = sts[p - a];
-    });
-    return hipSuccess;
-  };
-  hipError_t e = hipSuccess;
-  int rc = CORDAHIP_SUCCESS;
-  std::vector<uint64_t> piece_bytes;
-  for (size_t k = 0; k < chunks.size() && e == hipSuccess && rc == CORDAHIP_SUCCESS; k++) {
-    PackStage& st = d.pec[k % kPackStages];
-    e = finish(st);
-    if (e != hipSuccess) break;
-    const Chunk& c = chunks[k];
-    const uint64_t m = c.b - c.a;
-    // message bytes per piece (fixed pieces), then their prefix: each piece
-    // packs its messages at its own offset
-    const uint64_t npiece = (m + kGrain - 1) / kGrain;
-    piece_bytes.assign(npiece + 1, 0);
-    pool.parallel_for(npiece, 1, [&](uint64_t x, uint64_t y) {
-      for (uint64_t q = x; q < y; q++) {
-        uint64_t t = 0;
-        for (uint64_t p = c.a + q * kGrain; p < std::min(c.b, c.a + (q + 1) * kGrain); p++)
-          t += b->msg_off[lanes[p] + 1] - b->msg_off[lanes[p]];
-        piece_bytes[q + 1] = t;
-      }
-    });
-    for (uint64_t q = 0; q < npiece; q++) piece_bytes[q + 1] += piece_bytes[q];
-    const uint64_t mbytes = piece_bytes[npiece];
-    const size_t sz[9] = {m, m * 65, m, m * 72, m, std::max<uint64_t>(mbytes, 16), (m + 1) * 8, m, m};
-    for (int q = 0; q < 9; q++)
-      if (st.h[q].ensure(sz[q]) != hipSuccess || st.d[q].ensure(sz[q]) != hipSuccess) rc = CORDAHIP_ERR_OUT_OF_MEMORY;
-    if (rc != CORDAHIP_SUCCESS) break;
-    uint8_t *hsc = st.h[0].as<uint8_t>(), *hk = st.h[1].as<uint8_t>(), *hkl = st.h[2].as<uint8_t>(),
-            *hs = st.h[3].as<uint8_t>(), *hsl = st.h[4].as<uint8_t>(), *hm = st.h[5].as<uint8_t>(),
-            *hp = st.h[7].as<uint8_t>();
-    uint64_t* hmo = st.h[6].as<uint64_t>();
-    pool.parallel_for(npiece, 1, [&](uint64_t x, uint64_t y) {
-      for (uint64_t q = x; q < y; q++) {
-        uint64_t mo = piece_bytes[q];
-        for (uint64_t p = c.a + q * kGrain; p < std::min(c.b, c.a + (q + 1) * kGrain); p++) {
-          const uint64_t i = lanes[p], r = p - c.a;
-          hsc[r] = b->scheme[i];
-          const uint64_t kl = b->key_off[i + 1] - b->key_off[i];  // 33 or 65 (classified)
-          std::memcpy(hk + r * 65, b->key + b->key_off[i], kl);
-          std::memset(hk + r * 65 + kl, 0, 65 - kl);
-          hkl[r] = (uint8_t)kl;
-          const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
-          const uint64_t ml = b->msg_off[i + 1] - b->msg_off[i];
-          uint8_t pre = CORDAHIP_STATUS_OK;
-          if (sl <= 72) {
-            std::memcpy(hs + r * 72, b->sig + b->sig_off[i], sl);
-            std::memset(hs + r * 72 + sl, 0, 72 - sl);
-            hsl[r] = (uint8_t)sl;
-          } else {
-            // longer than the slot: no r, s < n fits, so the DER rules alone
-            // decide (BC: well-formed -> false, else SignatureException); the
-            // kernel still decodes the key first, so key errors keep precedence
-            DerInt dr, ds;
-            pre = (ml == 0 && do_verify) ? CORDAHIP_STATUS_EMPTY
-                  : der_decode_sig(b->sig + b->sig_off[i], (uint32_t)std::min<uint64_t>(sl, 0xffffffffu), dr, ds)
-                      ? CORDAHIP_STATUS_BAD_SIG
-                      : CORDAHIP_STATUS_MALFORMED_SIG;
-            std::memset(hs + r * 72, 0, 72);
-            hsl[r] = 72;
-          }
-          hp[r] = pre;
-          hmo[r] = mo;
-          std::memcpy(hm + mo, b->msg + b->msg_off[i], ml);
-          mo += ml;
-        }
-      }
-    });
-    hmo[m] = mbytes;
-    const size_t bytes[8] = {m, m * 65, m, m * 72, m, mbytes, (m + 1) * 8, m};
-    for (int q = 0; q < 8; q++)
-      if (bytes[q]) e = e ? e : hipMemcpyAsync(st.d[q].p, st.h[q].p, bytes[q], hipMemcpyHostToDevice, d.s_copy);
-    e = e ? e : hipEventRecord(st.copied, d.s_copy);
-    e = e ? e : hipStreamWaitEvent(d.s_ec, st.copied, 0);
-    if (e == hipSuccess) {
-      std::lock_guard<std::mutex> ge(d.ec_mu);
-      e = ec_verify_enqueue(d, st.d[0].as<uint8_t>(), st.d[1].as<uint8_t>(), st.d[2].as<uint8_t>(),
-                            st.d[3].as<uint8_t>(), st.d[4].as<uint8_t>(), st.d[5].as<uint8_t>(),
-                            st.d[6].as<uint64_t>(), 0, m, st.d[7].as<uint8_t>(), st.d[8].as<uint8_t>(), nullptr,
-                            b->flags, d.s_ec);
-    }
-    e = e ? e : hipMemcpyAsync(st.h[8].p, st.d[8].p, m, hipMemcpyDeviceToHost, d.s_ec);
-    e = e ? e : hipEventRecord(st.done, d.s_ec);
-    if (e == hipSuccess) {
-      st.pending = true;
-      st.tag1 = c.a;
-      st.tag2 = c.b;
-    }
-  }
-  for (int k = 0; k < kPackStages; k++) {
-    if (e == hipSuccess && rc == CORDAHIP_SUCCESS) e = finish(d.pec[k]);
-    d.pec[k].pending = false;
-  }
-  const hipError_t e1 = hipStreamSynchronize(d.s_copy), e2 = hipStreamSynchronize(d.s_ec);
-  if (rc != CORDAHIP_SUCCESS) return rc;
-  return (e || e1 || e2) ? CORDAHIP_ERR_HIP : CORDAHIP_SUCCESS;
-}
+// Lane classes of a generic batch: the per-lane checks that precede the
+// engines (statuses decided here are written at once).
+enum : uint16_t { kDirect = 0, kEc = 1, kEdBase = 2 };
 
-// Lane classes of a generic batch.
-enum : uint8_t { kDirect = 0, kEd = 1, kEc = 2 };
-
-inline uint8_t classify(const cordahip_sig_batch* b, uint64_t i, uint64_t& mlen) {
+inline uint16_t classify(const cordahip_sig_batch* b, const MsgView& mv, uint64_t i, uint64_t& mlen) {
   const uint8_t sch = b->scheme[i];
   const uint64_t kl = b->key_off[i + 1] - b->key_off[i];
+  mlen = mv.len(i);
   if (sch == CORDAHIP_SCHEME_ECDSA_SECP256K1_SHA256 || sch == CORDAHIP_SCHEME_ECDSA_SECP256R1_SHA256) {
     if (kl != 33 && kl != 65) {
       b->status[i] = CORDAHIP_STATUS_BAD_KEY;  // ECCurve.decodePoint: invalid point encoding
@@ -331,8 +199,242 @@ inline uint8_t classify(const cordahip_sig_batch* b, uint64_t i, uint64_t& mlen)
     b->status[i] = CORDAHIP_STATUS_BAD_KEY;  // EdDSAPublicKeySpec: "public-key length is wrong"
     return kDirect;
   }
-  mlen = b->msg_off[i + 1] - b->msg_off[i];
-  return kEd;
+  return kEdBase;  // + the piece-local message-length group
+}
+
+// Per-piece results of the classification pass of one chunk.
+struct PieceInfo {
+  std::vector<std::pair<uint64_t, uint64_t>> ed;  // (message length, lanes), piece-local group order
+  std::vector<uint32_t> ed_global;               // piece-local group -> chunk group
+  uint64_t ec = 0, ec_bytes = 0;                 // ECDSA lanes and their message bytes
+  bool too_long = false;
+};
+
+// ECDSA slot packing of lane i into row r (messages CSR at *mo)
+inline void pack_ec_row(const cordahip_sig_batch* b, const MsgView& mv, bool do_verify, uint64_t i, uint64_t r, uint8_t* hsc, uint8_t* hk,
+                        uint8_t* hkl, uint8_t* hs, uint8_t* hsl, uint8_t* hm, uint64_t* hmo, uint8_t* hp,
+                        uint64_t& mo) {
+  hsc[r] = b->scheme[i];
+  const uint64_t kl = b->key_off[i + 1] - b->key_off[i];  // 33 or 65 (classified)
+  std::memcpy(hk + r * 65, b->key + b->key_off[i], kl);
+  std::memset(hk + r * 65 + kl, 0, 65 - kl);
+  hkl[r] = (uint8_t)kl;
+  const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
+  const uint64_t ml = mv.len(i);
+  uint8_t pre = CORDAHIP_STATUS_OK;
+  if (sl <= 72) {
+    std::memcpy(hs + r * 72, b->sig + b->sig_off[i], sl);
+    std::memset(hs + r * 72 + sl, 0, 72 - sl);
+    hsl[r] = (uint8_t)sl;
+  } else {
+    // longer than the slot: no r, s < n fits, so the DER rules alone decide (BC:
+    // well-formed -> false, else SignatureException); the kernel still decodes
+    // the key first, so key errors keep precedence
+    DerInt dr, ds;
+    pre = (ml == 0 && do_verify) ? CORDAHIP_STATUS_EMPTY
+          : der_decode_sig(b->sig + b->sig_off[i], (uint32_t)std::min<uint64_t>(sl, 0xffffffffu), dr, ds)
+              ? CORDAHIP_STATUS_BAD_SIG
+              : CORDAHIP_STATUS_MALFORMED_SIG;
+    std::memset(hs + r * 72, 0, 72);
+    hsl[r] = 72;
+  }
+  hp[r] = pre;
+  hmo[r] = mo;
+  std::memcpy(hm + mo, mv.ptr(i), ml);
+  mo += ml;
+}
+
+// One device's input shard [lo, hi) of a generic batch, streamed in chunks
+// through kPackStages BatchStages. Per chunk, on the host pool: (1) classify
+// every lane (direct statuses written now; Ed25519 lanes grouped by message
+// length; ECDSA lanes) into per-lane class codes and per-piece counts, (2) pack
+// every lane straight into its row: Ed25519 rows group after group (each
+// group's messages at a 16-B aligned offset, one kernel launch per group),
+// ECDSA rows in lane order with CSR messages. Then H2D on the copy stream, the
+// Ed25519 launches on s_ed and the ECDSA launch on s_ec (beside each other),
+// status D2H on each section's stream. Classification and packing of chunk k
+// run while the GPU verifies chunks k-1 and k-2; a stage's statuses go back to
+// the caller's lanes when the stage comes round again.
+int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, const MsgView& mv, uint64_t lo,
+                 uint64_t hi) {
+  if (lo >= hi) return CORDAHIP_SUCCESS;
+  std::vector<Unit> units(1);
+  units[0].lo = lo;
+  units[0].hi = hi;
+  const std::vector<Chunk> chunks = make_chunks(units, chunk_lanes("CORDAHIP_HOST_CHUNK", kEdChunk));
+  const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
+  std::lock_guard<std::mutex> g(d.pb_mu);
+  if (hipSetDevice(d.id) != hipSuccess || ensure_streams(d) != hipSuccess) return CORDAHIP_ERR_HIP;
+  for (BatchStage& st : d.pb)
+    for (hipEvent_t* pe : {&st.copied, &st.ed_done, &st.ec_done})
+      if (!*pe && hipEventCreateWithFlags(pe, hipEventDisableTiming) != hipSuccess) return CORDAHIP_ERR_HIP;
+  HostPool& pool = *ctx->host;
+  auto finish = [&](BatchStage& st) -> hipError_t {  // wait for the stage's chunk, scatter its statuses
+    if (!st.pending) return hipSuccess;
+    st.pending = false;
+    hipError_t e = hipEventSynchronize(st.ed_done);
+    e = e ? e : hipEventSynchronize(st.ec_done);
+    if (e != hipSuccess) return e;
+    const uint8_t *se = st.h[4].as<uint8_t>(), *sc = st.h[13].as<uint8_t>();
+    const uint64_t ne = st.ed_lanes.size(), nc = st.ec_lanes.size();
+    pool.parallel_for(ne + nc, kGrain * 4, [&](uint64_t x, uint64_t y) {
+      for (uint64_t r = x; r < y; r++) {
+        if (r < ne) b->status[st.ed_lanes[r]] = se[r];
+        else b->status[st.ec_lanes[r - ne]] = sc[r - ne];
+      }
+    });
+    return hipSuccess;
+  };
+  std::vector<uint16_t> cls;
+  std::vector<PieceInfo> pieces;
+  std::vector<uint64_t> lens, grow, gmsg, ec_row0, ec_mo0;  // chunk groups: length, first row, message offset
+  std::vector<std::vector<uint64_t>> prow;                   // [piece][group]: the piece's first row in the group
+  hipError_t e = hipSuccess;
+  int rc = CORDAHIP_SUCCESS;
+  for (size_t k = 0; k < chunks.size() && e == hipSuccess && rc == CORDAHIP_SUCCESS; k++) {
+    BatchStage& st = d.pb[k % kPackStages];
+    e = finish(st);
+    if (e != hipSuccess) break;
+    const uint64_t a = chunks[k].a, m = chunks[k].b - a;
+    const uint64_t np = (m + kGrain - 1) / kGrain;
+    cls.resize(m);
+    pieces.resize(np);
+    // (1) classify
+    pool.parallel_for(np, 1, [&](uint64_t x, uint64_t y) {
+      for (uint64_t q = x; q < y; q++) {
+        PieceInfo& P = pieces[q];
+        P.ed.clear();
+        P.ec = P.ec_bytes = 0;
+        P.too_long = false;
+        for (uint64_t r = q * kGrain; r < std::min(m, (q + 1) * kGrain); r++) {
+          uint64_t mlen = 0;
+          uint16_t c = classify(b, mv, a + r, mlen);
+          if (c == kEc) {
+            P.ec++;
+            P.ec_bytes += mlen;
+          } else if (c == kEdBase) {
+            if (mlen > 0xffffffffull) P.too_long = true;
+            size_t j = 0;
+            while (j < P.ed.size() && P.ed[j].first != mlen) j++;
+            if (j == P.ed.size()) P.ed.push_back({mlen, 0});
+            P.ed[j].second++;
+            c = (uint16_t)(kEdBase + j);
+          }
+          cls[r] = c;
+        }
+      }
+    });
+    // (2) chunk layout: groups by length, rows and message offsets per piece
+    lens.clear();
+    for (const PieceInfo& P : pieces) {
+      if (P.too_long) rc = CORDAHIP_ERR_INVALID_ARG;
+      for (const auto& kv : P.ed) lens.push_back(kv.first);
+    }
+    if (rc != CORDAHIP_SUCCESS) break;
+    std::sort(lens.begin(), lens.end());
+    lens.erase(std::unique(lens.begin(), lens.end()), lens.end());
+    const size_t ng = lens.size();
+    prow.assign(np, std::vector<uint64_t>(ng, 0));
+    grow.assign(ng + 1, 0);
+    gmsg.assign(ng + 1, 0);
+    for (uint64_t q = 0; q < np; q++) {
+      PieceInfo& P = pieces[q];
+      P.ed_global.resize(P.ed.size());
+      for (size_t j = 0; j < P.ed.size(); j++)
+        P.ed_global[j] = (uint32_t)(std::lower_bound(lens.begin(), lens.end(), P.ed[j].first) - lens.begin());
+    }
+    for (size_t gi = 0; gi < ng; gi++) {  // rows of group gi, piece by piece
+      uint64_t r = grow[gi];
+      for (uint64_t q = 0; q < np; q++) {
+        prow[q][gi] = r;
+        for (size_t j = 0; j < pieces[q].ed.size(); j++)
+          if (pieces[q].ed_global[j] == gi) r += pieces[q].ed[j].second;
+      }
+      grow[gi + 1] = r;
+      gmsg[gi + 1] = (gmsg[gi] + (r - grow[gi]) * lens[gi] + 15) / 16 * 16;
+    }
+    ec_row0.assign(np + 1, 0);
+    ec_mo0.assign(np + 1, 0);
+    for (uint64_t q = 0; q < np; q++) {
+      ec_row0[q + 1] = ec_row0[q] + pieces[q].ec;
+      ec_mo0[q + 1] = ec_mo0[q] + pieces[q].ec_bytes;
+    }
+    const uint64_t ne = grow[ng], nc = ec_row0[np], mb = ec_mo0[np];
+    const size_t sz[14] = {ne * 32, ne * 64, std::max<uint64_t>(gmsg[ng], 16), ne, ne,
+                           nc, nc * 65, nc, nc * 72, nc, std::max<uint64_t>(mb, 16), (nc + 1) * 8, nc, nc};
+    for (int q = 0; q < 14; q++)
+      if (sz[q] && (st.h[q].ensure(sz[q]) != hipSuccess || st.d[q].ensure(sz[q]) != hipSuccess))
+        rc = CORDAHIP_ERR_OUT_OF_MEMORY;
+    if (rc != CORDAHIP_SUCCESS) break;
+    st.ed_lanes.resize(ne);
+    st.ec_lanes.resize(nc);
+    // (3) pack every lane into its row
+    pool.parallel_for(np, 1, [&](uint64_t x, uint64_t y) {
+      std::vector<uint64_t> row;
+      for (uint64_t q = x; q < y; q++) {
+        const PieceInfo& P = pieces[q];
+        row.assign(P.ed.size(), 0);
+        for (size_t j = 0; j < P.ed.size(); j++) row[j] = prow[q][P.ed_global[j]];
+        uint64_t er = ec_row0[q], mo = ec_mo0[q];
+        for (uint64_t r = q * kGrain; r < std::min(m, (q + 1) * kGrain); r++) {
+          const uint16_t c = cls[r];
+          const uint64_t i = a + r;
+          if (c == kEc) {
+            st.ec_lanes[er] = i;
+            pack_ec_row(b, mv, do_verify, i, er, st.h[5].as<uint8_t>(), st.h[6].as<uint8_t>(), st.h[7].as<uint8_t>(),
+                        st.h[8].as<uint8_t>(), st.h[9].as<uint8_t>(), st.h[10].as<uint8_t>(), st.h[11].as<uint64_t>(),
+                        st.h[12].as<uint8_t>(), mo);
+            er++;
+          } else if (c >= kEdBase) {
+            const size_t j = c - kEdBase, gi = P.ed_global[j];
+            const uint64_t rr = row[j]++;
+            st.ed_lanes[rr] = i;
+            // group gi's messages start at gmsg[gi]
+            pack_ed_row(b, mv, do_verify, i, (uint32_t)lens[gi], st.h[0].as<uint8_t>() + rr * 32,
+                        st.h[1].as<uint8_t>() + rr * 64,
+                        st.h[2].as<uint8_t>() + gmsg[gi] + (rr - grow[gi]) * lens[gi], st.h[3].as<uint8_t>() + rr);
+          }
+        }
+      }
+    });
+    if (nc) st.h[11].as<uint64_t>()[nc] = mb;
+    // (4) copies and launches
+    for (int q = 0; q < 14; q++) {
+      const size_t bytes = q == 2 ? gmsg[ng] : q == 10 ? mb : q == 4 || q == 13 ? 0 : sz[q];
+      if (bytes) e = e ? e : hipMemcpyAsync(st.d[q].p, st.h[q].p, bytes, hipMemcpyHostToDevice, d.s_copy);
+    }
+    e = e ? e : hipEventRecord(st.copied, d.s_copy);
+    e = e ? e : hipStreamWaitEvent(d.s_ed, st.copied, 0);
+    for (size_t gi = 0; gi < ng && e == hipSuccess; gi++) {
+      const uint64_t r0 = grow[gi], cnt = grow[gi + 1] - r0;
+      if (cnt)
+        e = ed_verify_enqueue(d, st.d[0].as<uint8_t>() + r0 * 32, st.d[1].as<uint8_t>() + r0 * 64,
+                              st.d[2].as<uint8_t>() + gmsg[gi], (uint32_t)lens[gi], cnt, st.d[3].as<uint8_t>() + r0,
+                              st.d[4].as<uint8_t>() + r0, nullptr, b->flags, d.s_ed);
+    }
+    if (ne) e = e ? e : hipMemcpyAsync(st.h[4].p, st.d[4].p, ne, hipMemcpyDeviceToHost, d.s_ed);
+    e = e ? e : hipEventRecord(st.ed_done, d.s_ed);
+    e = e ? e : hipStreamWaitEvent(d.s_ec, st.copied, 0);
+    if (nc && e == hipSuccess) {
+      std::lock_guard<std::mutex> ge(d.ec_mu);
+      e = ec_verify_enqueue(d, st.d[5].as<uint8_t>(), st.d[6].as<uint8_t>(), st.d[7].as<uint8_t>(),
+                            st.d[8].as<uint8_t>(), st.d[9].as<uint8_t>(), st.d[10].as<uint8_t>(),
+                            st.d[11].as<uint64_t>(), 0, nc, st.d[12].as<uint8_t>(), st.d[13].as<uint8_t>(), nullptr,
+                            b->flags, d.s_ec);
+    }
+    if (nc) e = e ? e : hipMemcpyAsync(st.h[13].p, st.d[13].p, nc, hipMemcpyDeviceToHost, d.s_ec);
+    e = e ? e : hipEventRecord(st.ec_done, d.s_ec);
+    if (e == hipSuccess) st.pending = true;
+  }
+  // drain every stage even after an error, so no queued work outlives the call
+  for (int k = 0; k < kPackStages; k++) {
+    if (e == hipSuccess && rc == CORDAHIP_SUCCESS) e = finish(d.pb[k]);
+    d.pb[k].pending = false;
+  }
+  const hipError_t e1 = hipStreamSynchronize(d.s_copy), e2 = hipStreamSynchronize(d.s_ed),
+                   e3 = hipStreamSynchronize(d.s_ec);
+  if (rc != CORDAHIP_SUCCESS) return rc;
+  return (e || e1 || e2 || e3) ? CORDAHIP_ERR_HIP : CORDAHIP_SUCCESS;
 }
 
 }  // namespace
@@ -348,113 +450,23 @@ void verdict_from_status(cordahip_ctx* ctx, const uint8_t* status, uint64_t n, u
   });
 }
 
-int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
+int sig_verify_msgs(cordahip_ctx* ctx, const cordahip_sig_batch* b, const MsgView& mv) {
   const uint64_t n = b->n;
   if (n == 0) return CORDAHIP_SUCCESS;
+  // contiguous 64-aligned input shards, one pipeline per device
+  const int rc = for_shards(ctx->devs, n, 64,
+                            [&](Device& d, uint64_t lo, uint64_t hi) { return sig_pipeline(ctx, d, b, mv, lo, hi); });
+  if (rc != CORDAHIP_SUCCESS) return rc;
+  if (b->verdict) verdict_from_status(ctx, b->status, n, b->verdict);
+  return CORDAHIP_SUCCESS;
+}
+
+int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
+  if (b->n == 0) return CORDAHIP_SUCCESS;
   if (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off || !b->msg || !b->msg_off || !b->status ||
       (b->flags & ~CORDAHIP_FLAG_IS_VALID))
     return CORDAHIP_ERR_INVALID_ARG;
-  HostPool& pool = *ctx->host;
-  // 1. classification: fixed pieces, two passes (count, then place) = a stable
-  // counting sort of the lanes into one list per Ed25519 message length + ECDSA
-  const uint64_t piece = std::max<uint64_t>(kGrain, (n + 8 * pool.threads() - 1) / (8 * pool.threads()));
-  const uint64_t npiece = (n + piece - 1) / piece;
-  struct PieceCount {
-    std::vector<std::pair<uint64_t, uint64_t>> ed;  // (message length, lanes)
-    uint64_t ec = 0;
-    bool too_long = false;
-  };
-  std::vector<PieceCount> pc(npiece);
-  pool.parallel_for(npiece, 1, [&](uint64_t x, uint64_t y) {
-    for (uint64_t q = x; q < y; q++) {
-      PieceCount& c = pc[q];
-      for (uint64_t i = q * piece; i < std::min(n, (q + 1) * piece); i++) {
-        uint64_t mlen = 0;
-        const uint8_t cls = classify(b, i, mlen);
-        if (cls == kEc) {
-          c.ec++;
-        } else if (cls == kEd) {
-          if (mlen > 0xffffffffull) c.too_long = true;
-          size_t k = 0;
-          while (k < c.ed.size() && c.ed[k].first != mlen) k++;
-          if (k == c.ed.size()) c.ed.push_back({mlen, 0});
-          c.ed[k].second++;
-        }
-      }
-    }
-  });
-  std::vector<uint64_t> lens;
-  uint64_t n_ec = 0;
-  for (const PieceCount& c : pc) {
-    if (c.too_long) return CORDAHIP_ERR_INVALID_ARG;
-    for (const auto& kv : c.ed) lens.push_back(kv.first);
-    n_ec += c.ec;
-  }
-  std::sort(lens.begin(), lens.end());
-  lens.erase(std::unique(lens.begin(), lens.end()), lens.end());
-  const size_t ng = lens.size();
-  // start[g][q]: where piece q's lanes of group g go; group ng = ECDSA
-  std::vector<std::vector<uint64_t>> start(ng + 1, std::vector<uint64_t>(npiece + 1, 0));
-  for (uint64_t q = 0; q < npiece; q++) {
-    for (size_t g = 0; g < ng; g++) {
-      uint64_t cnt = 0;
-      for (const auto& kv : pc[q].ed)
-        if (kv.first == lens[g]) cnt = kv.second;
-      start[g][q + 1] = start[g][q] + cnt;
-    }
-    start[ng][q + 1] = start[ng][q] + pc[q].ec;
-  }
-  std::vector<std::vector<uint64_t>> lists(ng + 1);
-  for (size_t g = 0; g <= ng; g++) lists[g].resize(start[g][npiece]);
-  pool.parallel_for(npiece, 1, [&](uint64_t x, uint64_t y) {
-    std::vector<uint64_t> pos(ng + 1);
-    for (uint64_t q = x; q < y; q++) {
-      for (size_t g = 0; g <= ng; g++) pos[g] = start[g][q];
-      for (uint64_t i = q * piece; i < std::min(n, (q + 1) * piece); i++) {
-        uint64_t mlen = 0;
-        const uint8_t cls = classify(b, i, mlen);
-        if (cls == kEc) {
-          lists[ng][pos[ng]++] = i;
-        } else if (cls == kEd) {
-          const size_t g = std::lower_bound(lens.begin(), lens.end(), mlen) - lens.begin();
-          lists[g][pos[g]++] = i;
-        }
-      }
-    }
-  });
-  (void)n_ec;
-  // 2. per device: its shard of every list; Ed25519 and ECDSA sections at once
-  const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
-  const CsrEdSource src{b, do_verify};
-  const uint64_t nd = ctx->devs.size();
-  std::vector<std::future<int>> fs;
-  for (uint64_t di = 0; di < nd; di++) {
-    std::vector<Unit> eu;
-    for (size_t g = 0; g < ng; g++) {
-      Unit u;
-      u.lanes = lists[g].data();
-      shard_range(lists[g].size(), nd, di, 64, u.lo, u.hi);
-      u.mlen = (uint32_t)lens[g];
-      if (u.lo < u.hi) eu.push_back(u);
-    }
-    Unit cu;
-    cu.lanes = lists[ng].data();
-    shard_range(lists[ng].size(), nd, di, 64, cu.lo, cu.hi);
-    Device* d = ctx->devs[di].get();
-    if (cu.lo < cu.hi) fs.push_back(std::async(std::launch::async, [=] { return ec_pipeline(ctx, *d, cu, b); }));
-    if (!eu.empty())
-      fs.push_back(std::async(std::launch::async,
-                              [=, &src] { return ed_pipeline(ctx, *d, eu, src, b->flags); }));
-  }
-  int rc = CORDAHIP_SUCCESS;
-  for (auto& f : fs) {
-    const int r = f.get();
-    if (r != CORDAHIP_SUCCESS && rc == CORDAHIP_SUCCESS) rc = r;
-  }
-  if (rc != CORDAHIP_SUCCESS) return rc;
-  // 3. verdict words
-  if (b->verdict) verdict_from_status(ctx, b->status, n, b->verdict);
-  return CORDAHIP_SUCCESS;
+  return sig_verify_msgs(ctx, b, MsgView{b->msg, b->msg_off, nullptr});
 }
 
 int ed25519_dense_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,

@@ -125,6 +125,19 @@ struct PackStage {
 };
 constexpr int kPackStages = 3;
 
+// one stage of the generic-batch pipeline (host_batch.cpp): a chunk of the
+// batch's lanes, classified and packed into BOTH sections' pinned buffers
+// (h/d[0..4] Ed25519 keys, sigs, msgs, pre-status, status; [5..13] ECDSA
+// scheme, keys, key_len, sigs, sig_len, msgs, msg_off, pre-status, status);
+// the lane lists say where each row's status goes back
+struct BatchStage {
+  hipEvent_t copied = nullptr, ed_done = nullptr, ec_done = nullptr;
+  PinBuf h[14];
+  DevBuf d[14];
+  std::vector<uint64_t> ed_lanes, ec_lanes;
+  bool pending = false;
+};
+
 struct TxWork {  // device buffers of the transaction paths (grow-only)
   DevBuf leaf_bytes, leaf_off, tx_leaf_off, hashes, txid, tx_status, tx_sig_off, msgs;
   DevBuf tok, tok_hash, tx_tok_off, root, stack;  // filtered-tx (partial Merkle tree) path
@@ -180,8 +193,9 @@ struct Device {
   std::mutex stream_mu;  // serialises use of sstage (C5)
   StreamStage sstage[kStreamStages];
   // packed host pipelines: one stage set per section, each behind its mutex
-  std::mutex ped_mu, pec_mu;
-  PackStage ped[kPackStages], pec[kPackStages];
+  std::mutex ped_mu, pb_mu;
+  PackStage ped[kPackStages];   // dense Ed25519 rows (cordahip_ed25519_verify_host)
+  BatchStage pb[kPackStages];   // generic CSR batches (cordahip_sig_verify / _submit)
 };
 
 // Fork-join pool for host-side packing and scattering. parallel_for splits
@@ -283,8 +297,20 @@ struct cordahip_ctx {
 
 namespace cordahip {
 namespace rt {
-// generic CSR batches (host_batch.cpp)
+// Where lane i's message is: the batch's CSR (msg + msg_off), or -- for the
+// signatures of a transaction batch, each over its transaction's id
+// (SignedTransaction.kt:98) -- the 32-byte id of transaction tx_of[i].
+struct MsgView {
+  const uint8_t* base;
+  const uint64_t* off;
+  const uint64_t* tx_of;
+  const uint8_t* ptr(uint64_t i) const { return tx_of ? base + 32 * tx_of[i] : base + off[i]; }
+  uint64_t len(uint64_t i) const { return tx_of ? 32 : off[i + 1] - off[i]; }
+};
+// generic CSR batches (host_batch.cpp); sig_verify_msgs takes the messages
+// from mv instead of b->msg / b->msg_off
 int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b);
+int sig_verify_msgs(cordahip_ctx* ctx, const cordahip_sig_batch* b, const MsgView& mv);
 // dense Ed25519 rows in host memory through the packed pipeline (host_batch.cpp)
 int ed25519_dense_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                        uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict);

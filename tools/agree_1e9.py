@@ -30,16 +30,35 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 def ecdsa_csr(sc, K, KL, S, SL, M):
-    kl = KL.astype(np.uint64)
-    sl = SL.astype(np.uint64)
-    kb = np.ascontiguousarray(np.concatenate([K[i, :kl[i]] for i in range(len(sc))])) if len(sc) else np.zeros(1, np.uint8)
-    sb = np.ascontiguousarray(np.concatenate([S[i, :sl[i]] for i in range(len(sc))])) if len(sc) else np.zeros(1, np.uint8)
+    """Slot-layout lanes -> the oracle's CSR (bytes in lane order, vectorised)."""
+    kl = KL.astype(np.int64)
+    sl = SL.astype(np.int64)
+    kb = np.ascontiguousarray(K[np.arange(K.shape[1])[None, :] < kl[:, None]])
+    sb = np.ascontiguousarray(S[np.arange(S.shape[1])[None, :] < sl[:, None]])
+    if kb.size == 0:
+        kb = np.zeros(1, np.uint8)
+    if sb.size == 0:
+        sb = np.zeros(1, np.uint8)
     ko = np.zeros(len(sc) + 1, np.uint64)
     so = np.zeros(len(sc) + 1, np.uint64)
     ko[1:] = np.cumsum(kl)
     so[1:] = np.cumsum(sl)
     mo = np.arange(len(sc) + 1, dtype=np.uint64) * M.shape[1]
     return kb, ko, sb, so, np.ascontiguousarray(M), mo
+
+
+def _log(args, scheme, b, n, checked, mism_c, mism_o, got, want, rejected):
+    """One JSON line per batch: counts plus SHA-256 digests of the GPU's and the
+    oracle's status bytes over the oracle-checked lanes (equal iff they agree)."""
+    import hashlib
+    if not args.log:
+        return
+    rec = {"scheme": scheme, "batch": b, "lanes": n, "oracle_checked": checked, "construction_mismatches": mism_c,
+           "oracle_mismatches": mism_o, "rejected": rejected,
+           "gpu_status_sha256": hashlib.sha256(got.tobytes()).hexdigest(),
+           "oracle_status_sha256": hashlib.sha256(want.tobytes()).hexdigest()}
+    with open(args.log, "a") as f:
+        f.write(json.dumps(rec) + "\n")
 
 
 def main():
@@ -50,6 +69,10 @@ def main():
     ap.add_argument("--sample-log2", type=int, default=15)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--oracle-all", action="store_true",
+                    help="oracle-check EVERY lane of every batch (not only the open lanes and a sample)")
+    ap.add_argument("--first", type=int, default=0, help="index of the first batch (seeds are per batch index)")
+    ap.add_argument("--log", default=None, help="append one JSON line per batch to this file")
     args = ap.parse_args()
 
     import torch
@@ -69,7 +92,7 @@ def main():
     t0 = time.time()
     gpu_s = 0.0
     with Engine(1) as eng:
-        for b in range(args.ed):
+        for b in range(args.first, args.first + args.ed):
             pubs, sigs, msgs, exp, _ = make_c2_corpus(eng, n, 0xA9EE0000 + b, dev, stream=stream)
             st = torch.empty(n, dtype=torch.uint8, device=dev)
             torch.cuda.synchronize(dev)
@@ -80,15 +103,20 @@ def main():
             known = exp >= 0
             mism = int((st[known].to(torch.int16) != exp[known]).sum())
             # oracle: every open lane plus the first `smp` lanes
-            idx = torch.nonzero(~known).flatten()
-            idx = torch.unique(torch.cat([idx, torch.arange(smp, device=dev)]))
+            if args.oracle_all:
+                idx = torch.arange(n, device=dev)
+            else:
+                idx = torch.nonzero(~known).flatten()
+                idx = torch.unique(torch.cat([idx, torch.arange(smp, device=dev)]))
             k = pubs[idx].cpu().numpy().copy()
             s = sigs[idx].cpu().numpy().copy()
             m = msgs[idx].cpu().numpy().copy()
             want = np.zeros(len(idx), np.uint8)
             orc.oracle_ed25519_verify_batch(len(idx), k.ctypes.data, s.ctypes.data, m.ctypes.data, 32,
                                             want.ctypes.data, args.threads)
-            mism_o = int((st[idx].cpu().numpy() != want).sum())
+            got = st[idx].cpu().numpy()
+            mism_o = int((got != want).sum())
+            _log(args, "ed25519", b, n, len(idx), mism, mism_o, got, want, int((st != 0).sum()))
             r = tot["ed25519"]
             r["lanes"] += n
             r["construction_checked"] += int(known.sum())
@@ -98,7 +126,7 @@ def main():
             print("ed25519 batch %d/%d: %d lanes, construction mism %d, oracle-checked %d mism %d (%.0f s)"
                   % (b + 1, args.ed, n, mism, len(idx), mism_o, time.time() - t0), flush=True)
             del pubs, sigs, msgs, exp, st
-        for b in range(args.ec):
+        for b in range(args.first, args.first + args.ec):
             sc, K, KL, S, SL, M, exp, _ = make_c3_corpus(eng, n, 0xA9EC0000 + b, dev, stream=stream)
             st = torch.empty(n, dtype=torch.uint8, device=dev)
             torch.cuda.synchronize(dev)
@@ -109,8 +137,11 @@ def main():
             exact = exp >= 0
             anyrej = exp == REJECT_ANY
             mism = int((st[exact].to(torch.int16) != exp[exact]).sum()) + int((st[anyrej] == 0).sum())
-            idx = torch.nonzero(~exact).flatten()
-            idx = torch.unique(torch.cat([idx, torch.arange(smp, device=dev)]))
+            if args.oracle_all:
+                idx = torch.arange(n, device=dev)
+            else:
+                idx = torch.nonzero(~exact).flatten()
+                idx = torch.unique(torch.cat([idx, torch.arange(smp, device=dev)]))
             csr = ecdsa_csr(sc[idx].cpu().numpy(), K[idx].cpu().numpy(), KL[idx].cpu().numpy(),
                             S[idx].cpu().numpy(), SL[idx].cpu().numpy(), M[idx].cpu().numpy())
             sch = np.ascontiguousarray(sc[idx].cpu().numpy())
@@ -119,7 +150,9 @@ def main():
             orc.oracle_ecdsa_verify_batch(len(idx), sch.ctypes.data, kb.ctypes.data, ko.ctypes.data, sb.ctypes.data,
                                           so.ctypes.data, Mc.ctypes.data, mo.ctypes.data, want.ctypes.data,
                                           args.threads)
-            mism_o = int((st[idx].cpu().numpy() != want).sum())
+            got = st[idx].cpu().numpy()
+            mism_o = int((got != want).sum())
+            _log(args, "ecdsa", b, n, len(idx), mism, mism_o, got, want, int((st != 0).sum()))
             r = tot["ecdsa"]
             r["lanes"] += n
             r["construction_checked"] += int(exact.sum() + anyrej.sum())
