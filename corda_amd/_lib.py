@@ -36,7 +36,8 @@ EXPORTS = [
 ERR_BUFFER_TOO_SMALL = -8
 # cordahip_kryo_item kinds (CORDAHIP_KRYO_*)
 KRYO_KINDS = {"raw": 0, "char": 1, "short": 2, "int": 3, "long": 4, "byte": 5, "boolean": 6, "float": 7,
-              "double": 8, "String": 9, "ed25519_key": 10, "public_key": 11, "kotlin_object": 12}
+              "double": 8, "String": 9, "ed25519_key": 10, "public_key": 11, "kotlin_object": 12, "party": 13,
+              "issue_command": 14}
 ABI_VERSION = 2
 FLAG_IS_VALID = 1  # CORDAHIP_FLAG_IS_VALID: Crypto.isValid semantics (no emptiness checks)
 TX_NO_LEAVES, TX_NO_SIGNATURES, TX_BAD_TREE = 6, 7, 8
@@ -197,6 +198,18 @@ def kryo_encode(items):
         elif kind in ("raw", "ed25519_key", "public_key"):
             b = bytes(value)
             it.len = len(b)
+        elif kind == "party":  # value = (X.500 name DER, key bytes, key class id); class_id = X500Name's id
+            name_der, key, key_class = value
+            b = bytes(name_der) + bytes(key)
+            it.len = len(b)
+            it.value = key_class
+        elif kind == "issue_command":  # value = (class name, nonce, [(key class id, key bytes)]); class_id = Arrays$ArrayList's
+            cls, nonce, keys = value
+            nm = cls.encode("ascii")
+            b = bytes([len(nm)]) + nm + bytes([len(keys)]) + b"".join(
+                int(kc).to_bytes(2, "little") + len(k).to_bytes(2, "little") + bytes(k) for kc, k in keys)
+            it.len = len(b)
+            it.value = nonce
         else:
             b = None
             it.value = ord(value) if (kind == "char" and isinstance(value, str)) else int(value)

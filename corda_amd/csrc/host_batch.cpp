@@ -23,6 +23,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <future>
 
@@ -38,6 +41,16 @@ namespace {
 // 2^24 launch, C2 measured)
 constexpr uint64_t kEdChunk = 1ull << 22;
 constexpr uint64_t kGrain = 1ull << 14;  // lanes per packing piece
+
+// CORDAHIP_TRACE=1: per-chunk host timings of the pipelines on stderr (wait for
+// the stage, classify, pack, enqueue), to see whether the host or the GPU bounds
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+bool tracing() {
+  static const bool on = getenv("CORDAHIP_TRACE") != nullptr;
+  return on;
+}
 
 uint64_t chunk_lanes(const char* env, uint64_t dflt) {
   const uint64_t v = env_lanes(env, 0);
@@ -291,10 +304,13 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
   std::vector<std::vector<uint64_t>> prow;                   // [piece][group]: the piece's first row in the group
   hipError_t e = hipSuccess;
   int rc = CORDAHIP_SUCCESS;
+  const double t_start = tracing() ? now_ms() : 0;
   for (size_t k = 0; k < chunks.size() && e == hipSuccess && rc == CORDAHIP_SUCCESS; k++) {
     BatchStage& st = d.pb[k % kPackStages];
+    const double t0 = tracing() ? now_ms() : 0;
     e = finish(st);
     if (e != hipSuccess) break;
+    const double t1 = tracing() ? now_ms() : 0;
     const uint64_t a = chunks[k].a, m = chunks[k].b - a;
     const uint64_t np = (m + kGrain - 1) / kGrain;
     cls.resize(m);
@@ -324,6 +340,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
         }
       }
     });
+    const double t2 = tracing() ? now_ms() : 0;
     // (2) chunk layout: groups by length, rows and message offsets per piece
     lens.clear();
     for (const PieceInfo& P : pieces) {
@@ -398,6 +415,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
       }
     });
     if (nc) st.h[11].as<uint64_t>()[nc] = mb;
+    const double t3 = tracing() ? now_ms() : 0;
     // (4) copies and launches
     for (int q = 0; q < 14; q++) {
       const size_t bytes = q == 2 ? gmsg[ng] : q == 10 ? mb : q == 4 || q == 13 ? 0 : sz[q];
@@ -425,6 +443,10 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     if (nc) e = e ? e : hipMemcpyAsync(st.h[13].p, st.d[13].p, nc, hipMemcpyDeviceToHost, d.s_ec);
     e = e ? e : hipEventRecord(st.ec_done, d.s_ec);
     if (e == hipSuccess) st.pending = true;
+    if (tracing())
+      fprintf(stderr, "[cordahip] dev %d chunk %zu: %llu lanes (%llu ed, %llu ec) at %.1f ms: wait %.2f classify %.2f "
+                      "pack %.2f enqueue %.2f ms\n", d.id, k, (unsigned long long)m, (unsigned long long)ne,
+              (unsigned long long)nc, t0 - t_start, t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
   }
   // drain every stage even after an error, so no queued work outlives the call
   for (int k = 0; k < kPackStages; k++) {
@@ -433,6 +455,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
   }
   const hipError_t e1 = hipStreamSynchronize(d.s_copy), e2 = hipStreamSynchronize(d.s_ed),
                    e3 = hipStreamSynchronize(d.s_ec);
+  if (tracing()) fprintf(stderr, "[cordahip] dev %d: shard done at %.1f ms\n", d.id, now_ms() - t_start);
   if (rc != CORDAHIP_SUCCESS) return rc;
   return (e || e1 || e2 || e3) ? CORDAHIP_ERR_HIP : CORDAHIP_SUCCESS;
 }

@@ -300,6 +300,27 @@ int cordahip_filtered_tx_submit(cordahip_ctx* ctx, const cordahip_filtered_tx_ba
  *                  KotlinObjectSerializer, CordaClassResolver.kt:76-99), e.g.
  *                  "net.corda.core.contracts.TransactionType$General"; data =
  *                  the class name as UTF-16 code units (len = chars)
+ *   PARTY          the notary Party (identity/Party.kt): NAME registration of
+ *                  "net.corda.core.identity.Party", CompatibleFieldSerializer
+ *                  (EXTENDED names, DefaultKryoCustomizer.kt:56-58) over
+ *                  AbstractParty.owningKey (key class + writeBytesWithLength) and
+ *                  Party.name (X500NameSerializer, Kryo.kt:615-624); data = the
+ *                  X.500 name's DER (self-delimiting) followed by the key bytes
+ *                  (A, or the SPKI DER); class_id = X500Name's registration id;
+ *                  value = the key class's registration id
+ *   ISSUE_COMMAND  Command(value = an issue command data class with one Long
+ *                  `nonce`, signers = Arrays.asList(keys)) as
+ *                  TransactionBuilder.addCommand(data, vararg keys) builds it
+ *                  (TransactionBuilder.kt:124, Structures.kt:285, Cash.kt:148);
+ *                  data = u8 class-name length, the command data's binary class
+ *                  name, u8 key count, per key u16 LE registration id, u16 LE
+ *                  length, key bytes; class_id = java.util.Arrays$ArrayList's
+ *                  registration id (ArraysAsListSerializer); value = the nonce
+ * Field values go through OutputChunked (1024-byte chunks + a zero chunk) as
+ * Kryo 4.0.0's CompatibleFieldSerializer writes them. PARTY / ISSUE_COMMAND are
+ * restated from Kryo 4.0.0 / kryo-serializers 0.41 published sources: PARITY
+ * UNPINNED (no JVM here), except the Ed25519 key bytes inside them, which the
+ * reference's own serialised keys pin (tests/golden/kryo_key_vectors.json).
  * class_id = kryo.getRegistration(cls).id on the node (registration order of
  * DefaultKryoCustomizer.kt is fixed per build; the JVM reads it once).
  * off[0..n] receives the CSR offsets; returns CORDAHIP_ERR_BUFFER_TOO_SMALL with
@@ -318,6 +339,8 @@ int cordahip_filtered_tx_submit(cordahip_ctx* ctx, const cordahip_filtered_tx_ba
 #define CORDAHIP_KRYO_ED25519_KEY 10
 #define CORDAHIP_KRYO_PUBLIC_KEY 11
 #define CORDAHIP_KRYO_KOTLIN_OBJECT 12
+#define CORDAHIP_KRYO_PARTY 13
+#define CORDAHIP_KRYO_ISSUE_COMMAND 14
 typedef struct {
   uint32_t kind;       /* CORDAHIP_KRYO_* */
   uint32_t class_id;   /* Kryo registration id (ED25519_KEY, PUBLIC_KEY) */

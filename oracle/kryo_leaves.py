@@ -17,12 +17,18 @@ not in /root/reference) wire format, restated from its published source:
   default registrations         int 0, String 1, float 2, boolean 3, byte 4, char 5,
                                 short 6, long 7, double 8, void 9
 Corda serializers: Ed25519PublicKeySerializer (Kryo.kt:383-393), PublicKeySerializer
-(:441-451), CordaClassResolver.registerImplicit's KotlinObjectSerializer
-(CordaClassResolver.kt:76-99).
+(:441-451), X500NameSerializer (:615-624), CordaClassResolver.registerImplicit's
+KotlinObjectSerializer and NAME registration (CordaClassResolver.kt:76-99);
+Kryo's CompatibleFieldSerializer (the default serializer, EXTENDED cached field
+names: DefaultKryoCustomizer.kt:56-58) with OutputChunked field framing, and
+kryo-serializers 0.41's ArraysAsListSerializer (DefaultKryoCustomizer.kt:60).
 
 Pinning: the char leaves of PartialMerkleTreeTest.kt:22-25 are the derived fixture
-(tests/golden/merkle_vectors.json "ref_*"); every other kind is PARITY UNPINNED
-(no Kryo, no JVM here: the bytes follow the published format, unconfirmed).
+(tests/golden/merkle_vectors.json "ref_*"); the Ed25519 key leaf (class id 45 +
+writeBytesWithLength) is pinned by the reference's own serialised keys
+(tests/golden/kryo_key_vectors.json, samples/irs-demo/.../trade.json:3,25); every
+other kind -- Party, the issue Command -- is PARITY UNPINNED (no Kryo, no JVM
+here: the bytes follow the published format, unconfirmed).
 """
 import struct
 
@@ -76,6 +82,70 @@ def write_string(s: str) -> bytes:
     return bytes(out)
 
 
+def varlong_zigzag(x: int) -> bytes:
+    """Output.writeVarLong(x, false): zig-zag, 7-bit groups, the 9th byte 8 bits."""
+    v = ((x << 1) ^ (x >> 63)) & (2**64 - 1)
+    out = bytearray()
+    for _ in range(8):
+        if v >> 7 == 0:
+            out.append(v)
+            return bytes(out)
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def chunked(data: bytes) -> bytes:
+    """OutputChunked(output, 1024) + endChunks(): <= 1024-byte chunks, each after
+    its varint length, then a zero-length chunk (CompatibleFieldSerializer's
+    per-field framing)."""
+    out = bytearray()
+    for p in range(0, len(data), 1024):
+        c = data[p:p + 1024]
+        out += varint(len(c)) + c
+    return bytes(out) + b"\x00"
+
+
+def class_name(name_id: int, name: str) -> bytes:
+    """DefaultClassResolver.writeName: NAME + 2 (= 1), the graph's name id, the name."""
+    return varint(1) + varint(name_id) + write_string(name)
+
+
+def fields_header(names) -> bytes:
+    """CompatibleFieldSerializer's first write of a class in a graph: the field
+    count and the EXTENDED cached names ("DeclaringSimpleName.field"), sorted."""
+    names = sorted(names)
+    return varint(len(names)) + b"".join(write_string(n) for n in names)
+
+
+def key_value(key_class: int, key: bytes) -> bytes:
+    """A key whose concrete class the field does not fix: class + writeBytesWithLength."""
+    return varint(key_class + 2) + varint(len(key)) + bytes(key)
+
+
+def party_body(name_der: bytes, key: bytes, key_class: int, x500_class: int) -> bytes:
+    """net.corda.core.identity.Party (identity/Party.kt: name: X500Name,
+    AbstractParty.owningKey: PublicKey) through CompatibleFieldSerializer; the
+    name via X500NameSerializer (Kryo.kt:615-624: writeBytes(encoded))."""
+    return (class_name(0, "net.corda.core.identity.Party") + fields_header(["AbstractParty.owningKey", "Party.name"])
+            + chunked(key_value(key_class, key)) + chunked(varint(x500_class + 2) + bytes(name_der)))
+
+
+def issue_command_body(cls: str, nonce: int, keys, aal_class: int) -> bytes:
+    """Command(value = <cls>(nonce: Long), signers = Arrays.asList(PublicKey[]))
+    (Structures.kt:285, TransactionBuilder.kt:124, Cash.kt:148): fields sorted
+    Command.signers, Command.value; the list via ArraysAsListSerializer
+    (kryo-serializers 0.41: length, component class, elements); PublicKey and the
+    command class by implicit NAME registration (name ids 1, 2)."""
+    signers = (varint(aal_class + 2) + varint(len(keys)) + class_name(1, "java.security.PublicKey")
+               + b"".join(key_value(kc, k) for kc, k in keys))
+    simple = cls.replace("$", ".").rsplit(".", 1)[-1]
+    value = class_name(2, cls) + fields_header([simple + ".nonce"]) + chunked(varlong_zigzag(nonce))
+    return (class_name(0, "net.corda.core.contracts.Command") + fields_header(["Command.signers", "Command.value"])
+            + chunked(signers) + chunked(value))
+
+
 def leaf(kind: str, value=None, class_id: int = 0) -> bytes:
     """The serialised leaf of one component (header included)."""
     if kind == "raw":
@@ -93,6 +163,8 @@ def leaf(kind: str, value=None, class_id: int = 0) -> bytes:
         "ed25519_key": lambda: varint(class_id + 2) + varint(32) + bytes(value),
         "public_key": lambda: varint(class_id + 2) + varint(len(value)) + bytes(value),
         "kotlin_object": lambda: varint(1) + varint(0) + write_string(value),
+        "party": lambda: party_body(value[0], value[1], value[2], class_id),
+        "issue_command": lambda: issue_command_body(value[0], value[1], value[2], class_id),
     }[kind]
     return HEADER + body()
 

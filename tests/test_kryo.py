@@ -137,3 +137,83 @@ def test_reference_ed25519_keys_decode_in_both_oracles(oracle):
             assert s["status"] == 1
             assert oracle.oracle_ed25519_verify(A, 32, sig, 64, msg, 32) == s["status"]
             assert E.verify_status(A, sig, msg) == s["status"]
+
+
+def _der(tag, body):
+    n = len(body)
+    if n < 128:
+        return bytes([tag, n]) + body
+    nb = n.to_bytes((n.bit_length() + 7) // 8, "big")
+    return bytes([tag, 0x80 | len(nb)]) + nb + body
+
+
+def x500_der(rdns):
+    """DER of an X.500 name from (oid bytes, value) pairs, one attribute per RDN,
+    values as UTF8String (BouncyCastle's default for O / L) or PrintableString (C)."""
+    out = b""
+    for oid, val in rdns:
+        tag = 0x13 if oid == bytes([0x55, 0x04, 0x06]) else 0x0C
+        out += _der(0x31, _der(0x30, _der(0x06, oid) + _der(tag, val.encode())))
+    return _der(0x30, out)
+
+
+O, L, C = bytes([0x55, 0x04, 0x0A]), bytes([0x55, 0x04, 0x07]), bytes([0x55, 0x04, 0x06])
+
+
+def test_party_and_issue_command_leaves_match_the_restatement():
+    """§8f-4 beyond keys and objects: the notary Party and the issue Command of a
+    cash-issue transaction (CashIssueFlow.kt:52-54 -> OnLedgerAsset.generateIssue,
+    TransactionBuilder.addCommand) natively, vs oracle/kryo_leaves.py. PARITY
+    UNPINNED beyond the key bytes inside them (checked against the reference's
+    own serialised key below)."""
+    rng = random.Random(11)
+    ref_keys = [bytes.fromhex(v["A"]) for v in _key_vectors()]
+    items = []
+    for i in range(120):
+        name = x500_der([(O, "Notary Service %d" % rng.randrange(1000)), (L, rng.choice(["Zurich", "London", "NY"])),
+                         (C, rng.choice(["CH", "GB", "US"]))] + ([(O, "x" * rng.randrange(100, 300))] if i % 7 == 0 else []))
+        if i % 3 == 0:
+            key, kc = rng.choice(ref_keys), 45
+        elif i % 3 == 1:
+            key, kc = bytes(rng.getrandbits(8) for _ in range(32)), rng.randrange(20, 200)
+        else:
+            key, kc = bytes(rng.getrandbits(8) for _ in range(91)), rng.randrange(20, 200)
+        items.append(("party", (name, key, kc), rng.randrange(20, 200)))
+        keys = [(45, rng.choice(ref_keys)) if rng.random() < 0.5 else (rng.randrange(20, 200), bytes(rng.getrandbits(8) for _ in range(rng.choice((32, 88, 91))))) for _ in range(rng.randrange(1, 4 if i % 11 else 40))]
+        cls = rng.choice(["net.corda.contracts.asset.Cash$Commands$Issue", "net.corda.contracts.asset.CommodityContract$Commands$Issue",
+                          "net.corda.contracts.asset.Obligation$Commands$Issue"])
+        items.append(("issue_command", (cls, rng.randrange(-2**63, 2**63), keys), rng.randrange(10, 100)))
+    got = _lib.kryo_encode(items)
+    for (k, v, c), g in zip(items, got):
+        assert g == K.leaf(k, v, c), (k, g.hex())
+    # a big signer list crosses the 1024-byte chunk boundary of the signers field
+    assert any(len(g) > 1100 for g in got)
+
+
+def test_party_leaf_shape_with_the_reference_key():
+    v = _key_vectors()[0]
+    A = bytes.fromhex(v["A"])
+    name = x500_der([(O, "Notary Service"), (L, "Zurich"), (C, "CH")])
+    leaf = _lib.kryo_encode([("party", (name, A, v["class_id"]), 50)])[0]
+    # header, NAME registration "net.corda.core.identity.Party", 2 field names,
+    # then the owningKey field: one chunk holding the pinned key serialisation
+    body = b"\x01\x00" + K.write_string("net.corda.core.identity.Party")
+    body += b"\x02" + K.write_string("AbstractParty.owningKey") + K.write_string("Party.name")
+    pinned = bytes.fromhex(v["leaf_without_references"])[8:]  # 2f 20 A
+    body += bytes([len(pinned)]) + pinned + b"\x00" + bytes([1 + len(name), 52]) + name + b"\x00"
+    assert leaf == K.HEADER + body
+
+
+def test_issue_command_leaf_shape():
+    A = bytes.fromhex(_key_vectors()[1]["A"])
+    leaf = _lib.kryo_encode([("issue_command", ("net.corda.contracts.asset.Cash$Commands$Issue", -1, [(45, A)]), 10)])[0]
+    assert leaf.startswith(K.HEADER + b"\x01\x00" + K.write_string("net.corda.core.contracts.Command") + b"\x02")
+    assert bytes([12, 1]) + b"\x01\x01" + K.write_string("java.security.PublicKey") + b"\x2f\x20" + A in leaf
+    assert leaf.endswith(K.write_string("Issue.nonce") + b"\x01\x01\x00\x00")  # zig-zag(-1) = 1, inner and outer end chunks
+
+
+def test_bad_composite_items_are_rejected():
+    with pytest.raises(_lib.EngineError):
+        _lib.kryo_encode([("party", (b"\x30\x40ab", b"k" * 32, 45), 50)])  # DER longer than the data
+    with pytest.raises(_lib.EngineError):
+        _lib.kryo_encode([("issue_command", ("net.corda.X$Issue", 1, []), 10)])  # no signers
