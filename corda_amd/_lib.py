@@ -20,6 +20,7 @@ STATUS_NAMES = {OK: "OK", BAD_SIG: "BAD_SIG", MALFORMED_SIG: "MALFORMED_SIG", BA
 RSA_SHA256, ECDSA_SECP256K1_SHA256, ECDSA_SECP256R1_SHA256, EDDSA_ED25519_SHA512, SPHINCS256_SHA256 = 1, 2, 3, 4, 5
 
 SUCCESS = 0
+ERR_TIMEOUT = -5
 ERR_NOT_IMPLEMENTED = -7
 
 # every symbol include/cordahip.h declares (checked by tests/test_abi.py)

@@ -1199,9 +1199,11 @@ CDEV void ecdsa_affine_lane(uint32_t* __restrict__ rec) {
 
 // One kernel per curve (launched over the whole chunk; the other curve's lanes
 // exit at once, and the partition makes them whole waves): the register
-// allocations differ (P-256 fits 164 VGPRs = 3 waves per SIMD, secp256k1's
-// GLV ladder needs ~221 = 2 waves), and a combined kernel runs both at the
-// larger one.
+// allocations differ (P-256 allocates 164 VGPRs = 3 waves per SIMD, secp256k1's
+// GLV ladder 221 = 2 waves), and a combined kernel runs both at the larger one.
+// amdgpu_waves_per_eu(2) is a lower bound on occupancy, i.e. a VGPR CAP of 256
+// for both (the allocation itself sets 3 waves for P-256); every budget >= 164
+// leaves room for fp29_asm.hpp's fixed accumulators v160..v163.
 template <int S>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ecdsa_ladder_kernel(
     const unsigned int* __restrict__ perm, const uint8_t* __restrict__ scheme, uint64_t base, uint64_t m,

@@ -48,6 +48,9 @@ CDEV int booth_digit_col(const uint32_t* col, int j) {
 #ifndef ED_LADDER_WAVES
 #define ED_LADDER_WAVES 2
 #endif
+// the generated asm blocks (fe25519_asm.hpp) clobber the fixed accumulator
+// VGPRs v160..v167, so the kernel needs a budget of >= 168 VGPRs: 512 / waves
+static_assert(512 / ED_LADDER_WAVES >= 168, "fe25519_asm.hpp's v160..v167 accumulators need >= 168 VGPRs per lane");
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_LADDER_WAVES))) ed25519_ladder_half_kernel(
     uint64_t base, uint64_t m, const uint32_t* __restrict__ btab, const uint32_t* __restrict__ ws,

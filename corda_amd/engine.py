@@ -228,6 +228,13 @@ class Ticket:
 
     def __init__(self, eng: Engine, ticket: int, result, keep):
         self.eng, self.ticket, self._result, self._keep = eng, ticket, result, keep
+        self._waited = False
+
+    def __del__(self):
+        # a ticket dropped without wait(): the pool may still be writing into the
+        # buffers self._keep pins, so wait for it before they can be freed
+        if not getattr(self, "_waited", True) and self.eng.ctx:
+            lib().cordahip_wait(self.eng.ctx, self.ticket, -1)
 
     def poll(self) -> bool:
         r = lib().cordahip_poll(self.eng.ctx, self.ticket)
@@ -236,5 +243,8 @@ class Ticket:
         return r == 1
 
     def wait(self, timeout_ns: int = -1):
-        check(lib().cordahip_wait(self.eng.ctx, self.ticket, timeout_ns), "cordahip_wait")
+        rc = lib().cordahip_wait(self.eng.ctx, self.ticket, timeout_ns)
+        if rc != _lib.ERR_TIMEOUT:
+            self._waited = True  # released by the library (successfully or not)
+        check(rc, "cordahip_wait")
         return self._result()

@@ -145,7 +145,12 @@ int cordahip_ed25519_verify_host(cordahip_ctx* ctx, const uint8_t* keys, const u
  * scheme[n]; keys in 65-byte slots (SEC1 04||X||Y or 02/03||X) + key_len[n];
  * DER signatures in 72-byte slots + sig_len[n] (72 = the longest DER encoding of
  * r, s < 2^256); msgs n*msg_len. Device memory; lanes are partitioned by curve on
- * the device (one curve per wavefront), status and verdict come back in input order. */
+ * the device (one curve per wavefront), status and verdict come back in input order.
+ * A lane with sig_len > 72 does not fit its slot: it is MALFORMED_SIG here (EMPTY
+ * first under doVerify rules), without reading past the slot. BouncyCastle would
+ * say BAD_SIG for such a signature when its DER is well formed (an INTEGER of more
+ * than 33 bytes is >= n): use the generic batch (cordahip_sig_verify), which
+ * decides those lanes by the DER rules, for BC parity on over-long signatures. */
 int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_scheme, const void* d_keys,
                                  const void* d_key_len, const void* d_sigs, const void* d_sig_len, const void* d_msgs,
                                  uint32_t msg_len, uint64_t n, void* d_status, void* d_verdict, void* hip_stream);
@@ -354,7 +359,8 @@ int cordahip_kryo_encode(const cordahip_kryo_item* items, uint64_t n, uint8_t* o
  * `device`, from HIP events recorded around its launches on the stream it ran
  * on (waits for them); -1 if the thread made no such call. Each call gets its
  * own event pair from a per-device ring of 64, so concurrent callers on other
- * threads or streams do not disturb it. */
+ * threads or streams do not disturb it -- up to 64 calls on the device in
+ * between: after more, the slot has been reused and the result is -1. */
 double cordahip_last_kernel_ms(cordahip_ctx* ctx, int device);
 
 /* The in-process partition rule: shard `shard` of `nshards` over n lanes is
