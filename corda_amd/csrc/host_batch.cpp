@@ -37,20 +37,14 @@ namespace cordahip {
 namespace rt {
 namespace {
 
-// lanes per chunk: 2^22 (launches of 2^22 lose ~1% to grid tails against one
-// 2^24 launch, C2 measured)
-constexpr uint64_t kEdChunk = 1ull << 22;
+// lanes per chunk after the ramp (chunk/16, chunk/4, chunk): 2^23. The host
+// packs ~6x (Ed25519) / ~3.5x (ECDSA) faster than the GPU verifies
+// (profiles/r03_trace_*_host.txt, CORDAHIP_TRACE), so a x4 ramp keeps the GPU
+// fed from a short first pack, and big chunks mean few launches and few grid
+// tails (2^22-lane chunks: c2h 92.7 M/s). Pinned staging: ~1.1 GB per stage
+// for Ed25519 rows, ~1.5 GB for ECDSA slots (grow-only, 3 stages).
+constexpr uint64_t kEdChunk = 1ull << 23;
 constexpr uint64_t kGrain = 1ull << 14;  // lanes per packing piece
-
-// CORDAHIP_TRACE=1: per-chunk host timings of the pipelines on stderr (wait for
-// the stage, classify, pack, enqueue), to see whether the host or the GPU bounds
-double now_ms() {
-  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-bool tracing() {
-  static const bool on = getenv("CORDAHIP_TRACE") != nullptr;
-  return on;
-}
 
 uint64_t chunk_lanes(const char* env, uint64_t dflt) {
   const uint64_t v = env_lanes(env, 0);
@@ -480,7 +474,9 @@ int sig_verify_msgs(cordahip_ctx* ctx, const cordahip_sig_batch* b, const MsgVie
   const int rc = for_shards(ctx->devs, n, 64,
                             [&](Device& d, uint64_t lo, uint64_t hi) { return sig_pipeline(ctx, d, b, mv, lo, hi); });
   if (rc != CORDAHIP_SUCCESS) return rc;
+  const double tv = tracing() ? now_ms() : 0;
   if (b->verdict) verdict_from_status(ctx, b->status, n, b->verdict);
+  if (tracing()) fprintf(stderr, "[cordahip] verdict words: %.2f ms\n", now_ms() - tv);
   return CORDAHIP_SUCCESS;
 }
 

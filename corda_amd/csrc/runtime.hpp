@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -247,6 +249,17 @@ class WorkerPool {
   std::vector<std::thread> threads_;
   bool stop_ = false;
 };
+
+// CORDAHIP_TRACE=1: host-side phase timings of the host pipelines on stderr
+// (wait for a stage, classify, pack, enqueue; tx-id / signature phases), to
+// see whether the host or the GPU bounds a host batch
+inline double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+inline bool tracing() {
+  static const bool on = getenv("CORDAHIP_TRACE") != nullptr;
+  return on;
+}
 
 int hip_err(hipError_t e);
 hipError_t ensure_streams(Device& d);
