@@ -37,13 +37,15 @@ namespace cordahip {
 namespace rt {
 namespace {
 
-// lanes per chunk after the ramp (chunk/16, chunk/4, chunk): 2^23. The host
-// packs ~6x (Ed25519) / ~3.5x (ECDSA) faster than the GPU verifies
-// (profiles/r03_trace_*_host.txt, CORDAHIP_TRACE), so a x4 ramp keeps the GPU
-// fed from a short first pack, and big chunks mean few launches and few grid
-// tails (2^22-lane chunks: c2h 92.7 M/s). Pinned staging: ~1.1 GB per stage
-// for Ed25519 rows, ~1.5 GB for ECDSA slots (grow-only, 3 stages).
-constexpr uint64_t kEdChunk = 1ull << 23;
+// lanes per chunk after the ramp (chunk/16, chunk/4, chunk): 2^22. The host
+// packs ~6x (Ed25519) / ~3.5x (ECDSA) faster than the GPU verifies, and PCIe
+// carries ~3x the GPU's rate (profiles/r03_trace_*_host.txt, CORDAHIP_TRACE),
+// so a x4 ramp keeps the GPU fed from a short first pack. 2^23-lane chunks
+// measured worse (c2h 87.6 vs 92.7 M/s, profiles/r03_bench_c2h_chunk23.json):
+// the 1.1 GB H2D of the first big chunk can no longer hide behind the 2^21-lane
+// chunk before it. Pinned staging: ~0.55 GB per stage for Ed25519 rows, ~0.75
+// GB for ECDSA slots (grow-only, 3 stages).
+constexpr uint64_t kEdChunk = 1ull << 22;
 constexpr uint64_t kGrain = 1ull << 14;  // lanes per packing piece
 
 uint64_t chunk_lanes(const char* env, uint64_t dflt) {
