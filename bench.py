@@ -453,7 +453,7 @@ class C4:
 # ---- C5: verifier-module queue drain, mixed schemes, pinned host memory -------
 class C5:
     kernel = "ed25519 prep/ladder + ecdsa prep/inv/ladder, 3-stage H2D/kernel/D2H pipeline"
-    pmc = None
+    pmc = "r03_pmc_c5.json"  # tools/gpu_pmc.sh over bench.py --workload c5 (device-side HBM bytes per lane)
     host_timed = True  # the drain is synchronous and owns its streams: wall time, PCIe included
 
     def __init__(self, eng, device, stream, rank, args):

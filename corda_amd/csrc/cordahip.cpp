@@ -305,21 +305,17 @@ int tx_acquire_host(Device& d) {
   return CORDAHIP_SUCCESS;
 }
 
-// Transaction ids for txs [t0, t1) on one device (offsets rebased to the shard).
+// Transaction ids for txs [t0, t1) on one device. The caller's offset arrays go
+// to the device as they are (absolute offsets, no host rebasing pass): the
+// kernels get base pointers shifted by the shard's first byte / first leaf.
 int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1) {
+  (void)ctx;
   std::lock_guard<std::mutex> g(d.tx_mu);
   if (int rc = tx_acquire_host(d)) return rc;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1];
   const uint64_t nleaves = l1 - l0;
   const uint64_t b0 = b->leaf_off[l0], b1 = b->leaf_off[l1];
-  std::vector<uint64_t> loff(nleaves + 1), toff(ntx + 1);
-  ctx->host->parallel_for(nleaves + 1, 1 << 16, [&](uint64_t x, uint64_t y) {
-    for (uint64_t i = x; i < y; i++) loff[i] = b->leaf_off[l0 + i] - b0;
-  });
-  ctx->host->parallel_for(ntx + 1, 1 << 16, [&](uint64_t x, uint64_t y) {
-    for (uint64_t i = x; i < y; i++) toff[i] = b->tx_leaf_off[t0 + i] - l0;
-  });
   TxWork& w = d.tx;
   if (w.leaf_bytes.ensure(std::max<uint64_t>(b1 - b0, 16)) || w.leaf_off.ensure((nleaves + 1) * 8) ||
       w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
@@ -328,11 +324,13 @@ int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uin
   hipStream_t s = d.stream;
   hipError_t e = hipSuccess;
   if (b1 > b0) e = hipMemcpyAsync(w.leaf_bytes.p, b->leaf_bytes + b0, b1 - b0, hipMemcpyHostToDevice, s);
-  e = e ? e : hipMemcpyAsync(w.leaf_off.p, loff.data(), (nleaves + 1) * 8, hipMemcpyHostToDevice, s);
-  e = e ? e : hipMemcpyAsync(w.tx_leaf_off.p, toff.data(), (ntx + 1) * 8, hipMemcpyHostToDevice, s);
-  e = e ? e : launch_sha256_leaves(w.leaf_bytes.as<uint8_t>(), w.leaf_off.as<uint64_t>(), nleaves,
-                                   w.hashes.as<uint32_t>(), s);
-  e = e ? e : launch_merkle_root(w.hashes.as<uint32_t>(), w.tx_leaf_off.as<uint64_t>(), ntx, w.txid.as<uint8_t>(),
+  e = e ? e : hipMemcpyAsync(w.leaf_off.p, b->leaf_off + l0, (nleaves + 1) * 8, hipMemcpyHostToDevice, s);
+  e = e ? e : hipMemcpyAsync(w.tx_leaf_off.p, b->tx_leaf_off + t0, (ntx + 1) * 8, hipMemcpyHostToDevice, s);
+  // leaf i's bytes at leaf_bytes + (leaf_off[l0 + i] - b0); tx t's hashes at hashes + (tx_leaf_off[t] - l0) * 8
+  const uint8_t* bytes_base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(w.leaf_bytes.p) - b0);
+  uint32_t* hash_base = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(w.hashes.p) - l0 * 32);
+  e = e ? e : launch_sha256_leaves(bytes_base, w.leaf_off.as<uint64_t>(), nleaves, w.hashes.as<uint32_t>(), s);
+  e = e ? e : launch_merkle_root(hash_base, w.tx_leaf_off.as<uint64_t>(), ntx, w.txid.as<uint8_t>(),
                                  w.tx_status.as<uint8_t>(), s);
   e = e ? e : hipMemcpyAsync(b->txid + t0 * 32, w.txid.p, ntx * 32, hipMemcpyDeviceToHost, s);
   e = e ? e : hipMemcpyAsync(b->tx_status + t0, w.tx_status.p, ntx, hipMemcpyDeviceToHost, s);
