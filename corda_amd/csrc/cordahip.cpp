@@ -356,10 +356,13 @@ int tx_ids_range(cordahip_ctx* ctx, const cordahip_txid_batch* b, uint64_t t0, u
 }
 
 // SignedTransaction.checkSignaturesAreValid over the batch: tx ids (K3/K4),
-// then every signature over its tx's id (the generic signature pipeline), then
-// the per-tx first failing signature. Large batches run in slices of
-// transactions: slice j+1's ids (leaf bytes over PCIe, SHA-256, Merkle) are
-// computed while slice j's signatures are verified.
+// every signature over its tx's id (the generic signature pipeline), then the
+// per-tx first failing signature. The ids are produced in growing slices of
+// transactions on their own thread (leaf bytes over PCIe, SHA-256, Merkle;
+// d.tx_mu / d.stream) while ONE signature pipeline over all signatures (d.pb_mu
+// / the pipeline streams) packs each chunk as soon as its transactions' ids
+// have arrived (MsgView::ready): PCIe carries the leaves while the GPU
+// verifies earlier signatures, and the signature launches stay big.
 int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   const uint64_t ntx = b->tx.ntx;
   if (ntx == 0) return CORDAHIP_SUCCESS;
@@ -376,28 +379,54 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
     for (uint64_t t = x; t < y; t++)
       for (uint64_t s = b->tx_sig_off[t]; s < b->tx_sig_off[t + 1]; s++) tx_of[s] = t;
   });
-  uint64_t slices = ntx >= (1u << 16) ? 4 : 1;
+  // tx-id slices (CORDAHIP_TX_SLICES, default 16 from 65,536 transactions): each
+  // lands ~1/16 of the leaf bytes, so the signature chunks (2^19 lanes, half a
+  // slice's signatures at C4's 2 per tx) wait for little
+  uint64_t slices = ntx >= (1u << 16) ? 16 : 1;
   if (const char* v = getenv("CORDAHIP_TX_SLICES")) slices = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
-  slices = std::min<uint64_t>(slices, std::max<uint64_t>(ntx, 1));
-  auto tb = [&](uint64_t j) { return ntx * j / slices; };
-  int rc = tx_ids_range(ctx, &b->tx, tb(0), tb(1));
-  const double t1 = tracing() ? now_ms() : 0;
-  for (uint64_t j = 0; j < slices && rc == CORDAHIP_SUCCESS; j++) {
-    std::future<int> next;
-    if (j + 1 < slices) next = std::async(std::launch::async, [&, j] { return tx_ids_range(ctx, &b->tx, tb(j + 1), tb(j + 2)); });
-    const uint64_t s0 = b->tx_sig_off[tb(j)], s1 = b->tx_sig_off[tb(j + 1)];
-    if (s1 > s0) {
-      // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
-      cordahip_sig_batch sb{s1 - s0, b->scheme + s0, b->key, b->key_off + s0, b->sig, b->sig_off + s0, b->tx.txid,
-                            nullptr, b->sig_status + s0, nullptr, 0u};
-      rc = sig_verify_msgs(ctx, &sb, MsgView{b->tx.txid, nullptr, tx_of.data() + s0});
+  std::vector<uint64_t> bound{0};
+  for (uint64_t q = 1; q <= slices; q++) bound.push_back(ntx * q / slices);
+  std::mutex wm_mu;
+  std::condition_variable wm_cv;
+  uint64_t wm = 0;  // transactions whose ids (and statuses) are on the host
+  int ids_rc = CORDAHIP_SUCCESS;
+  double t_ids = 0;
+  std::thread ids([&] {
+    for (size_t j = 1; j < bound.size(); j++) {
+      const int r = tx_ids_range(ctx, &b->tx, bound[j - 1], bound[j]);
+      std::lock_guard<std::mutex> g(wm_mu);
+      if (r != CORDAHIP_SUCCESS) {
+        ids_rc = r;
+        break;
+      }
+      wm = bound[j];
+      wm_cv.notify_all();
     }
-    if (next.valid()) {
-      const int r2 = next.get();
-      if (rc == CORDAHIP_SUCCESS) rc = r2;
-    }
+    std::lock_guard<std::mutex> g(wm_mu);
+    if (ids_rc == CORDAHIP_SUCCESS) wm = ntx;
+    if (tracing()) t_ids = now_ms();
+    wm_cv.notify_all();
+  });
+  int rc = CORDAHIP_SUCCESS;
+  if (nsig) {
+    const std::function<bool(uint64_t)> ready = [&](uint64_t end) {
+      const uint64_t need = end ? tx_of[end - 1] + 1 : 0;
+      std::unique_lock<std::mutex> g(wm_mu);
+      wm_cv.wait(g, [&] { return wm >= need || ids_rc != CORDAHIP_SUCCESS; });
+      return ids_rc == CORDAHIP_SUCCESS;
+    };
+    MsgView mv{b->tx.txid, nullptr, tx_of.data()};
+    mv.ready = &ready;
+    if (slices > 1) mv.chunk = 1u << 19;
+    // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
+    cordahip_sig_batch sb{nsig, b->scheme, b->key, b->key_off, b->sig, b->sig_off, b->tx.txid, nullptr,
+                          b->sig_status, nullptr, 0u};
+    rc = sig_verify_msgs(ctx, &sb, mv);
   }
+  ids.join();
+  if (ids_rc != CORDAHIP_SUCCESS) return ids_rc;
   if (rc != CORDAHIP_SUCCESS) return rc;
+  const double t1 = tracing() ? t_ids : 0;
   const double t2 = tracing() ? now_ms() : 0;
   ctx->host->parallel_for(ntx, 4096, [&](uint64_t t0, uint64_t t1) {
     for (uint64_t t = t0; t < t1; t++) {
@@ -420,9 +449,9 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
     }
   });
   if (tracing())
-    fprintf(stderr, "[cordahip] signed tx batch: %llu txs, %llu sigs, %llu slices: first ids %.2f ms, ids + "
-            "signatures %.2f ms, reduce %.2f ms\n", (unsigned long long)ntx, (unsigned long long)nsig,
-            (unsigned long long)slices, t1 - t0, t2 - t1, now_ms() - t2);
+    fprintf(stderr, "[cordahip] signed tx batch: %llu txs, %llu sigs, %llu id slices: all ids at %.2f ms, "
+            "signatures done at %.2f ms, reduce %.2f ms\n", (unsigned long long)ntx, (unsigned long long)nsig,
+            (unsigned long long)slices, t1 - t0, t2 - t0, now_ms() - t2);
   return CORDAHIP_SUCCESS;
 }
 

@@ -270,7 +270,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
   std::vector<Unit> units(1);
   units[0].lo = lo;
   units[0].hi = hi;
-  const std::vector<Chunk> chunks = make_chunks(units, chunk_lanes("CORDAHIP_HOST_CHUNK", kEdChunk));
+  const std::vector<Chunk> chunks = make_chunks(units, mv.chunk ? mv.chunk : chunk_lanes("CORDAHIP_HOST_CHUNK", kEdChunk));
   const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
   std::lock_guard<std::mutex> g(d.pb_mu);
   if (hipSetDevice(d.id) != hipSuccess || ensure_streams(d) != hipSuccess) return CORDAHIP_ERR_HIP;
@@ -308,6 +308,10 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     if (e != hipSuccess) break;
     const double t1 = tracing() ? now_ms() : 0;
     const uint64_t a = chunks[k].a, m = chunks[k].b - a;
+    if (mv.ready && !(*mv.ready)(chunks[k].b)) {  // this chunk's messages are not there yet: wait for them
+      rc = CORDAHIP_ERR_HIP;  // their producer failed (its own error is what the caller returns)
+      break;
+    }
     const uint64_t np = (m + kGrain - 1) / kGrain;
     cls.resize(m);
     pieces.resize(np);

@@ -147,9 +147,14 @@ def main():
             sch = np.ascontiguousarray(sc[idx].cpu().numpy())
             kb, ko, sb, so, Mc, mo = csr
             want = np.zeros(len(idx), np.uint8)
-            orc.oracle_ecdsa_verify_batch(len(idx), sch.ctypes.data, kb.ctypes.data, ko.ctypes.data, sb.ctypes.data,
-                                          so.ctypes.data, Mc.ctypes.data, mo.ctypes.data, want.ctypes.data,
-                                          args.threads)
+            # in pieces with a progress line each (a silent 4-minute oracle call looks hung to the box)
+            step = 1 << 20
+            for p0 in range(0, len(idx), step):
+                p1 = min(len(idx), p0 + step)
+                orc.oracle_ecdsa_verify_batch(p1 - p0, sch[p0:].ctypes.data, kb.ctypes.data, ko[p0:].ctypes.data,
+                                              sb.ctypes.data, so[p0:].ctypes.data, Mc.ctypes.data, mo[p0:].ctypes.data,
+                                              want[p0:].ctypes.data, args.threads)
+                print("  ecdsa batch %d: oracle %d/%d lanes (%.0f s)" % (b, p1, len(idx), time.time() - t0), flush=True)
             got = st[idx].cpu().numpy()
             mism_o = int((got != want).sum())
             _log(args, "ecdsa", b, n, len(idx), mism, mism_o, got, want, int((st != 0).sum()))
