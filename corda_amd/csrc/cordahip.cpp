@@ -308,10 +308,15 @@ int tx_acquire_host(Device& d) {
 // Transaction ids for txs [t0, t1) on one device. The caller's offset arrays go
 // to the device as they are (absolute offsets, no host rebasing pass): the
 // kernels get base pointers shifted by the shard's first byte / first leaf.
-int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1) {
+// on_copy_stream: run on the device's pipeline copy stream instead of its
+// context stream (the signed-tx path: the id slices then never queue behind
+// the signature kernels on a shared hardware queue), finishing on an event.
+int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1,
+                 bool on_copy_stream = false) {
   (void)ctx;
   std::lock_guard<std::mutex> g(d.tx_mu);
   if (int rc = tx_acquire_host(d)) return rc;
+  if (on_copy_stream && ensure_streams(d) != hipSuccess) return CORDAHIP_ERR_HIP;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1];
   const uint64_t nleaves = l1 - l0;
@@ -321,7 +326,7 @@ int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uin
       w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
       w.txid.ensure(ntx * 32) || w.tx_status.ensure(ntx))
     return CORDAHIP_ERR_OUT_OF_MEMORY;
-  hipStream_t s = d.stream;
+  hipStream_t s = on_copy_stream ? d.s_copy : d.stream;
   hipError_t e = hipSuccess;
   if (b1 > b0) e = hipMemcpyAsync(w.leaf_bytes.p, b->leaf_bytes + b0, b1 - b0, hipMemcpyHostToDevice, s);
   e = e ? e : hipMemcpyAsync(w.leaf_off.p, b->leaf_off + l0, (nleaves + 1) * 8, hipMemcpyHostToDevice, s);
@@ -335,7 +340,7 @@ int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uin
   e = e ? e : hipMemcpyAsync(b->txid + t0 * 32, w.txid.p, ntx * 32, hipMemcpyDeviceToHost, s);
   e = e ? e : hipMemcpyAsync(b->tx_status + t0, w.tx_status.p, ntx, hipMemcpyDeviceToHost, s);
   e = e ? e : hipEventRecord(d.tx_ev, s);
-  e = e ? e : hipStreamSynchronize(s);
+  e = e ? e : hipEventSynchronize(d.tx_ev);
   return hip_err(e);
 }
 
@@ -349,10 +354,12 @@ int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
 }
 
 // tx ids of transactions [t0, t1) of b, split over the context devices
-int tx_ids_range(cordahip_ctx* ctx, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1) {
+int tx_ids_range(cordahip_ctx* ctx, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1,
+                 bool on_copy_stream = false) {
   if (t1 <= t0) return CORDAHIP_SUCCESS;
-  return for_shards(ctx->devs, t1 - t0, 1,
-                    [&](Device& d, uint64_t lo, uint64_t hi) { return tx_ids_shard(ctx, d, b, t0 + lo, t0 + hi); });
+  return for_shards(ctx->devs, t1 - t0, 1, [&](Device& d, uint64_t lo, uint64_t hi) {
+    return tx_ids_shard(ctx, d, b, t0 + lo, t0 + hi, on_copy_stream);
+  });
 }
 
 // SignedTransaction.checkSignaturesAreValid over the batch: tx ids (K3/K4),
@@ -393,7 +400,7 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   double t_ids = 0;
   std::thread ids([&] {
     for (size_t j = 1; j < bound.size(); j++) {
-      const int r = tx_ids_range(ctx, &b->tx, bound[j - 1], bound[j]);
+      const int r = tx_ids_range(ctx, &b->tx, bound[j - 1], bound[j], true);
       std::lock_guard<std::mutex> g(wm_mu);
       if (r != CORDAHIP_SUCCESS) {
         ids_rc = r;
