@@ -308,15 +308,10 @@ int tx_acquire_host(Device& d) {
 // Transaction ids for txs [t0, t1) on one device. The caller's offset arrays go
 // to the device as they are (absolute offsets, no host rebasing pass): the
 // kernels get base pointers shifted by the shard's first byte / first leaf.
-// on_copy_stream: run on the device's pipeline copy stream instead of its
-// context stream (the signed-tx path: the id slices then never queue behind
-// the signature kernels on a shared hardware queue), finishing on an event.
-int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1,
-                 bool on_copy_stream = false) {
+int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1) {
   (void)ctx;
   std::lock_guard<std::mutex> g(d.tx_mu);
   if (int rc = tx_acquire_host(d)) return rc;
-  if (on_copy_stream && ensure_streams(d) != hipSuccess) return CORDAHIP_ERR_HIP;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1];
   const uint64_t nleaves = l1 - l0;
@@ -326,7 +321,7 @@ int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uin
       w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
       w.txid.ensure(ntx * 32) || w.tx_status.ensure(ntx))
     return CORDAHIP_ERR_OUT_OF_MEMORY;
-  hipStream_t s = on_copy_stream ? d.s_copy : d.stream;
+  hipStream_t s = d.stream;
   hipError_t e = hipSuccess;
   if (b1 > b0) e = hipMemcpyAsync(w.leaf_bytes.p, b->leaf_bytes + b0, b1 - b0, hipMemcpyHostToDevice, s);
   e = e ? e : hipMemcpyAsync(w.leaf_off.p, b->leaf_off + l0, (nleaves + 1) * 8, hipMemcpyHostToDevice, s);
@@ -353,30 +348,63 @@ int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
                     [&](Device& d, uint64_t t0, uint64_t t1) { return tx_ids_shard(ctx, d, b, t0, t1); });
 }
 
-// tx ids of transactions [t0, t1) of b, split over the context devices
-int tx_ids_range(cordahip_ctx* ctx, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1,
-                 bool on_copy_stream = false) {
-  if (t1 <= t0) return CORDAHIP_SUCCESS;
-  return for_shards(ctx->devs, t1 - t0, 1, [&](Device& d, uint64_t lo, uint64_t hi) {
-    return tx_ids_shard(ctx, d, b, t0 + lo, t0 + hi, on_copy_stream);
-  });
+// The tx ids of one device's shard, in slices, ALL enqueued at once on the
+// device's context stream (d.tx_mu held, the previous users of d.tx finished):
+// slice j's leaf bytes and offsets go H2D into their region of whole-shard
+// buffers (offset arrays unchanged, shifted base pointers), its SHA-256 and
+// Merkle kernels run, its ids and statuses come back, then ev[j] is recorded.
+// The host waits on the events in order -- no round trip per slice.
+hipError_t tx_ids_enqueue_slices(Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound,
+                                 std::vector<hipEvent_t>& ev) {
+  const uint64_t t0 = bound.front(), t1 = bound.back(), ntx = t1 - t0;
+  const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
+  const uint64_t b0 = b->leaf_off[l0], b1 = b->leaf_off[l1];
+  TxWork& w = d.tx;
+  if (w.leaf_bytes.ensure(std::max<uint64_t>(b1 - b0, 16)) || w.leaf_off.ensure((nleaves + 1) * 8) ||
+      w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
+      w.txid.ensure(std::max<uint64_t>(ntx, 1) * 32) || w.tx_status.ensure(std::max<uint64_t>(ntx, 1)))
+    return hipErrorOutOfMemory;
+  hipStream_t s = d.stream;
+  const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
+  const uint8_t* bytes_base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(w.leaf_bytes.p) - b0);
+  uint32_t* hash_base = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(w.hashes.p) - l0 * 32);
+  hipError_t e = hipSuccess;
+  for (size_t j = 0; j + 1 < bound.size() && e == hipSuccess; j++) {
+    const uint64_t ts0 = bound[j], ts1 = bound[j + 1];
+    const uint64_t ls0 = b->tx_leaf_off[ts0], ls1 = b->tx_leaf_off[ts1];
+    const uint64_t bs0 = b->leaf_off[ls0], bs1 = b->leaf_off[ls1];
+    if (bs1 > bs0) e = hipMemcpyAsync(w.leaf_bytes.as<uint8_t>() + (bs0 - b0), b->leaf_bytes + bs0, bs1 - bs0, h2d, s);
+    e = e ? e : hipMemcpyAsync(w.leaf_off.as<uint64_t>() + (ls0 - l0), b->leaf_off + ls0, (ls1 - ls0 + 1) * 8, h2d, s);
+    e = e ? e : hipMemcpyAsync(w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), b->tx_leaf_off + ts0, (ts1 - ts0 + 1) * 8, h2d, s);
+    e = e ? e : launch_sha256_leaves(bytes_base, w.leaf_off.as<uint64_t>() + (ls0 - l0), ls1 - ls0,
+                                     w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
+    e = e ? e : launch_merkle_root(hash_base, w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), ts1 - ts0,
+                                   w.txid.as<uint8_t>() + (ts0 - t0) * 32, w.tx_status.as<uint8_t>() + (ts0 - t0), s);
+    if (ts1 > ts0) {
+      e = e ? e : hipMemcpyAsync(b->txid + ts0 * 32, w.txid.as<uint8_t>() + (ts0 - t0) * 32, (ts1 - ts0) * 32, d2h, s);
+      e = e ? e : hipMemcpyAsync(b->tx_status + ts0, w.tx_status.as<uint8_t>() + (ts0 - t0), ts1 - ts0, d2h, s);
+    }
+    e = e ? e : hipEventRecord(ev[j], s);
+  }
+  return e ? e : hipEventRecord(d.tx_ev, s);
 }
 
 // SignedTransaction.checkSignaturesAreValid over the batch: tx ids (K3/K4),
 // every signature over its tx's id (the generic signature pipeline), then the
-// per-tx first failing signature. The ids are produced in growing slices of
-// transactions on their own thread (leaf bytes over PCIe, SHA-256, Merkle;
-// d.tx_mu / d.stream) while ONE signature pipeline over all signatures (d.pb_mu
-// / the pipeline streams) packs each chunk as soon as its transactions' ids
-// have arrived (MsgView::ready): PCIe carries the leaves while the GPU
-// verifies earlier signatures, and the signature launches stay big.
+// per-tx first failing signature. Every device's tx ids are enqueued at once in
+// 16 slices on its context stream (tx_ids_enqueue_slices); one waiter thread
+// per device follows the slice events and raises that device's watermark,
+// while ONE signature pipeline over all signatures (d.pb_mu, the pipeline
+// streams) packs each chunk as soon as the ids of its transactions are on the
+// host (MsgView::ready): the 1.05 GB of leaf bytes of C4's 1.25 M transactions
+// cross PCIe while the GPU verifies the signatures of earlier transactions.
 int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   const uint64_t ntx = b->tx.ntx;
   if (ntx == 0) return CORDAHIP_SUCCESS;
-  if (ntx && (!b->tx_sig_off || !b->first_bad_sig || !b->sig_status)) return CORDAHIP_ERR_INVALID_ARG;
-  if (ntx && (!b->tx.leaf_off || !b->tx.tx_leaf_off || !b->tx.txid || !b->tx.tx_status || !b->tx.leaf_bytes))
+  if (!b->tx_sig_off || !b->first_bad_sig || !b->sig_status) return CORDAHIP_ERR_INVALID_ARG;
+  if (!b->tx.leaf_off || !b->tx.tx_leaf_off || !b->tx.txid || !b->tx.tx_status || !b->tx.leaf_bytes)
     return CORDAHIP_ERR_INVALID_ARG;
-  const uint64_t nsig = ntx ? b->tx_sig_off[ntx] : 0;
+  const uint64_t nsig = b->tx_sig_off[ntx];
   if (nsig && (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off)) return CORDAHIP_ERR_INVALID_ARG;
   const double t0 = tracing() ? now_ms() : 0;
   // each signature signs its transaction's id (SignedTransaction.kt:98): the
@@ -386,42 +414,77 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
     for (uint64_t t = x; t < y; t++)
       for (uint64_t s = b->tx_sig_off[t]; s < b->tx_sig_off[t + 1]; s++) tx_of[s] = t;
   });
-  // tx-id slices (CORDAHIP_TX_SLICES, default 16 from 65,536 transactions): each
-  // lands ~1/16 of the leaf bytes, so the signature chunks (2^19 lanes, half a
-  // slice's signatures at C4's 2 per tx) wait for little
+  // per device: its contiguous tx shard [lo, hi) in slices (CORDAHIP_TX_SLICES,
+  // default 16 from 65,536 transactions; each lands ~1/16 of the leaf bytes)
+  const uint64_t nd = ctx->devs.size();
   uint64_t slices = ntx >= (1u << 16) ? 16 : 1;
   if (const char* v = getenv("CORDAHIP_TX_SLICES")) slices = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
-  std::vector<uint64_t> bound{0};
-  for (uint64_t q = 1; q <= slices; q++) bound.push_back(ntx * q / slices);
+  struct Shard {
+    uint64_t lo = 0, hi = 0, done = 0;  // ids of [lo, done) are on the host
+    std::vector<uint64_t> bound;
+    std::vector<hipEvent_t> ev;
+  };
+  std::vector<Shard> sh(nd);
   std::mutex wm_mu;
   std::condition_variable wm_cv;
-  uint64_t wm = 0;  // transactions whose ids (and statuses) are on the host
   int ids_rc = CORDAHIP_SUCCESS;
-  double t_ids = 0;
-  std::thread ids([&] {
-    for (size_t j = 1; j < bound.size(); j++) {
-      const int r = tx_ids_range(ctx, &b->tx, bound[j - 1], bound[j], true);
-      std::lock_guard<std::mutex> g(wm_mu);
-      if (r != CORDAHIP_SUCCESS) {
-        ids_rc = r;
-        break;
-      }
-      wm = bound[j];
-      wm_cv.notify_all();
-    }
+  auto fail = [&](int r) {
     std::lock_guard<std::mutex> g(wm_mu);
-    if (ids_rc == CORDAHIP_SUCCESS) wm = ntx;
-    if (tracing()) t_ids = now_ms();
+    if (ids_rc == CORDAHIP_SUCCESS) ids_rc = r;
     wm_cv.notify_all();
-  });
+  };
+  for (uint64_t i = 0; i < nd; i++) {
+    shard_range(ntx, nd, i, 1, sh[i].lo, sh[i].hi);
+    sh[i].done = sh[i].lo;
+  }
+  std::vector<std::thread> waiters;
+  for (uint64_t i = 0; i < nd; i++) {
+    Shard& S = sh[i];
+    if (S.lo >= S.hi) continue;
+    for (uint64_t q = 0; q <= slices; q++) S.bound.push_back(S.lo + (S.hi - S.lo) * q / slices);
+    S.ev.assign(slices, nullptr);
+    Device& d = *ctx->devs[i];
+    int r = CORDAHIP_SUCCESS;
+    {
+      std::lock_guard<std::mutex> g(d.tx_mu);
+      r = tx_acquire_host(d);
+      for (auto& e : S.ev)
+        if (r == CORDAHIP_SUCCESS && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) r = CORDAHIP_ERR_HIP;
+      if (r == CORDAHIP_SUCCESS && tx_ids_enqueue_slices(d, &b->tx, S.bound, S.ev) != hipSuccess) r = CORDAHIP_ERR_HIP;
+    }
+    if (r != CORDAHIP_SUCCESS) {
+      fail(r);
+      break;
+    }
+    waiters.emplace_back([&, i] {
+      Shard& W = sh[i];
+      (void)hipSetDevice(ctx->devs[i]->id);
+      for (size_t j = 0; j < W.ev.size(); j++) {
+        if (hipEventSynchronize(W.ev[j]) != hipSuccess) {
+          fail(CORDAHIP_ERR_HIP);
+          return;
+        }
+        std::lock_guard<std::mutex> g(wm_mu);
+        W.done = W.bound[j + 1];
+        wm_cv.notify_all();
+      }
+    });
+  }
+  // lanes [a, e) may be packed once every tx they sign has its id on the host
+  const std::function<bool(uint64_t, uint64_t)> ready = [&](uint64_t a, uint64_t e) {
+    if (a >= e) return true;
+    const uint64_t x = tx_of[a], y = tx_of[e - 1] + 1;
+    std::unique_lock<std::mutex> g(wm_mu);
+    wm_cv.wait(g, [&] {
+      if (ids_rc != CORDAHIP_SUCCESS) return true;
+      for (const Shard& S : sh)
+        if (S.lo < y && x < S.hi && S.done < std::min(S.hi, y)) return false;
+      return true;
+    });
+    return ids_rc == CORDAHIP_SUCCESS;
+  };
   int rc = CORDAHIP_SUCCESS;
-  if (nsig) {
-    const std::function<bool(uint64_t)> ready = [&](uint64_t end) {
-      const uint64_t need = end ? tx_of[end - 1] + 1 : 0;
-      std::unique_lock<std::mutex> g(wm_mu);
-      wm_cv.wait(g, [&] { return wm >= need || ids_rc != CORDAHIP_SUCCESS; });
-      return ids_rc == CORDAHIP_SUCCESS;
-    };
+  if (nsig && ids_rc == CORDAHIP_SUCCESS) {
     MsgView mv{b->tx.txid, nullptr, tx_of.data()};
     mv.ready = &ready;
     if (slices > 1) mv.chunk = 1u << 19;
@@ -430,10 +493,15 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
                           b->sig_status, nullptr, 0u};
     rc = sig_verify_msgs(ctx, &sb, mv);
   }
-  ids.join();
+  for (auto& t : waiters) t.join();
+  for (uint64_t i = 0; i < nd; i++) {
+    (void)hipSetDevice(ctx->devs[i]->id);
+    for (hipEvent_t e : sh[i].ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+  const double t_ids = tracing() ? now_ms() : 0;
   if (ids_rc != CORDAHIP_SUCCESS) return ids_rc;
   if (rc != CORDAHIP_SUCCESS) return rc;
-  const double t1 = tracing() ? t_ids : 0;
   const double t2 = tracing() ? now_ms() : 0;
   ctx->host->parallel_for(ntx, 4096, [&](uint64_t t0, uint64_t t1) {
     for (uint64_t t = t0; t < t1; t++) {
@@ -456,9 +524,9 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
     }
   });
   if (tracing())
-    fprintf(stderr, "[cordahip] signed tx batch: %llu txs, %llu sigs, %llu id slices: all ids at %.2f ms, "
+    fprintf(stderr, "[cordahip] signed tx batch: %llu txs, %llu sigs, %llu id slices per device: ids and "
             "signatures done at %.2f ms, reduce %.2f ms\n", (unsigned long long)ntx, (unsigned long long)nsig,
-            (unsigned long long)slices, t1 - t0, t2 - t0, now_ms() - t2);
+            (unsigned long long)slices, t_ids - t0, now_ms() - t2);
   return CORDAHIP_SUCCESS;
 }
 

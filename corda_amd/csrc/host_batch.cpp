@@ -308,7 +308,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     if (e != hipSuccess) break;
     const double t1 = tracing() ? now_ms() : 0;
     const uint64_t a = chunks[k].a, m = chunks[k].b - a;
-    if (mv.ready && !(*mv.ready)(chunks[k].b)) {  // this chunk's messages are not there yet: wait for them
+    if (mv.ready && !(*mv.ready)(chunks[k].a, chunks[k].b)) {  // this chunk's messages are not there yet: wait for them
       rc = CORDAHIP_ERR_HIP;  // their producer failed (its own error is what the caller returns)
       break;
     }

@@ -317,10 +317,10 @@ struct MsgView {
   const uint8_t* base;
   const uint64_t* off;
   const uint64_t* tx_of;
-  // optional: blocks until the messages of lanes [0, end) exist (a producer --
-  // the tx-id slices of a signed-tx batch -- is still writing them); false =
-  // the producer failed
-  const std::function<bool(uint64_t end)>* ready = nullptr;
+  // optional: blocks until the messages of lanes [begin, end) exist (a
+  // producer -- the tx-id slices of a signed-tx batch -- is still writing
+  // them); false = the producer failed
+  const std::function<bool(uint64_t begin, uint64_t end)>* ready = nullptr;
   uint64_t chunk = 0;  // lanes per pipeline chunk (0: the default, CORDAHIP_HOST_CHUNK)
   const uint8_t* ptr(uint64_t i) const { return tx_of ? base + 32 * tx_of[i] : base + off[i]; }
   uint64_t len(uint64_t i) const { return tx_of ? 32 : off[i + 1] - off[i]; }

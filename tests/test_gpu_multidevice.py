@@ -7,8 +7,9 @@ reassembly of statuses / verdict words run for real. tests/multidev_worker.py
 drives the generic CSR batch (both sections), the dense host rows, tx ids,
 signed and filtered transactions and the C5 stream, and compares every result
 with the goldens / oracle and with a one-device context. Small pipeline chunks
-(CORDAHIP_HOST_CHUNK / _EC_CHUNK / CORDAHIP_STREAM_CHUNK) make every shard span
-several chunks and reuse all pipeline stages."""
+(CORDAHIP_HOST_CHUNK / CORDAHIP_STREAM_CHUNK) make every shard span several
+chunks and reuse all pipeline stages; CORDAHIP_TX_SLICES=5 runs every device's
+tx ids of a signed-tx batch as 5 asynchronous slices feeding the signatures."""
 import json
 import os
 import subprocess
@@ -23,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.parametrize("replicas", [2, 3])
 def test_multi_device_context(replicas):
     env = dict(os.environ, CORDAHIP_TEST_DEVICE_REPLICAS=str(replicas), CORDAHIP_HOST_CHUNK="256",
-               CORDAHIP_HOST_EC_CHUNK="128", CORDAHIP_STREAM_CHUNK="512")
+               CORDAHIP_STREAM_CHUNK="512", CORDAHIP_TX_SLICES="5")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "multidev_worker.py")], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

@@ -80,6 +80,43 @@ def test_signed_tx_semantics(engine, oracle):
     assert len(sig_st) == len(flat)
 
 
+@pytest.mark.parametrize("slices", ["1", "3", "16"])
+def test_signed_tx_id_slices(engine, oracle, slices, monkeypatch):
+    """cordahip_signed_tx_verify with the tx ids in asynchronous slices that feed
+    the signature pipeline (CORDAHIP_TX_SLICES; the default is 16 from 65,536
+    transactions): results must not depend on the slicing, including slices
+    with no transactions and transactions without signatures or components."""
+    monkeypatch.setenv("CORDAHIP_TX_SLICES", slices)
+    monkeypatch.setenv("CORDAHIP_HOST_CHUNK", "128")
+    rng = random.Random(31)
+    txs = [[bytes(rng.getrandbits(8) for _ in range(n)) for n in (120, 60, 43)] for _ in range(150)]
+    ids, _ = engine.tx_ids(txs)
+    sigs = []
+    for t in range(150):
+        per = []
+        for j in range(t % 4):
+            p, s = _sign(oracle, hashlib.sha256(b"sl%d" % j).digest(), ids[t].tobytes())
+            if t % 11 == 5 and j == 1:
+                s = s[:3] + bytes([s[3] ^ 2]) + s[4:]
+            per.append((ED, p, s))
+        sigs.append(per)
+    txs[7] = []  # no components
+    got_ids, tx_st, first_bad, sig_st = engine.signed_tx_verify(txs, sigs)
+    want = []
+    for t in range(150):
+        if not sigs[t]:
+            want.append(7)
+        elif not txs[t]:
+            want.append(6)
+        elif t % 11 == 5 and len(sigs[t]) > 1:
+            want.append(1)
+        else:
+            want.append(0)
+    assert [int(x) for x in tx_st] == want
+    assert [int(x) for x in first_bad] == [1 if w == 1 else -1 for w in want]
+    assert all(got_ids[t].tobytes() == ids[t].tobytes() for t in range(150) if t != 7)
+
+
 def test_signed_tx_device_path(engine, oracle):
     torch = pytest.importorskip("torch")
     rng = random.Random(12)
