@@ -281,6 +281,23 @@ CDEV void f29_mulk_red(f29& r, const f29& a) {
   }
   f29_fold<F>(r, a.v[8] * K + cy);
 }
+// r = K a with one carry pass and NO fold: limbs 0..7 < 2^29, the top limb
+// keeps the bits >= 2^232. For a REDC output a (value < 1.5p when its operands
+// were < 4p each) and K = 3: value < 4.5p, top < 2^26.2 -- the P-256
+// doubling's alpha, whose products alpha^2 (< 20.25 p^2) and alpha (4 beta - X3)
+// (< 27 p^2) stay under the Montgomery bound R p ~ 32 p^2 (the fold's ~25
+// instructions per doubling saved; tests/test_fp29_model.py checks the columns).
+template <class F, int K>
+CDEV void f29_mulk_carry(f29& r, const f29& a) {
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = a.v[i] * K + cy;
+    r.v[i] = t & kMask29;
+    cy = t >> 29;
+  }
+  r.v[8] = a.v[8] * K + cy;
+}
 
 // canonical residue in [0, p), limbs fully normalised
 template <class F>

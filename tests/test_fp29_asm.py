@@ -38,8 +38,9 @@ def parse_header(text):
     return funcs
 
 
-def emulate(lines, ops, a, b):
-    """Run one asm body; a/b: {0: limbs, 1: limbs}; returns (r0 limbs, r1 limbs)."""
+def emulate(lines, ops, a, b, subs=None):
+    """Run one asm body; a/b: {0: limbs, 1: limbs}; subs: {"s00": limbs, ...};
+    returns (r0 limbs, r1 limbs) as the asm leaves them (before any fold)."""
     vals = {}
     for n, e in ops.items():
         if isinstance(e, int):
@@ -48,6 +49,9 @@ def emulate(lines, ops, a, b):
         mm = re.fullmatch(r"([ab])([01])\.v\[(\d)\]", e)
         if mm and int(mm.group(2)) in (a if mm.group(1) == "a" else b):
             vals[n] = (a if mm.group(1) == "a" else b)[int(mm.group(2))][int(mm.group(3))]
+        ms = re.fullmatch(r"(s\d\d)\.v\[(\d)\]", e)
+        if ms:
+            vals[n] = subs[ms.group(1)][int(ms.group(2))]
     acc = {"v[160:161]": 0, "v[162:163]": 0}  # exact integers: a wrap is an error
 
     def val(x):
@@ -80,10 +84,8 @@ def emulate(lines, ops, a, b):
             vals[dst(x[0])] = (val(x[1]) * val(x[2])) & M32
         elif op == "v_and_b32":
             vals[dst(x[0])] = val(x[1]) & val(x[2])
-        elif op == "v_sub_u32":
-            r = val(x[1]) - val(x[2])
-            assert r >= 0
-            vals[dst(x[0])] = r
+        elif op == "v_sub_u32":  # wraps mod 2^32 (the folded top limb may)
+            vals[dst(x[0])] = (val(x[1]) - val(x[2])) & M32
         elif op == "v_lshrrev_b64":
             acc[x[0]] = val(x[2]) >> int(x[1])
         elif op == "v_add_u32":
@@ -165,3 +167,52 @@ def test_pairs_match_f29_mul(curve, shape):
             assert got[q] == want
             assert value(want) % p == value(a[q]) * value(b[q]) * rinv % p
             assert value(want) < 2 * p
+
+
+@pytest.mark.parametrize("curve", ["k1", "r1"])
+@pytest.mark.parametrize("spec", gen_fp29_asm.SUB_FUNCS, ids=[f[1] for f in gen_fp29_asm.SUB_FUNCS])
+def test_sub_variants_match_product_then_subtract(curve, spec):
+    """The *_sub blocks: product and subtraction in one REDC, then f29_fold,
+    give the limbs of the product followed by a subtract-and-reduce pass with
+    the same multiple of p (tests/test_fp29_model.py's F.mul(a, b, subs)),
+    for operands and norm subtrahends at the top of their ranges."""
+    import test_fp29_model as model
+
+    kinds, name, sub_spec, _ = spec
+    with open(HDR) as f:
+        funcs = parse_header(f.read())
+    lines, ops = funcs["f29a_%s_%s" % (name, curve)]
+    F = model.FIELDS[2 if curve == "k1" else 3]
+    p = F.p
+    rng = random.Random(hash((curve, name)) & 0xffff)
+
+    def norm(top=False):  # a norm value (< 2p) in normalised limbs; top: 2p - 1
+        v = 2 * p - 1 if top else rng.randrange(2 * p)
+        return [(v >> (29 * i)) & M29 for i in range(8)] + [v >> 232]
+
+    for it in range(40):
+        edge = it < 2  # every operand and subtrahend at 2p - 1
+        a = {0: norm(edge), 1: norm(edge)}
+        b = {0: norm(edge), 1: norm(edge)}
+        for q in range(len(kinds)):
+            if kinds[q] == "sqr":
+                b[q] = a[q]
+        subs = {}
+        for q, sp in enumerate(sub_spec):
+            for j, sk in enumerate(sp):
+                if sk == "e":
+                    subs["s%d%d" % (q, j)] = norm(edge)
+        got = emulate(lines, ops, a, b, subs)
+        want = []
+        for q in range(len(kinds)):
+            if sub_spec[q] and sub_spec[q][0] == "o":
+                ss = [want[0]] * len(sub_spec[q])
+            else:
+                ss = [subs["s%d%d" % (q, j)] for j in range(len(sub_spec[q]))]
+            want.append(F.mul(a[q], b[q], tuple(ss)))
+        for q in range(len(kinds)):
+            if sub_spec[q]:
+                g = F.fold(got[q][:8] + [0], got[q][8])
+            else:
+                g = got[q]
+            assert g == want[q], (q, g, want[q])

@@ -43,10 +43,19 @@ class Fp29:
     def val(a):
         return sum(v << (29 * i) for i, v in enumerate(a))
 
-    def mul(self, a, b):
+    def mul(self, a, b, subs=()):
+        """f29_mul; with subs, the fp29_asm.hpp *_sub variants: output column
+        9 + i also accumulates limb i of kp - sum subs (k = 4, or 6 for three),
+        the top limb wraps mod 2^32, then f29_fold (fp29.hpp)."""
         assert all(0 <= x < U32 for x in a + b)
         va, vb = self.val(a), self.val(b)
         assert va * vb < R * self.p, "Montgomery input bound a b < R p"
+        if subs:
+            skp = self.skp[4 if len(subs) <= 2 else 6]
+            for sb in subs:
+                assert self.val(sb) < 2 * self.p and all(x < (1 << 29) + (1 << 15) for x in sb[:8])
+            xs = [skp[i] - sum(sb[i] for sb in subs) for i in range(9)]
+            assert all(0 <= x < U32 for x in xs[:8])
         q, t, acc = [0] * 9, [0] * 9, 0
         for k in range(17):
             acc += sum(a[j] * b[k - j] for j in range(max(0, k - 8), min(k, 8) + 1))
@@ -56,9 +65,18 @@ class Fp29:
                 acc += q[k] * self.m[0]
                 assert acc & M29 == 0
             else:
+                if subs:
+                    acc += xs[k - 9]
                 t[k - 9] = acc & M29
             assert acc < U64, "column %d overflows" % k
             acc >>= 29
+        if subs:
+            top = (acc + xs[8]) % U32
+            assert top == acc + xs[8], "the folded top stays below 2^32 as a value"
+            out = self.fold(t[:8] + [0], top)
+            want = (va * vb * pow(R, -1, self.p) - sum(self.val(sb) for sb in subs)) % self.p
+            assert self.val(out) % self.p == want
+            return out
         t[8] = acc
         assert t[8] < U32
         assert self.val(t) % self.p == va * vb * pow(R, -1, self.p) % self.p
@@ -152,6 +170,19 @@ class Fp29:
         assert top < U32
         return self.fold(r, top)
 
+    def mulk_carry(self, a, k):
+        """f29_mulk_carry: k a with one carry pass, no fold (limbs 0..7 normalised,
+        the top limb keeps the rest); a a REDC output (value < 1.5p), k = 3."""
+        assert self.val(a) < 3 * self.p // 2
+        r, c = [0] * 9, 0
+        for i in range(8):
+            t = a[i] * k + c
+            assert t < U32
+            r[i], c = t & M29, t >> 29
+        r[8] = a[8] * k + c
+        assert r[8] < U32 and self.val(r) == k * self.val(a)
+        return r
+
     def canon(self, a):
         t = self.red(a)
         c = 0
@@ -213,6 +244,9 @@ class Fp29:
 
 
 FIELDS = {2: Fp29(gen.P_K1, 1), 3: Fp29(gen.P_R1, 2)}
+# ecdsa.hip EC_Z3_MUL: Z3 of the P-256 doubling and of the mixed addition as one
+# product (2 Y Z, 2 Z1 H) instead of a square minus two norms
+Z3_MUL = True
 AM3 = {2: False, 3: True}
 
 
@@ -226,26 +260,25 @@ def jdbl(F, am3, P):
         t, u = F.sub(X, delta), F.add(X, delta)
         x4 = F.add(F.add(X, X), F.add(X, X))
         b4, a3 = F.mul(x4, gamma), F.mul(t, u)      # 4 beta = (4 X) gamma: no mulk_red pass
-        a3 = F.mulk_red(a3, 3)
-        yz = F.add(Y, Z)
-        x3, yz = F.sqr(a3), F.sqr(yz)
-        x3 = F.subs_red(x3, b4, b4)
-        z3 = F.subs_red(yz, gamma, delta)
+        a3 = F.mulk_carry(a3, 3)                    # alpha < 4.5p, not folded
+        x3 = F.mul(a3, a3, (b4, b4))                # X3 = alpha^2 - 8 beta, folded into the REDC
+        if Z3_MUL:
+            z3 = F.mul(F.add(Y, Y), Z)              # Z3 = 2 Y Z as one product
+        else:
+            yz = F.add(Y, Z)
+            z3 = F.mul(yz, yz, (gamma, delta))      # Z3 = (Y + Z)^2 - gamma - delta, folded
         u = F.sub_loose(b4, x3)
-        t = F.add(gamma, gamma)
-        t, y3 = F.sqr(t), F.mul(a3, u)
-        y3 = F.subs_red(y3, t, t)
+        t = F.sqr(F.add(gamma, gamma))
+        y3 = F.mul(a3, u, (t, t))                   # Y3 = alpha (4 beta - X3) - 8 gamma^2
     else:
         A, B = F.sqr(X), F.sqr(Y)
         x4 = F.add(F.add(X, X), F.add(X, X))
         C, D = F.sqr(B), F.mul(x4, B)           # D = 2((X + B)^2 - A - C) = 4 X B, one product
         E = F.mulk_red(A, 3)
         t = F.add(Y, Y)
-        x3, z3 = F.sqr(E), F.mul(t, Z)
-        x3 = F.subs_red(x3, D, D)
-        y3 = F.mul(E, F.sub_loose(D, x3))
+        x3, z3 = F.mul(E, E, (D, D)), F.mul(t, Z)  # X3 = E^2 - 2 D folded into the REDC
         u = F.mulk_red(C, 4)
-        y3 = F.subs_red(y3, u, u)
+        y3 = F.mul(E, F.sub_loose(D, x3), (u, u))   # Y3 = E (D - X3) - 8 C
     return (x3, y3, z3)
 
 
@@ -279,21 +312,22 @@ def jmadd(F, am3, P, x2, y2):
         return (x2, F.red(y2), list(F.one))
     X1, Y1, Z1 = P
     z1z1, t = F.sqr(Z1), F.mul(y2, Z1)
-    u2, s2 = F.mul(x2, z1z1), F.mul(t, z1z1)
-    h, rr = F.subs_red(u2, X1), F.subs_red(s2, Y1)
+    h, rr = F.mul(x2, z1z1, (X1,)), F.mul(t, z1z1, (Y1,))  # H = U2 - X1, R = S2 - Y1 (+4p)
     if F.iszero_norm(h):
         return jdbl(F, am3, P) if F.iszero_norm(rr) else None
     rr = F.add(rr, rr)
-    hh, x3 = F.sqr(h), F.sqr(rr)
+    hh = F.sqr(h)
     i = F.add(hh, hh)
     i = F.add(i, i)
     j, v = F.mul(h, i), F.mul(X1, i)
-    x3 = F.subs_red(x3, j, v, v)
-    t = F.sub(v, x3)
-    y3, t = F.mul(rr, t), F.mul(Y1, j)
-    y3 = F.subs_red(y3, t, t)
-    t = F.sqr(F.add(Z1, h))
-    return (x3, y3, F.subs_red(t, z1z1, hh))
+    x3, t = F.mul(rr, rr, (j, v, v)), F.mul(Y1, j)  # X3 = r^2 - J - 2 V (+6p)
+    y3 = F.mul(rr, F.sub(v, x3), (t, t))            # Y3 = r (V - X3) - 2 Y1 J
+    if Z3_MUL:
+        z3 = F.mul(F.add(Z1, Z1), h)                # Z3 = 2 Z1 H
+    else:
+        zh = F.add(Z1, h)
+        z3 = F.mul(zh, zh, (z1z1, hh))              # Z3 = (Z1 + H)^2 - Z1Z1 - HH, folded
+    return (x3, y3, z3)
 
 
 def affine(F, P):
@@ -434,3 +468,37 @@ def test_mixed_addition_with_loose_negated_y(scheme):
 
 def test_glv_split_bound():
     assert gen.check() <= 129
+
+
+def max_columns(F, amax, bmax, sqr=False, xmax=0):
+    """Upper bound of every 64-bit column value of f29_mul (P-256 special-form
+    REDC terms, q_k < 2^29) from per-limb upper bounds of the operands, plus
+    an added term < xmax in the output columns (the *_sub variants)."""
+    cols, carry = [], 0
+    for k in range(17):
+        s = carry
+        for j in range(max(0, k - 8), min(k, 8) + 1):
+            s += amax[j] * bmax[k - j]
+        s += sum(M29 * c for c, lo, hi, off in ((1 << 9, 3, 11, 3), (1 << 18, 6, 14, 6), (F.m[7], 7, 15, 7),
+                                                 (F.m[8], 8, 16, 8)) if lo <= k <= hi)
+        if k < 9:
+            s += M29  # the p == -1 term: column + (2^29 - 1) q... bounded by one more 2^29
+        else:
+            s += xmax
+        cols.append(s)
+        carry = s >> 29
+    return cols
+
+
+def test_alpha_products_worst_case_columns():
+    """P-256 doubling with the unfolded alpha = 3 m (m a REDC output < 1.5p):
+    alpha^2 and alpha (4 beta - X3) (a sub_loose operand) stay below 2^64 in
+    every column for the worst limb of every operand, not just sampled ones."""
+    F = FIELDS[3]
+    norm = [(1 << 29) + (1 << 15)] * 2 + [1 << 29] * 6 + [1 << 25]
+    alpha = [1 << 29] * 8 + [((9 * F.p) // 2 >> 232) + 1]
+    loose = [norm[i] + F.skp[4][i] for i in range(9)]  # b4 + 4p - x3, b4 norm
+    for a, b, sq, xm in ((alpha, alpha, True, U32), (alpha, loose, False, U32)):
+        cols = max_columns(F, a, b, sq, xm)
+        assert max(cols) < U64, [c.bit_length() for c in cols]
+    assert (9 * F.p // 2) ** 2 < R * F.p and (9 * F.p // 2) * 6 * F.p < R * F.p
