@@ -160,22 +160,34 @@ int hip_err(hipError_t e) { return e == hipSuccess ? CORDAHIP_SUCCESS : CORDAHIP
 hipError_t ensure_streams(Device& d) {
   std::lock_guard<std::mutex> g(d.streams_mu);
   if (d.s_copy) return hipSuccess;
-  // the ECDSA stream at the higher priority: HIP gives it a hardware queue of
-  // its own (at normal priority it shared one with s_ed, and the two sections'
-  // kernels ran one after the other)
-  int lo = 0, hi = 0;
+  // Every pipeline stream needs a hardware queue of its own: streams sharing a
+  // queue serialise, and a copy enqueued early (the tx-id slices' leaf bytes,
+  // a C5 chunk waiting for its stage) then holds back every later kernel of the
+  // other stream. HIP hands out pool queues (GPU_MAX_HW_QUEUES, 4 on the box)
+  // round-robin over every stream of the process, so a 4th pipeline stream
+  // shared one with s_ed or s_copy depending on creation order (c4h 45.1 M
+  // sigs/s, or C5 84.6 instead of 95.8 M/s: profiles/r03_stream_queues.json). A
+  // stream created with a CU mask (here: all CUs) gets a dedicated queue; the
+  // ECDSA stream keeps the higher priority, which also gives it a queue of its
+  // own (at normal priority it shared s_ed's and the two sections ran back to back).
+  int lo = 0, hi = 0, ncu = 0;
   hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-  hipStream_t c = nullptr, x = nullptr, y = nullptr;
-  e = e ? e : hipStreamCreateWithFlags(&c, hipStreamNonBlocking);
-  e = e ? e : hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
+  e = e ? e : hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d.id);
+  std::vector<uint32_t> all((std::max(ncu, 1) + 31) / 32, 0xffffffffu);
+  auto dedicated = [&](hipStream_t* st) { return hipExtStreamCreateWithCUMask(st, (uint32_t)all.size(), all.data()); };
+  hipStream_t c = nullptr, x = nullptr, y = nullptr, z = nullptr;
+  e = e ? e : dedicated(&c);
+  e = e ? e : dedicated(&x);
   e = e ? e : hipStreamCreateWithPriority(&y, hipStreamNonBlocking, hi);
+  e = e ? e : dedicated(&z);
   if (e != hipSuccess) {
-    for (hipStream_t s : {c, x, y})
+    for (hipStream_t s : {c, x, y, z})
       if (s) (void)hipStreamDestroy(s);
     return e;
   }
   d.s_ed = x;
   d.s_ec = y;
+  d.s_idcopy = z;
   d.s_copy = c;
   return hipSuccess;
 }
@@ -353,9 +365,13 @@ int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
 // slice j's leaf bytes and offsets go H2D into their region of whole-shard
 // buffers (offset arrays unchanged, shifted base pointers), its SHA-256 and
 // Merkle kernels run, its ids and statuses come back, then ev[j] is recorded.
-// The host waits on the events in order -- no round trip per slice.
+// The host waits on the events in order -- no round trip per slice. The
+// slices' H2D copies go on d.s_idcopy, each followed by its event cev[j] that
+// the kernels wait on: the copies stream back to back at the PCIe rate while
+// earlier slices hash (in one stream, each slice's copy waited for the previous
+// slice's kernels and D2H: ~0.4 ms of idle PCIe per slice, profiles/r03_trace_c4h).
 hipError_t tx_ids_enqueue_slices(Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound,
-                                 std::vector<hipEvent_t>& ev) {
+                                 std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& cev) {
   const uint64_t t0 = bound.front(), t1 = bound.back(), ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
   const uint64_t b0 = b->leaf_off[l0], b1 = b->leaf_off[l1];
@@ -364,7 +380,7 @@ hipError_t tx_ids_enqueue_slices(Device& d, const cordahip_txid_batch* b, const 
       w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
       w.txid.ensure(std::max<uint64_t>(ntx, 1) * 32) || w.tx_status.ensure(std::max<uint64_t>(ntx, 1)))
     return hipErrorOutOfMemory;
-  hipStream_t s = d.stream;
+  hipStream_t s = d.stream, sc = d.s_idcopy ? d.s_idcopy : d.stream;
   const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
   const uint8_t* bytes_base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(w.leaf_bytes.p) - b0);
   uint32_t* hash_base = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(w.hashes.p) - l0 * 32);
@@ -373,9 +389,11 @@ hipError_t tx_ids_enqueue_slices(Device& d, const cordahip_txid_batch* b, const 
     const uint64_t ts0 = bound[j], ts1 = bound[j + 1];
     const uint64_t ls0 = b->tx_leaf_off[ts0], ls1 = b->tx_leaf_off[ts1];
     const uint64_t bs0 = b->leaf_off[ls0], bs1 = b->leaf_off[ls1];
-    if (bs1 > bs0) e = hipMemcpyAsync(w.leaf_bytes.as<uint8_t>() + (bs0 - b0), b->leaf_bytes + bs0, bs1 - bs0, h2d, s);
-    e = e ? e : hipMemcpyAsync(w.leaf_off.as<uint64_t>() + (ls0 - l0), b->leaf_off + ls0, (ls1 - ls0 + 1) * 8, h2d, s);
-    e = e ? e : hipMemcpyAsync(w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), b->tx_leaf_off + ts0, (ts1 - ts0 + 1) * 8, h2d, s);
+    if (bs1 > bs0) e = hipMemcpyAsync(w.leaf_bytes.as<uint8_t>() + (bs0 - b0), b->leaf_bytes + bs0, bs1 - bs0, h2d, sc);
+    e = e ? e : hipMemcpyAsync(w.leaf_off.as<uint64_t>() + (ls0 - l0), b->leaf_off + ls0, (ls1 - ls0 + 1) * 8, h2d, sc);
+    e = e ? e : hipMemcpyAsync(w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), b->tx_leaf_off + ts0, (ts1 - ts0 + 1) * 8, h2d, sc);
+    e = e ? e : hipEventRecord(cev[j], sc);
+    e = e ? e : hipStreamWaitEvent(s, cev[j], 0);
     e = e ? e : launch_sha256_leaves(bytes_base, w.leaf_off.as<uint64_t>() + (ls0 - l0), ls1 - ls0,
                                      w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
     e = e ? e : launch_merkle_root(hash_base, w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), ts1 - ts0,
@@ -422,7 +440,7 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   struct Shard {
     uint64_t lo = 0, hi = 0, done = 0;  // ids of [lo, done) are on the host
     std::vector<uint64_t> bound;
-    std::vector<hipEvent_t> ev;
+    std::vector<hipEvent_t> ev, cev;  // per slice: ids on the host; leaf bytes on the device
   };
   std::vector<Shard> sh(nd);
   std::mutex wm_mu;
@@ -443,14 +461,19 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
     if (S.lo >= S.hi) continue;
     for (uint64_t q = 0; q <= slices; q++) S.bound.push_back(S.lo + (S.hi - S.lo) * q / slices);
     S.ev.assign(slices, nullptr);
+    S.cev.assign(slices, nullptr);
     Device& d = *ctx->devs[i];
     int r = CORDAHIP_SUCCESS;
     {
       std::lock_guard<std::mutex> g(d.tx_mu);
       r = tx_acquire_host(d);
-      for (auto& e : S.ev)
-        if (r == CORDAHIP_SUCCESS && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) r = CORDAHIP_ERR_HIP;
-      if (r == CORDAHIP_SUCCESS && tx_ids_enqueue_slices(d, &b->tx, S.bound, S.ev) != hipSuccess) r = CORDAHIP_ERR_HIP;
+      if (r == CORDAHIP_SUCCESS && ensure_streams(d) != hipSuccess) r = CORDAHIP_ERR_HIP;
+      for (auto* v : {&S.ev, &S.cev})
+        for (auto& e : *v)
+          if (r == CORDAHIP_SUCCESS && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+            r = CORDAHIP_ERR_HIP;
+      if (r == CORDAHIP_SUCCESS && tx_ids_enqueue_slices(d, &b->tx, S.bound, S.ev, S.cev) != hipSuccess)
+        r = CORDAHIP_ERR_HIP;
     }
     if (r != CORDAHIP_SUCCESS) {
       fail(r);
@@ -487,7 +510,13 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   if (nsig && ids_rc == CORDAHIP_SUCCESS) {
     MsgView mv{b->tx.txid, nullptr, tx_of.data()};
     mv.ready = &ready;
-    if (slices > 1) mv.chunk = 1u << 19;
+    // chunks of about one id slice's signatures (C4: ~156 k): each chunk is
+    // ready when its slice's ids land, and after the last slice the GPU drains
+    // one slice's signatures, not a 2^19-lane chunk (c4h A/B on one box:
+    // 2^19 57.9, 2^18 59.4, 2^17 64.5 M sigs/s)
+    if (slices > 1)
+      mv.chunk = std::min<uint64_t>(1u << 19, std::max<uint64_t>(1u << 16, (nsig / nd / slices + 63) / 64 * 64));
+    if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) mv.chunk = std::max<uint64_t>(64, strtoull(v, nullptr, 10));
     // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
     cordahip_sig_batch sb{nsig, b->scheme, b->key, b->key_off, b->sig, b->sig_off, b->tx.txid, nullptr,
                           b->sig_status, nullptr, 0u};
@@ -496,8 +525,9 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   for (auto& t : waiters) t.join();
   for (uint64_t i = 0; i < nd; i++) {
     (void)hipSetDevice(ctx->devs[i]->id);
-    for (hipEvent_t e : sh[i].ev)
-      if (e) (void)hipEventDestroy(e);
+    for (auto* v : {&sh[i].ev, &sh[i].cev})
+      for (hipEvent_t e : *v)
+        if (e) (void)hipEventDestroy(e);
   }
   const double t_ids = tracing() ? now_ms() : 0;
   if (ids_rc != CORDAHIP_SUCCESS) return ids_rc;
@@ -733,7 +763,7 @@ void free_device(Device& d) {
     for (hipEvent_t ev : {st.ed_copied, st.ec_copied, st.ed_done, st.ec_done})
       if (ev) (void)hipEventDestroy(ev);
   }
-  for (hipStream_t ss : {d.s_copy, d.s_ed, d.s_ec})
+  for (hipStream_t ss : {d.s_copy, d.s_ed, d.s_ec, d.s_idcopy})
     if (ss) (void)hipStreamDestroy(ss);
   for (DevBuf* b : {&d.tx.leaf_bytes, &d.tx.leaf_off, &d.tx.tx_leaf_off, &d.tx.hashes, &d.tx.txid, &d.tx.tx_status,
                     &d.tx.tx_sig_off, &d.tx.msgs, &d.tx.tok, &d.tx.tok_hash, &d.tx.tx_tok_off, &d.tx.root,

@@ -192,6 +192,9 @@ struct Device {
   // serialise (with 6 stage streams C5 ran 90.6 M/s at 4 queues, 93.4 at 8).
   std::mutex streams_mu;
   hipStream_t s_copy = nullptr, s_ed = nullptr, s_ec = nullptr;
+  // signed-tx batches: the id slices' leaf-byte H2D on a stream of its own, so
+  // slice j + 1's bytes cross PCIe while slice j hashes (d.stream)
+  hipStream_t s_idcopy = nullptr;
   std::mutex stream_mu;  // serialises use of sstage (C5)
   StreamStage sstage[kStreamStages];
   // packed host pipelines: one stage set per section, each behind its mutex
