@@ -510,12 +510,14 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   if (nsig && ids_rc == CORDAHIP_SUCCESS) {
     MsgView mv{b->tx.txid, nullptr, tx_of.data()};
     mv.ready = &ready;
-    // chunks of about one id slice's signatures (C4: ~156 k): each chunk is
-    // ready when its slice's ids land, and after the last slice the GPU drains
-    // one slice's signatures, not a 2^19-lane chunk (c4h A/B on one box:
-    // 2^19 57.9, 2^18 59.4, 2^17 64.5 M sigs/s)
+    // chunks of about one id slice's signatures, in whole multiples of 2^17
+    // lanes (one full-occupancy round of the Ed25519 ladder: 2 waves x 1024
+    // SIMDs x 64): each chunk is ready soon after its slice's ids land, and
+    // after the last slice the GPU drains ~one slice's signatures instead of a
+    // 2^19-lane chunk. c4h on one box: 2^17 64.8 / 64.1, 2^18 65.2 / 63.0,
+    // 156,224 (a slice, 1.2 ladder rounds) 60.3 / 53.3, 2^19 57.9 M sigs/s
     if (slices > 1)
-      mv.chunk = std::min<uint64_t>(1u << 19, std::max<uint64_t>(1u << 16, (nsig / nd / slices + 63) / 64 * 64));
+      mv.chunk = (1u << 17) * std::min<uint64_t>(4, std::max<uint64_t>(1, nsig / nd / slices >> 17));
     if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) mv.chunk = std::max<uint64_t>(64, strtoull(v, nullptr, 10));
     // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
     cordahip_sig_batch sb{nsig, b->scheme, b->key, b->key_off, b->sig, b->sig_off, b->tx.txid, nullptr,
