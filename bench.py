@@ -281,7 +281,7 @@ class C1(C2):
 # ---- C3: mixed secp256k1 / P-256 ECDSA ----------------------------------------
 class C3:
     kernel = "ecdsa_prep_kernel + ecdsa_inv_kernel + ecdsa_ladder_kernel"
-    pmc = "r02_pmc_ecdsa_verify.json"
+    pmc = "r03_pmc_ecdsa_verify.json"
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
