@@ -476,6 +476,10 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
         r = CORDAHIP_ERR_HIP;
     }
     if (r != CORDAHIP_SUCCESS) {
+      // slices already enqueued on this device still write into the caller's
+      // txid / tx_status: let them finish before the call returns
+      for (hipStream_t st : {d.s_idcopy, d.stream})
+        if (st) (void)hipStreamSynchronize(st);
       fail(r);
       break;
     }
