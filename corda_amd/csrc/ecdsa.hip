@@ -127,12 +127,6 @@ struct jpt {
 #ifndef EC_USE_ASM2
 #define EC_USE_ASM2 1
 #endif
-#ifndef EC_Z3_MUL
-#define EC_Z3_MUL 1
-#endif
-#ifndef EC_ALPHA_NOFOLD
-#define EC_ALPHA_NOFOLD 1
-#endif
 // single products of the ladder's formulas (no partner): one asm chain each
 template <class F>
 CDEV void f29_mul1(f29& r, const f29& a, const f29& b) {
@@ -196,9 +190,6 @@ CDEV void f29_sqr_mul_pair(f29& r0, const f29& a0, f29& r1, const f29& a1, const
 // output columns (fp29_asm.hpp *_sub variants): red(a b + 4p - s0 - s1), or
 // + 6p with three subtrahends; the C versions (EC_USE_ASM2 0) compute the same
 // limbs as a product and one f29_sub*_red pass with the same multiple of p.
-#ifndef EC_REDC_SUB
-#define EC_REDC_SUB 1
-#endif
 template <class F>  // r0 = a0 b0 - s00, r1 = a1 b1 - s10 (+4p each)
 CDEV void f29_mul_pair_s1s1(f29& r0, const f29& a0, const f29& b0, const f29& s00, f29& r1, const f29& a1,
                             const f29& b1, const f29& s10) {
@@ -296,6 +287,33 @@ CDEV void f29_sqr_mul_pair_s2s2(f29& r0, const f29& a0, const f29& s00, const f2
 #endif
 }
 
+template <class F>  // r0 = a0 b0 + c0 d0 with ONE REDC (the column sums stay < 2^64 for the
+                    // mixed addition's operands: tests/test_fp29_model.py)
+CDEV void f29_mul2(f29& r0, const f29& a0, const f29& b0, const f29& c0, const f29& d0) {
+#if EC_USE_ASM2
+  if constexpr (F::kRed == 1) f29a_mul2_k1(r0, a0, b0, c0, d0);
+  else f29a_mul2_r1(r0, a0, b0, c0, d0);
+#else
+  f29 t0, t1, z;
+  for (int i = 0; i < 9; i++) z.v[i] = 0;
+  f29_mul<F>(t0, a0, b0);
+  f29_mul<F>(t1, c0, d0);
+  f29_add(t0, t0, t1);  // another representative of the same residue (< 4p)
+  f29_sub2_red<F>(r0, t0, z, z);
+#endif
+}
+template <class F>  // r0 = a0^2 - s00 - s01 - s02 (+6p)
+CDEV void f29_sqr1_s3(f29& r0, const f29& a0, const f29& s00, const f29& s01, const f29& s02) {
+#if EC_USE_ASM2
+  if constexpr (F::kRed == 1) f29a_sqr_s3_k1(r0, a0, s00, s01, s02);
+  else f29a_sqr_s3_r1(r0, a0, s00, s01, s02);
+#else
+  f29 t0;
+  f29_sqr<F>(t0, a0);
+  f29_sub3_red<F>(r0, t0, s00, s01, s02);
+#endif
+}
+
 // 2P. a = -3: dbl-2001-b (3M + 5S); a = 0: dbl-2009-l (2M + 5S) with
 // D = 4XB as one product (3M + 4S). Prime-order
 // curves have no 2-torsion, so only the point at infinity is exceptional.
@@ -319,41 +337,15 @@ CDEV void jdbl(jpt& r, const jpt& p) {
     f29_add(x4, p.X, p.X);
     f29_add(x4, x4, x4);        // 4X < 8p, limbs < 2^31: (4X) gamma < 16 p^2 < R p
     f29_mul_pair<F>(b4, x4, gamma, a3, t, u);  // 4 beta directly (no f29_mulk_red pass)
-#if EC_ALPHA_NOFOLD
     f29_mulk_carry<F, 3>(a3, a3);  // alpha = 3 (X - delta)(X + delta) < 4.5p, unfolded
-#else
-    f29_mulk_red<F, 3>(a3, a3);  // alpha = 3 (X - delta)(X + delta)
-#endif
-#if EC_Z3_MUL
-    // Z3 = 2 Y Z as one product instead of (Y + Z)^2 - gamma - delta: a
-    // product's 28 extra instructions against a square's and a subtract pass
+    // Z3 = 2 Y Z as one product instead of (Y + Z)^2 - gamma - delta (4M + 4S;
+    // equal time with the square form once both subtractions ride in REDCs,
+    // fewer instructions: profiles/r03_ec_glue_ab/)
     f29_add(yz, p.Y, p.Y);  // 2Y < 4p, limbs < 2^30.1
-#if EC_REDC_SUB
     f29_sqr_mul_pair_s2<F>(x3, a3, b4, b4, z3, yz, p.Z);  // X3 = alpha^2 - 8 beta
-#else
-    f29_sqr_mul_pair<F>(x3, a3, z3, yz, p.Z);
-    f29_sub2_red<F>(x3, x3, b4, b4);       // X3 = alpha^2 - 8 beta
-#endif
-#else
-    f29_add(yz, p.Y, p.Z);
-#if EC_REDC_SUB
-    // X3 = alpha^2 - 8 beta, Z3 = (Y + Z)^2 - gamma - delta: two squares, each
-    // subtraction folded into its REDC
-    f29_sqr_pair_s2s2<F>(x3, a3, b4, b4, z3, yz, gamma, delta);
-#else
-    f29_sqr_pair<F>(x3, a3, yz, yz);
-    f29_sub2_red<F>(x3, x3, b4, b4);       // X3 = alpha^2 - 8 beta
-    f29_sub2_red<F>(z3, yz, gamma, delta);  // Z3 = (Y + Z)^2 - gamma - delta
-#endif
-#endif
     f29_sub_loose<F>(u, b4, x3);  // < 6p, only the operand of alpha * u
     f29_add(t, gamma, gamma);
-#if EC_REDC_SUB
     f29_sqr_mul_pair_o2<F>(t, t, y3, a3, u);  // Y3 = alpha (4 beta - X3) - 2 (2 gamma)^2
-#else
-    f29_sqr_mul_pair<F>(t, t, y3, a3, u);  // 4 gamma^2, alpha (4 beta - X3)
-    f29_sub2_red<F>(y3, y3, t, t);          // Y3 = alpha (4 beta - X3) - 8 gamma^2
-#endif
   } else {
     f29 A, B, Cc, D, E, x4;
     f29_sqr_pair<F>(A, p.X, B, p.Y);
@@ -362,21 +354,12 @@ CDEV void jdbl(jpt& r, const jpt& p) {
     // D = 2 ((X + B)^2 - A - C) = 4 X B as one product: cheaper than the
     // square, the subtract pass and the doubling pass it replaces
     f29_sqr_mul_pair<F>(Cc, B, D, x4, B);
-    f29_mulk_red<F, 3>(E, A);    // E = 3 A
+    f29_mulk_carry<F, 3>(E, A);  // E = 3 A < 3.4p, unfolded (A < 1.125p: a square of a norm X)
     f29_add(t, p.Y, p.Y);
-#if EC_REDC_SUB
     f29_sqr_mul_pair_s2<F>(x3, E, D, D, z3, t, p.Z);  // X3 = E^2 - 2 D, Z3 = 2 Y Z
     f29_sub_loose<F>(t, D, x3);  // < 6p, only the operand of E * t
     f29_mulk_red<F, 4>(u, Cc);   // 4 C
     f29_mul1_s2<F>(y3, E, t, u, u);  // Y3 = E (D - X3) - 8 C
-#else
-    f29_sqr_mul_pair<F>(x3, E, z3, t, p.Z);  // E^2, Z3 = 2 Y Z
-    f29_sub2_red<F>(x3, x3, D, D);           // X3 = E^2 - 2 D
-    f29_sub_loose<F>(t, D, x3);  // < 6p, only the operand of E * t
-    f29_mul1<F>(y3, E, t);
-    f29_mulk_red<F, 4>(u, Cc);   // 4 C
-    f29_sub2_red<F>(y3, y3, u, u);  // Y3 = E (D - X3) - 8 C
-#endif
   }
   r.X = x3;
   r.Y = y3;
@@ -456,12 +439,8 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
     r.inf = false;
     return;
   }
+  // every subtraction after a product rides in that product's REDC (*_s blocks)
   f29 z1z1, u2, h, hh, i, j, rr, v, t, x3, y3, z3;
-#if EC_REDC_SUB
-#if !EC_Z3_MUL
-  f29 s2;
-#endif
-  // the subtractions after products ride in the products' REDC (*_s variants)
   f29_sqr_mul_pair<F>(z1z1, p.Z, t, y2, p.Z);
   f29_mul_pair_s1s1<F>(h, x2, z1z1, p.X, rr, t, z1z1, p.Y);  // H = U2 - X1, R = S2 - Y1
   if (f29_iszero_norm<F>(h)) {  // h, rr norm (folded outputs)
@@ -473,56 +452,17 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
     return;
   }
   f29_add(rr, rr, rr);
-#if EC_Z3_MUL
   f29_add(t, p.Z, p.Z);
-  f29_sqr_mul_pair<F>(hh, h, z3, t, h);  // HH, Z3 = 2 Z1 H
-#else
-  f29_sqr1<F>(hh, h);
-#endif
+  f29_sqr_mul_pair<F>(hh, h, z3, t, h);  // HH, Z3 = 2 Z1 H (= (Z1 + H)^2 - Z1Z1 - HH)
   f29_add(i, hh, hh);
   f29_add(i, i, i);             // I = 4 HH, < 8p
   f29_mul_pair<F>(j, h, i, v, p.X, i);
-  f29_sqr_mul_pair_s3<F>(x3, rr, j, v, v, t, p.Y, j);  // X3 = r^2 - J - 2 V, Y1 J
+  // Y1 J is only ever subtracted: Y3 = r (V - X3) + Y1 (4p - 2J) as ONE REDC
+  // (-0.8% P-256, -1.5% secp256k1 ladder time, profiles/r03_ec_y3_ab/)
+  f29_sqr1_s3<F>(x3, rr, j, v, v);  // X3 = r^2 - J - 2 V
   f29_sub<F>(u2, v, x3);
-#if EC_Z3_MUL
-  f29_mul1_s2<F>(y3, rr, u2, t, t);  // Y3 = r (V - X3) - 2 Y1 J
-#else
-  f29_add(s2, p.Z, h);
-  // Z3 = (Z1 + H)^2 - Z1Z1 - HH, Y3 = r (V - X3) - 2 Y1 J
-  f29_sqr_mul_pair_s2s2<F>(z3, s2, z1z1, hh, y3, rr, u2, t, t);
-#endif
-#else
-  f29 s2;
-  f29_sqr_mul_pair<F>(z1z1, p.Z, t, y2, p.Z);
-  f29_mul_pair<F>(u2, x2, z1z1, s2, t, z1z1);
-  f29_sub_red<F>(h, u2, p.X);
-  f29_sub_red<F>(rr, s2, p.Y);
-  if (f29_iszero_norm<F>(h)) {  // h, rr norm (f29_sub_red outputs)
-    if (f29_iszero_norm<F>(rr)) {
-      jdbl<C>(r, p);
-    } else {
-      r.inf = true;
-    }
-    return;
-  }
-  f29_add(rr, rr, rr);
-  f29_sqr_pair<F>(hh, h, x3, rr);
-  f29_add(i, hh, hh);
-  f29_add(i, i, i);             // I = 4 HH, < 8p
-  f29_mul_pair<F>(j, h, i, v, p.X, i);
-  f29_sub3_red<F>(x3, x3, j, v, v);  // X3 = r^2 - J - 2 V
-  f29_sub<F>(t, v, x3);
-  f29_mul_pair<F>(y3, rr, t, t, p.Y, j);
-  f29_sub2_red<F>(y3, y3, t, t);     // Y3 = r (V - X3) - 2 Y1 J
-#if EC_Z3_MUL
-  f29_add(t, p.Z, p.Z);
-  f29_mul1<F>(z3, t, h);  // Z3 = 2 Z1 H (= (Z1 + H)^2 - Z1Z1 - HH without the subtract pass)
-#else
-  f29_add(t, p.Z, h);
-  f29_sqr1<F>(t, t);
-  f29_sub2_red<F>(z3, t, z1z1, hh);  // Z3 = (Z1 + H)^2 - Z1Z1 - HH
-#endif
-#endif
+  f29_neg2_norm<F>(t, j);
+  f29_mul2<F>(y3, rr, u2, p.Y, t);
   r.X = x3;
   r.Y = y3;
   r.Z = z3;

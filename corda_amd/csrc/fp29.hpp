@@ -299,6 +299,21 @@ CDEV void f29_mulk_carry(f29& r, const f29& a) {
   r.v[8] = a.v[8] * K + cy;
 }
 
+// r = 4p - 2a for a norm a, one carry pass: limbs 0..7 < 2^29, value < 4p
+// (F::sub4p's limbs exceed 2a's, so no limb goes negative; the top limb is
+// the value's bits >= 2^232, >= 0). The mixed addition's Y1 (4p - 2J) operand.
+template <class F>
+CDEV void f29_neg2_norm(f29& r, const f29& a) {
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t t = F::sub4p(i) - 2 * a.v[i] + cy;
+    r.v[i] = t & kMask29;
+    cy = t >> 29;
+  }
+  r.v[8] = F::sub4p(8) - 2 * a.v[8] + cy;
+}
+
 // canonical residue in [0, p), limbs fully normalised
 template <class F>
 CDEV void f29_canon(f29& r, const f29& a) {

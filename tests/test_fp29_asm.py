@@ -49,7 +49,7 @@ def emulate(lines, ops, a, b, subs=None):
         mm = re.fullmatch(r"([ab])([01])\.v\[(\d)\]", e)
         if mm and int(mm.group(2)) in (a if mm.group(1) == "a" else b):
             vals[n] = (a if mm.group(1) == "a" else b)[int(mm.group(2))][int(mm.group(3))]
-        ms = re.fullmatch(r"(s\d\d)\.v\[(\d)\]", e)
+        ms = re.fullmatch(r"(s\d\d|[cd]0)\.v\[(\d)\]", e)
         if ms:
             vals[n] = subs[ms.group(1)][int(ms.group(2))]
     acc = {"v[160:161]": 0, "v[162:163]": 0}  # exact integers: a wrap is an error
@@ -175,7 +175,8 @@ def test_sub_variants_match_product_then_subtract(curve, spec):
     """The *_sub blocks: product and subtraction in one REDC, then f29_fold,
     give the limbs of the product followed by a subtract-and-reduce pass with
     the same multiple of p (tests/test_fp29_model.py's F.mul(a, b, subs)),
-    for operands and norm subtrahends at the top of their ranges."""
+    for operands and norm subtrahends at the top of their ranges; mul2 (a b + c d,
+    one REDC) gives the limbs of F.mul2."""
     import test_fp29_model as model
 
     kinds, name, sub_spec, _ = spec
@@ -197,7 +198,7 @@ def test_sub_variants_match_product_then_subtract(curve, spec):
         for q in range(len(kinds)):
             if kinds[q] == "sqr":
                 b[q] = a[q]
-        subs = {}
+        subs = {"c0": norm(edge), "d0": norm(edge)} if kinds[0] == "mul2" else {}
         for q, sp in enumerate(sub_spec):
             for j, sk in enumerate(sp):
                 if sk == "e":
@@ -205,6 +206,9 @@ def test_sub_variants_match_product_then_subtract(curve, spec):
         got = emulate(lines, ops, a, b, subs)
         want = []
         for q in range(len(kinds)):
+            if kinds[q] == "mul2":
+                want.append(F.mul2(a[q], b[q], subs["c0"], subs["d0"]))
+                continue
             if sub_spec[q] and sub_spec[q][0] == "o":
                 ss = [want[0]] * len(sub_spec[q])
             else:

@@ -183,6 +183,43 @@ class Fp29:
         assert r[8] < U32 and self.val(r) == k * self.val(a)
         return r
 
+    def neg2_norm(self, a):
+        """fp29.hpp f29_neg2_norm: 4p - 2a for a norm a, one carry pass."""
+        s4 = self.skp[4]
+        assert self.val(a) < 2 * self.p and all(x < (1 << 29) + (1 << 15) for x in a[:8])
+        r, c = [0] * 9, 0
+        for i in range(8):
+            t = s4[i] - 2 * a[i] + c
+            assert 0 <= t < U32
+            r[i], c = t & M29, t >> 29
+        r[8] = s4[8] - 2 * a[8] + c
+        assert 0 <= r[8] < U32 and self.val(r) == 4 * self.p - 2 * self.val(a)
+        return r
+
+    def mul2(self, a, b, c, d):
+        """fp29_asm.hpp mul2: a b + c d in the same 64-bit columns, one REDC."""
+        assert all(0 <= x < U32 for x in a + b + c + d)
+        va, vb, vc, vd = (self.val(x) for x in (a, b, c, d))
+        assert va * vb + vc * vd < R * self.p, "Montgomery input bound"
+        q, t, acc = [0] * 9, [0] * 9, 0
+        for k in range(17):
+            rng = range(max(0, k - 8), min(k, 8) + 1)
+            acc += sum(a[j] * b[k - j] + c[j] * d[k - j] for j in rng)
+            acc += sum(q[j] * self.m[k - j] for j in range(max(0, k - 8), min(k, 9)))
+            if k < 9:
+                q[k] = ((acc % U32) * self.minv % U32) & M29
+                acc += q[k] * self.m[0]
+                assert acc & M29 == 0
+            else:
+                t[k - 9] = acc & M29
+            assert acc < U64, "column %d overflows" % k
+            acc >>= 29
+        t[8] = acc
+        assert t[8] < U32
+        assert self.val(t) % self.p == (va * vb + vc * vd) * pow(R, -1, self.p) % self.p
+        assert self.val(t) < 2 * self.p
+        return t
+
     def canon(self, a):
         t = self.red(a)
         c = 0
@@ -244,9 +281,6 @@ class Fp29:
 
 
 FIELDS = {2: Fp29(gen.P_K1, 1), 3: Fp29(gen.P_R1, 2)}
-# ecdsa.hip EC_Z3_MUL: Z3 of the P-256 doubling and of the mixed addition as one
-# product (2 Y Z, 2 Z1 H) instead of a square minus two norms
-Z3_MUL = True
 AM3 = {2: False, 3: True}
 
 
@@ -262,11 +296,7 @@ def jdbl(F, am3, P):
         b4, a3 = F.mul(x4, gamma), F.mul(t, u)      # 4 beta = (4 X) gamma: no mulk_red pass
         a3 = F.mulk_carry(a3, 3)                    # alpha < 4.5p, not folded
         x3 = F.mul(a3, a3, (b4, b4))                # X3 = alpha^2 - 8 beta, folded into the REDC
-        if Z3_MUL:
-            z3 = F.mul(F.add(Y, Y), Z)              # Z3 = 2 Y Z as one product
-        else:
-            yz = F.add(Y, Z)
-            z3 = F.mul(yz, yz, (gamma, delta))      # Z3 = (Y + Z)^2 - gamma - delta, folded
+        z3 = F.mul(F.add(Y, Y), Z)                  # Z3 = 2 Y Z as one product
         u = F.sub_loose(b4, x3)
         t = F.sqr(F.add(gamma, gamma))
         y3 = F.mul(a3, u, (t, t))                   # Y3 = alpha (4 beta - X3) - 8 gamma^2
@@ -274,7 +304,7 @@ def jdbl(F, am3, P):
         A, B = F.sqr(X), F.sqr(Y)
         x4 = F.add(F.add(X, X), F.add(X, X))
         C, D = F.sqr(B), F.mul(x4, B)           # D = 2((X + B)^2 - A - C) = 4 X B, one product
-        E = F.mulk_red(A, 3)
+        E = F.mulk_carry(A, 3)                  # E = 3 A, not folded
         t = F.add(Y, Y)
         x3, z3 = F.mul(E, E, (D, D)), F.mul(t, Z)  # X3 = E^2 - 2 D folded into the REDC
         u = F.mulk_red(C, 4)
@@ -320,13 +350,9 @@ def jmadd(F, am3, P, x2, y2):
     i = F.add(hh, hh)
     i = F.add(i, i)
     j, v = F.mul(h, i), F.mul(X1, i)
-    x3, t = F.mul(rr, rr, (j, v, v)), F.mul(Y1, j)  # X3 = r^2 - J - 2 V (+6p)
-    y3 = F.mul(rr, F.sub(v, x3), (t, t))            # Y3 = r (V - X3) - 2 Y1 J
-    if Z3_MUL:
-        z3 = F.mul(F.add(Z1, Z1), h)                # Z3 = 2 Z1 H
-    else:
-        zh = F.add(Z1, h)
-        z3 = F.mul(zh, zh, (z1z1, hh))              # Z3 = (Z1 + H)^2 - Z1Z1 - HH, folded
+    x3 = F.mul(rr, rr, (j, v, v))                   # X3 = r^2 - J - 2 V (+6p)
+    y3 = F.mul2(rr, F.sub(v, x3), Y1, F.neg2_norm(j))  # Y3 = r (V - X3) + Y1 (4p - 2J), one REDC
+    z3 = F.mul(F.add(Z1, Z1), h)                    # Z3 = 2 Z1 H
     return (x3, y3, z3)
 
 
@@ -470,15 +496,18 @@ def test_glv_split_bound():
     assert gen.check() <= 129
 
 
-def max_columns(F, amax, bmax, sqr=False, xmax=0):
+def max_columns(F, amax, bmax, sqr=False, xmax=0, cmax=None, dmax=None):
     """Upper bound of every 64-bit column value of f29_mul (P-256 special-form
     REDC terms, q_k < 2^29) from per-limb upper bounds of the operands, plus
-    an added term < xmax in the output columns (the *_sub variants)."""
+    an added term < xmax in the output columns (the *_sub variants) and, for
+    mul2, the second product c d in the same columns."""
     cols, carry = [], 0
     for k in range(17):
         s = carry
         for j in range(max(0, k - 8), min(k, 8) + 1):
             s += amax[j] * bmax[k - j]
+            if cmax:
+                s += cmax[j] * dmax[k - j]
         s += sum(M29 * c for c, lo, hi, off in ((1 << 9, 3, 11, 3), (1 << 18, 6, 14, 6), (F.m[7], 7, 15, 7),
                                                  (F.m[8], 8, 16, 8)) if lo <= k <= hi)
         if k < 9:
@@ -502,3 +531,10 @@ def test_alpha_products_worst_case_columns():
         cols = max_columns(F, a, b, sq, xm)
         assert max(cols) < U64, [c.bit_length() for c in cols]
     assert (9 * F.p // 2) ** 2 < R * F.p and (9 * F.p // 2) * 6 * F.p < R * F.p
+    # mixed addition's Y3 = r (V - X3) + Y1 (4p - 2J) as one REDC: r = 2R (limbs
+    # of two norms), V - X3 and 4p - 2J carry-normalised (f29_sub, f29_neg2_norm)
+    rr = [2 * x for x in norm]
+    nrm = [1 << 29] * 8 + [((6 * F.p) >> 232) + 1]
+    cols = max_columns(F, rr, nrm, False, 0, norm, nrm)
+    assert max(cols) < U64, [c.bit_length() for c in cols]
+    assert 4 * F.p * 4 * F.p + 2 * F.p * 4 * F.p < R * F.p

@@ -82,9 +82,12 @@ def product_terms(kind, curve, nsub=0):
     for k in range(17):
         st = []
         lo, hi = max(0, k - 8), min(k, 8)
-        if kind == "mul":
+        if kind in ("mul", "mul2"):
             for j in range(lo, hi + 1):
                 st.append(("mad", "a%d" % j, "b%d" % (k - j)))
+            if kind == "mul2":  # + c d in the same columns: one REDC for the sum
+                for j in range(lo, hi + 1):
+                    st.append(("mad", "c%d" % j, "d%d" % (k - j)))
         else:
             for j in range(lo, hi + 1):
                 if 2 * j < k:
@@ -228,8 +231,11 @@ def gen(curve, kinds, subs=((), ())):
             outs.append('[x_%d] "=&v"(x%d)' % (p, p))
             decl.append("uint32_t x%d;" % p)
         ins += ['[a%d_%d] "v"(a%d.v[%d])' % (k, p, p, k) for k in range(9)]
-        if kind == "mul":
+        if kind in ("mul", "mul2"):
             ins += ['[b%d_%d] "v"(b%d.v[%d])' % (k, p, p, k) for k in range(9)]
+        if kind == "mul2":
+            ins += ['[c%d_%d] "v"(c%d.v[%d])' % (k, p, p, k) for k in range(9)]
+            ins += ['[d%d_%d] "v"(d%d.v[%d])' % (k, p, p, k) for k in range(9)]
         for j, sk in enumerate(subs[p]):
             if sk == "e":
                 ins += ['[s%d%d_%d] "v"(s%d%d.v[%d])' % (p, j, k, p, j, k) for k in range(9)]
@@ -291,6 +297,10 @@ SUB_FUNCS = (
      "f29& r0, const f29& a0, const f29& s00, const f29& s01, const f29& s02, f29& r1, const f29& a1, const f29& b1"),
     (("sqr", "mul"), "sqr_mul_o2", ((), ("o", "o")), "f29& r0, const f29& a0, f29& r1, const f29& a1, const f29& b1"),
     (("mul",), "mul_s2", (("e", "e"),), "f29& r0, const f29& a0, const f29& b0, const f29& s00, const f29& s01"),
+    #   mul2:         r0 = a0 b0 + c0 d0, ONE REDC             (jmadd: Y3 = r (V - X3) + Y1 (4p - 2J))
+    #   sqr_s3:       r0 = a0^2 - s00 - s01 - s02              (jmadd: X3, now unpaired)
+    (("mul2",), "mul2", ((),), "f29& r0, const f29& a0, const f29& b0, const f29& c0, const f29& d0"),
+    (("sqr",), "sqr_s3", (("e", "e", "e"),), "f29& r0, const f29& a0, const f29& s00, const f29& s01, const f29& s02"),
     #   sqr_sqr_s2s2: r0 = a0^2 - s00 - s01, r1 = a1^2 - s10 - s11  (P-256 jdbl: X3, Z3)
     #   sqr_mul_s2s2: r0 = a0^2 - s00 - s01, r1 = a1 b1 - s10 - s11 (jmadd: Z3, Y3)
     (("sqr", "sqr"), "sqr_sqr_s2s2", (("e", "e"), ("e", "e")),
