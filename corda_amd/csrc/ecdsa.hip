@@ -470,14 +470,19 @@ CDEV void jmadd(jpt& r, const jpt& p, const f29& x2, const f29& y2) {
 }
 
 // ---- G tables: entry k = [k]G affine (Montgomery, canonical) ---------------
-// Booth windows of kGBits over the fixed base: 16-bit digits (|d| <= 2^15)
-// cut the ladder's G additions from 32 to 16 (P-256) and from 34 to 18
-// (secp256k1's two 129-bit halves) for tables of 2^15 + 1 affine entries
-// (2.6 MB each, L2/MALL-resident; 12-bit windows measured 2.2%
-// slower, profiles/r02_c3_field_ab.json); the window is a multiple of the 4-bit
-// Q window so both share the doublings. Tables [0, kGEntries) = [k]G and, for
+// Booth windows of kGBits over the fixed base: 20-bit digits (|d| <= 2^19)
+// cut the ladder's G additions from 32 to 13 (P-256) and from 34 to 14
+// (secp256k1's two 129-bit halves) for tables of 2^19 + 1 affine entries
+// (42 MB each, gathered from MALL; 12-bit windows measured 2.2% slower than
+// 16-bit ones, profiles/r02_c3_field_ab.json, and 20-bit ones +0.9% on C3,
+// profiles/r03_ec_g20_ab/); the window is a multiple of the 4-bit Q window so
+// both share the doublings. Tables [0, kGEntries) = [k]G and, for
 // secp256k1, [kGEntries, 2 kGEntries) = [k](lambda G) = (beta x, y).
-static constexpr int kGBits = 16;
+#ifndef EC_G_BITS
+#define EC_G_BITS 20
+#endif
+static constexpr int kGBits = EC_G_BITS;
+static_assert(kGBits % 4 == 0, "G windows must share the 4-bit Q windows' doublings");
 static constexpr int kGEntries = (1 << (kGBits - 1)) + 1;
 static constexpr int kGEntryWords = 20;  // x[9], y[9], 2 pad: five 16-B loads
 static constexpr int kGTables = 2;
