@@ -13,8 +13,13 @@ Other workloads (`--workload`), same contract, used for profiling the other rows
       (5 leaves, 1-3 Ed25519 signers): leaf SHA-256 + Merkle id + signatures
       + per-tx reduce (K3/K4/K1/K5); 10^7 / 8 txs per GPU by default.
 
-Contract: `python bench.py --gpus N --steps K --warmup W` (N > 1 under
-torch.distributed.run, one rank per GPU); rank 0 prints ONE JSON line.
+Contract: `python bench.py --gpus N --steps K --warmup W`; rank 0 prints ONE
+JSON line. N > 1 runs one rank per GPU: under torch.distributed.run (WORLD_SIZE
+set, and it must equal N), or -- when WORLD_SIZE is unset -- bench.py starts
+the N ranks itself as a child `torch.distributed.run` before anything touches
+the GPU, relays rank 0's line and exits non-zero if any rank fails. Every rank
+binds its host threads to its GPU's NUMA node before HIP starts
+(corda_amd/numa.py) and records the node in `config`.
 Weak scaling: every rank verifies its own batch; value = all ranks'
 verifications / max-over-ranks wall time of the K timed steps. C5 also has a
 strong-scaling mode, `--global-log2 G` (a fixed 2^28 stream split
@@ -68,15 +73,20 @@ def _cgroup_cpus():
         return None
 
 
+_NUMA = {}  # this rank's NUMA binding (corda_amd.numa.bind_rank), set in main()
+
+
 def _cores():
     """Host threads for the CPU legs: every CPU this process may run on
     (sched_getaffinity), capped by the cgroup CPU quota when one is set (more
-    threads than the quota only time-slice), shared evenly by the ranks."""
+    threads than the quota only time-slice), shared evenly by the ranks that
+    share those CPUs (the ranks bound to the same NUMA node, else all local ranks)."""
     n = len(os.sched_getaffinity(0))
     q = _cgroup_cpus()
     if q:
         n = min(n, q)
-    return max(1, n // int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    share = _NUMA.get("ranks_on_node") or int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    return max(1, n // share)
 
 
 def _cpu_info():
@@ -459,7 +469,9 @@ class C5:
     def __init__(self, eng, device, stream, rank, args):
         import torch
         from corda_amd.corpus import make_c2_corpus, make_c3_corpus
-        self.torch, self.eng = torch, eng
+        self.torch, self.eng, self.device = torch, eng, device
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.verdict = None  # built per step when N > 1 (the all-gather operand)
         n = 1 << args.batch_log2
         n_ec = n // 5  # 80% Ed25519 / 10% P-256 / 10% secp256k1
         n_ed = n - n_ec
@@ -500,6 +512,17 @@ class C5:
     def step(self):
         for _ in range(self.passes):
             self.eng.stream_verify(self.ed, self.ec)
+        if self.world > 1:
+            self.verdict = self._verdict_words()
+
+    def _verdict_words(self):
+        """The rank's verdict mask (bit i = lane i OK, Ed25519 lanes then ECDSA lanes)
+        as device words, the operand of the step's RCCL all-gather: the
+        drain leaves its statuses in pinned host memory, so they go H2D once and are
+        packed on the GPU (~1 ms of a ~170 ms step)."""
+        t = self.torch
+        st = t.cat([self.ed[3], self.ec[6]]).to(self.device, non_blocking=True)
+        return _pack_verdict(st)
 
     def check(self):
         t = self.torch
@@ -720,7 +743,126 @@ class C4H(C4):
         return C4.cpu_baseline(self, sample)
 
 
-WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c4": C4, "c5": C5, "c2h": C2H, "c3h": C3H, "c4h": C4H}
+def _pack_verdict(status):
+    """uint8 statuses (length a multiple of 64) -> int64 verdict words, bit i = (status[i] == 0)."""
+    import torch
+    ok = (status == 0).view(-1, 64).to(torch.int64)
+    return (ok << torch.arange(64, device=status.device, dtype=torch.int64)).sum(dim=1)
+
+
+class Stub:
+    """CPU-only stand-in for the multi-process launcher tests (`--workload stub`,
+    gloo, no GPU, no library): the same main() -- launcher, NUMA record, barrier
+    + max-over-ranks timing, verdict all-gather -- around a trivial step (SHA-256
+    of a 64 KiB buffer) over a seeded status vector."""
+    kernel = "stub (CPU, no kernel)"
+    pmc = None
+    host_timed = True
+
+    def __init__(self, eng, device, stream, rank, args):
+        import hashlib
+        import torch
+        self.hashlib, self.torch = hashlib, torch
+        if os.environ.get("CORDA_BENCH_STUB_FAIL_RANK") == str(rank):  # launcher test: a rank that dies
+            raise SystemExit("stub: rank %d fails on request" % rank)
+        self.n = n = 1 << min(args.batch_log2, 16)
+        rng = np.random.default_rng(0xC0DA0000 + rank)
+        self.status = torch.from_numpy((rng.random(n) < 0.01).astype(np.uint8))
+        self.verdict = _pack_verdict(self.status)
+        self.buf = rng.bytes(1 << 16)
+        self.units = n
+        self.macs = 0
+        self.workload = "stub: launcher test, %d seeded lanes per rank, no GPU work" % n
+        self.data = "synthetic: seeded statuses (numpy), CPU only"
+        self.config = {"batch_per_gpu": n}
+
+    def step(self):
+        self.hashlib.sha256(self.buf).digest()
+
+    def check(self):
+        return {"mismatches_vs_construction": 0, "lanes": self.n, "accepted": int((self.status == 0).sum())}
+
+    def cpu_baseline(self, sample):
+        return {"value": None, "unit": "verifications/s", "cores": _cores(), "kind": "port",
+                "sample": "stub workload: no CPU baseline"}
+
+
+WORKLOADS = {"c1": C1, "c2": C2, "c3": C3, "c4": C4, "c5": C5, "c2h": C2H, "c3h": C3H, "c4h": C4H, "stub": Stub}
+
+
+def _launch(n, argv):
+    """Start N ranks as a child torch.distributed.run (this process has not touched
+    the GPU, and never execs: the ranks are children), relay rank 0's JSON line,
+    and return non-zero if any rank failed or the line is missing."""
+    import signal
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + list(argv)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1, env=dict(os.environ, CORDA_BENCH_CHILD="1"))
+    prev = signal.signal(signal.SIGTERM, lambda *_: p.send_signal(signal.SIGTERM))
+    lines = []
+    try:
+        for line in p.stdout:
+            if line.startswith("{") and '"metric"' in line:
+                lines.append(line.strip())
+            else:
+                sys.stderr.write(line)
+        rc = p.wait()
+    except BaseException:
+        p.terminate()
+        p.wait()
+        raise
+    finally:
+        signal.signal(signal.SIGTERM, prev)
+    if rc != 0:
+        print("bench.py: a rank failed (torch.distributed.run exit %d)" % rc, file=sys.stderr)
+        return rc if rc > 0 else 1
+    if len(lines) != 1:
+        print("bench.py: expected one JSON line from rank 0, got %d" % len(lines), file=sys.stderr)
+        return 3
+    print(lines[0], flush=True)
+    return 0
+
+
+def _clock_under_load(device_index, run_step, sync, ms_per_step):
+    """Shader clock while the workload runs: one extra, UNTIMED step with the
+    libcordaprobe.so sampler resident beside it (8 one-wave workgroups, one per
+    XCD, stamping s_memtime / s_memrealtime; corda_amd/csrc/clock_probe.hip).
+    Returns the median per-interval clock and its spread."""
+    import ctypes
+    so = os.path.join(ROOT, "corda_amd", "libcordaprobe.so")
+    if not os.path.exists(so):
+        return {"error": "libcordaprobe.so not built"}
+    lib = ctypes.CDLL(so)
+    lib.cordaprobe_clock_start.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.POINTER(ctypes.c_void_p)]
+    lib.cordaprobe_clock_finish.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_uint32,
+                                            ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double)]
+    nblk, nsmp = 8, 65
+    window = max(5.0, 0.7 * ms_per_step)  # inside the step: the sampler must not outlive the workload
+    h = ctypes.c_void_p()
+    rc = lib.cordaprobe_clock_start(device_index, window, nblk, nsmp, ctypes.byref(h))
+    if rc not in (0, -2):
+        return {"error": "cordaprobe_clock_start rc %d" % rc}
+    run_step()
+    sync()
+    buf = (ctypes.c_double * (nblk * nsmp))()
+    m = ctypes.c_uint32()
+    mhz = ctypes.c_double()
+    rc2 = lib.cordaprobe_clock_finish(h, buf, nblk * nsmp, ctypes.byref(m), ctypes.byref(mhz))
+    if rc != 0 or rc2 != 0:
+        return {"error": "sampler not resident before the step (rc %d) / finish rc %d" % (rc, rc2)}
+    v = np.sort(np.array(buf[:m.value]))
+    if v.size == 0:
+        return {"error": "no samples"}
+    return {"clock_ghz": float(np.median(v)), "clock_ghz_p10": float(np.percentile(v, 10)),
+            "clock_ghz_p90": float(np.percentile(v, 90)), "samples": int(v.size), "window_ms": window,
+            "realtime_mhz_check": mhz.value,
+            "method": "s_memtime/s_memrealtime x 100 MHz per interval, 8 one-wave workgroups (one per XCD) "
+                      "resident beside one extra untimed step of this workload; median over intervals"}
 
 
 def main():
@@ -733,39 +875,78 @@ def main():
     ap.add_argument("--c4-txs", type=int, default=10_000_000 // 8)
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock sampling step")
     ap.add_argument("--global-log2", type=int, default=None,
                     help="C5 only: strong scaling over a fixed 2^G global batch (SURVEY 8d C5: G = 28)")
     args = ap.parse_args()
     if args.global_log2 and args.workload != "c5":
         ap.error("--global-log2 applies to --workload c5")
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
     if args.batch_log2 is None:
         args.batch_log2 = 20 if args.workload == "c1" else 24
+
+    # --gpus N: one rank per GPU. Without a launcher's WORLD_SIZE, start the ranks
+    # here (nothing has touched the GPU yet); under one, the two must agree.
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(_launch(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d" % (os.environ["WORLD_SIZE"], args.gpus), file=sys.stderr)
+        sys.exit(2)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    stub = args.workload == "stub"
+
+    # host threads next to the GPU, before HIP starts its own threads (they inherit it)
+    from corda_amd.numa import bind_rank, numa_of_gpu
+    _NUMA.update(bind_rank(local_rank, apply=not stub))
+    if _NUMA.get("cpus_bound"):
+        nodes = [numa_of_gpu(r) for r in range(local_world)]
+        _NUMA["ranks_on_node"] = max(1, sum(1 for x in nodes if x and x["numa_node"] == _NUMA["numa_node"]))
 
     import torch
     import torch.distributed as dist
     from corda_amd.dist import gather_verdicts, max_over_ranks
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=device)
+    if stub:
+        device = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+        sync = lambda: None  # noqa: E731
+    else:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl", device_id=device)
+        sync = lambda: torch.cuda.synchronize(device)  # noqa: E731
+        try:  # the NUMA choice was made from sysfs before HIP init: confirm it names this device
+            from corda_amd.numa import location_matches
+            pr = torch.cuda.get_device_properties(local_rank)
+            _NUMA["numa_check"] = location_matches(_NUMA, int(getattr(pr, "pci_bus_id", -1)),
+                                                   int(getattr(pr, "pci_device_id", -1)),
+                                                   int(getattr(pr, "pci_domain_id", 0)))
+        except Exception as e:  # noqa: BLE001 - diagnostic only
+            _NUMA["numa_check"] = "unavailable: %s" % type(e).__name__
 
-    from corda_amd.engine import Engine
-
-    eng = Engine(1 << local_rank)
-    # one explicit stream carries corpus generation, the kernels and the timing
-    # events, so the events bracket exactly the launches they time
-    stream = torch.cuda.Stream(device)
-    torch.cuda.set_stream(stream)
+    if stub:
+        eng, stream = None, None
+    else:
+        from corda_amd.engine import Engine
+        eng = Engine(1 << local_rank)
+        # one explicit stream carries corpus generation, the kernels and the timing
+        # events, so the events bracket exactly the launches they time
+        stream = torch.cuda.Stream(device)
+        torch.cuda.set_stream(stream)
     t_gen = time.perf_counter()
     wl = WORKLOADS[args.workload](eng, device, stream, rank, args)
-    torch.cuda.synchronize(device)
+    sync()
     t_gen = time.perf_counter() - t_gen
-    verdict = getattr(wl, "verdict", None)
+    host_timed = getattr(wl, "host_timed", False)
 
     def step(ev_s=None, ev_e=None):
         if ev_s is not None:
@@ -773,44 +954,63 @@ def main():
         wl.step()
         if ev_e is not None:
             ev_e.record(stream)
+        verdict = getattr(wl, "verdict", None)
         if world > 1 and verdict is not None:
             gather_verdicts(verdict, world)  # the only data-path collective (RCCL all-gather)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(device)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(device)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    sync()
+    evs = [(None, None)] * args.steps if host_timed else \
+        [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(*evs[k])
-    torch.cuda.synchronize(device)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    sync()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    if getattr(wl, "host_timed", False):
+    if host_timed:
         kernel_ms = elapsed * 1e3 / args.steps  # synchronous host-buffer drain: the wall clock is the measure
+    else:
+        kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    # after the timed region: the verdict all-gather reassembles every rank's mask
+    gather = None
+    verdict = getattr(wl, "verdict", None)
+    if world > 1 and verdict is not None:
+        g = gather_verdicts(verdict, world)
+        nv = verdict.numel()
+        gather = bool(torch.equal(g[rank * nv:(rank + 1) * nv], verdict))
+    # the shader clock this box holds under this workload (one more, untimed step)
+    clock = None
+    if not stub and not args.no_clock:
+        clock = _clock_under_load(local_rank, step, sync, elapsed * 1e3 / args.steps)
     chk = wl.check()
     elapsed = max_over_ranks(elapsed, device)
     for key in ("mismatches_vs_construction", "mismatches_vs_oracle_open_lanes"):
         if key in chk:
             chk[key] = int(max_over_ranks(float(chk[key]), device))
+    if gather is not None:
+        chk["verdict_allgather_ok_all_ranks"] = max_over_ranks(0.0 if gather else 1.0, device) == 0.0
+    numa_nodes = _gather_ints(_NUMA.get("numa_node"), world, device)
 
     if rank == 0:
         value = world * wl.units * args.steps / elapsed
         achieved = wl.macs * wl.units / (kernel_ms * 1e-3) / 1e12
         # HBM bytes per step from the committed PMC passes (tools/gpu_pmc.sh:
         # FETCH_SIZE and WRITE_SIZE in separate passes), scaled to this step
-        traffic = None
+        traffic, traffic_src = None, None
         pmc_file = os.path.join(ROOT, "profiles", wl.pmc) if wl.pmc else None
         if pmc_file and os.path.exists(pmc_file):
             with open(pmc_file) as f:
                 per_unit = json.load(f).get("hbm_bytes_per_unit")
             traffic = per_unit * wl.units if per_unit else None
+            traffic_src = "profiles/%s (bytes per unit x units per step)" % wl.pmc
         out = {
             "metric": METRIC,
             "value": value,
@@ -825,26 +1025,51 @@ def main():
             "dtype": "u32",
             "data": wl.data,
             "config": dict({"workload": wl.workload,
-                            "parallelism": "dp%d (independent shards, RCCL all-gather of verdict masks)" % world},
+                            "parallelism": "dp%d (independent shards, RCCL all-gather of verdict masks)" % world,
+                            "launcher": "torch.distributed.run (%s)" % ("bench.py child" if
+                                                                        os.environ.get("CORDA_BENCH_CHILD") else
+                                                                        "external") if world > 1 else "in-process",
+                            "numa_node": _NUMA.get("numa_node"), "numa_nodes_by_rank": numa_nodes,
+                            "numa": {k: v for k, v in _NUMA.items() if k != "numa_node"}},
                            **wl.config),
             "roofline": {"bound": "valu", "achieved": achieved, "peak": INT_MAC_PEAK_T,
                          "unit": "Tlimb-MAC/s", "frac": achieved / INT_MAC_PEAK_T, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": wl.kernel, "kernel_ms": kernel_ms,
                          "work_per_unit": "%d limb-MACs per verification (SURVEY §8d)" % wl.macs},
             "int_alu_peak_frac": achieved / INT_MAC_PEAK_T,
             "verdict_check": chk,
             "corpus_gen_s": t_gen,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if clock is not None:
+            out["clock"] = clock
+            if clock.get("clock_ghz"):
+                out["clock_ghz"] = clock["clock_ghz"]
+                # per-GPU verifications per 10^6 shader cycles: comparable across boxes
+                out["verifs_per_mclk"] = value / world / (clock["clock_ghz"] * 1e3)
+        if world == 1 and not args.no_cpu_baseline and not stub:
             # bounded samples sized for ~10 s of 16-thread CPU work each (C1: its whole 2^20 set)
             sample = args.cpu_sample or {"c1": 1 << 20, "c2": 1 << 22, "c3": 1 << 20, "c4": 1 << 20, "c5": 1 << 21,
                                          "c2h": 1 << 22, "c3h": 1 << 20, "c4h": 1 << 20}[args.workload]
             out["cpu_baseline"] = wl.cpu_baseline(min(sample, wl.units))
             out["cpu_baseline"].update(_cpu_info())
         print(json.dumps(out), flush=True)
-    eng.close()
+    if eng is not None:
+        eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _gather_ints(x, world, device):
+    """Every rank's small int (None -> -1) as a list, for the rank-0 line."""
+    if world == 1:
+        return [x]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([-1 if x is None else int(x)], dtype=torch.int64, device=device)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [int(v[0]) for v in out]
 
 
 if __name__ == "__main__":

@@ -38,7 +38,7 @@ ERR_BUFFER_TOO_SMALL = -8
 # cordahip_kryo_item kinds (CORDAHIP_KRYO_*)
 KRYO_KINDS = {"raw": 0, "char": 1, "short": 2, "int": 3, "long": 4, "byte": 5, "boolean": 6, "float": 7,
               "double": 8, "String": 9, "ed25519_key": 10, "public_key": 11, "kotlin_object": 12, "party": 13,
-              "issue_command": 14}
+              "issue_command": 14, "cash_state": 15}
 ABI_VERSION = 2
 FLAG_IS_VALID = 1  # CORDAHIP_FLAG_IS_VALID: Crypto.isValid semantics (no emptiness checks)
 TX_NO_LEAVES, TX_NO_SIGNATURES, TX_BAD_TREE = 6, 7, 8
@@ -181,6 +181,26 @@ def shard_range(n: int, nshards: int, shard: int, align: int = 64):
     return lo.value, hi.value
 
 
+def _pack_party(p):
+    """(X.500 name DER or b"" for an AnonymousParty, key bytes, key registration id)"""
+    name, key, key_class = p
+    return (int(key_class).to_bytes(2, "little") + len(key).to_bytes(2, "little") + bytes(key)
+            + len(name).to_bytes(2, "little") + bytes(name))
+
+
+def pack_cash_state(d):
+    """The CORDAHIP_KRYO_CASH_STATE payload (include/cordahip.h) of a dict with keys
+    issuer / owner / notary (parties as _pack_party takes them), reference (bytes),
+    currency (ISO code), digits (its fraction digits), legal_ref (32 bytes),
+    encumbrance (None or an int); the quantity goes in the item's value."""
+    enc = d.get("encumbrance")
+    code = d["currency"].encode("ascii")
+    return (_pack_party(d["issuer"]) + bytes([len(d["reference"])]) + bytes(d["reference"]) + _pack_party(d["owner"])
+            + _pack_party(d["notary"]) + bytes([len(code)]) + code + int(d["digits"]).to_bytes(1, "little", signed=True)
+            + bytes(d["legal_ref"]) + bytes([0 if enc is None else 1])
+            + (0 if enc is None else int(enc)).to_bytes(4, "little", signed=True))
+
+
 def kryo_encode(items):
     """Leaf preimages of transaction components (cordahip_kryo_encode; host only, no
     device). items: (kind, value, class_id) with kind a KRYO_KINDS key; value: bytes
@@ -211,6 +231,10 @@ def kryo_encode(items):
                 int(kc).to_bytes(2, "little") + len(k).to_bytes(2, "little") + bytes(k) for kc, k in keys)
             it.len = len(b)
             it.value = nonce
+        elif kind == "cash_state":  # value = a dict (pack_cash_state); class_id = X500Name's id
+            b = pack_cash_state(value)
+            it.len = len(b)
+            it.value = int(value["quantity"])
         else:
             b = None
             it.value = ord(value) if (kind == "char" and isinstance(value, str)) else int(value)

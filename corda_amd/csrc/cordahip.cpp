@@ -456,6 +456,28 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
     sh[i].done = sh[i].lo;
   }
   std::vector<std::thread> waiters;
+  // Every exit joins the waiters and frees the slice events, exceptions included
+  // (std::bad_alloc from the pipeline's host vectors, std::system_error from a
+  // thread start): a joinable std::thread destroyed by unwinding would call
+  // std::terminate in the caller's process (the JVM).
+  struct Cleanup {
+    std::vector<std::thread>& waiters;
+    std::vector<Shard>& sh;
+    cordahip_ctx* ctx;
+    ~Cleanup() {
+      for (auto& t : waiters)
+        if (t.joinable()) t.join();
+      for (uint64_t i = 0; i < sh.size(); i++) {
+        (void)hipSetDevice(ctx->devs[i]->id);
+        for (auto* v : {&sh[i].ev, &sh[i].cev})
+          for (hipEvent_t& e : *v)
+            if (e) {
+              (void)hipEventDestroy(e);
+              e = nullptr;
+            }
+      }
+    }
+  } cleanup{waiters, sh, ctx};
   for (uint64_t i = 0; i < nd; i++) {
     Shard& S = sh[i];
     if (S.lo >= S.hi) continue;
@@ -526,15 +548,15 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
     // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
     cordahip_sig_batch sb{nsig, b->scheme, b->key, b->key_off, b->sig, b->sig_off, b->tx.txid, nullptr,
                           b->sig_status, nullptr, 0u};
-    rc = sig_verify_msgs(ctx, &sb, mv);
+    try {
+      rc = sig_verify_msgs(ctx, &sb, mv);
+    } catch (const std::bad_alloc&) {
+      rc = CORDAHIP_ERR_OUT_OF_MEMORY;
+    } catch (...) {
+      rc = CORDAHIP_ERR_HIP;
+    }
   }
   for (auto& t : waiters) t.join();
-  for (uint64_t i = 0; i < nd; i++) {
-    (void)hipSetDevice(ctx->devs[i]->id);
-    for (auto* v : {&sh[i].ev, &sh[i].cev})
-      for (hipEvent_t e : *v)
-        if (e) (void)hipEventDestroy(e);
-  }
   const double t_ids = tracing() ? now_ms() : 0;
   if (ids_rc != CORDAHIP_SUCCESS) return ids_rc;
   if (rc != CORDAHIP_SUCCESS) return rc;
@@ -790,6 +812,19 @@ void free_device(Device& d) {
 
 }  // namespace
 
+// Synchronous entry points run host code that allocates (staging vectors,
+// worker threads): no C++ exception may cross the C ABI into the JVM.
+template <class F>
+int guarded(F&& f) noexcept {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return CORDAHIP_ERR_OUT_OF_MEMORY;
+  } catch (...) {
+    return CORDAHIP_ERR_HIP;
+  }
+}
+
 extern "C" {
 
 uint32_t cordahip_abi_version(void) { return CORDAHIP_ABI_VERSION; }
@@ -815,8 +850,15 @@ void cordahip_shard_range(uint64_t n, uint32_t nshards, uint32_t shard, uint64_t
   if (hi) *hi = b;
 }
 
+static int init_impl(uint32_t device_mask, cordahip_ctx** out);
+
 int cordahip_init(uint32_t device_mask, cordahip_ctx** out) {
   if (!out) return CORDAHIP_ERR_INVALID_ARG;
+  *out = nullptr;
+  return guarded([&] { return init_impl(device_mask, out); });
+}
+
+static int init_impl(uint32_t device_mask, cordahip_ctx** out) {
   *out = nullptr;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return CORDAHIP_ERR_NO_DEVICE;
@@ -904,35 +946,43 @@ int cordahip_free_pinned(cordahip_ctx* ctx, void* host) {
 
 int cordahip_sig_verify(cordahip_ctx* ctx, const cordahip_sig_batch* batch) {
   if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
-  return sig_verify_impl(ctx, batch);
+  return guarded([&] { return sig_verify_impl(ctx, batch); });
 }
 
 int cordahip_sig_submit(cordahip_ctx* ctx, const cordahip_sig_batch* batch, uint64_t* ticket) {
   if (!ctx || !batch || !ticket) return CORDAHIP_ERR_INVALID_ARG;
   const cordahip_sig_batch copy = *batch;  // descriptor by value; buffers stay caller-owned
-  *ticket = submit_job(ctx, [ctx, copy] { return sig_verify_impl(ctx, &copy); });
-  return CORDAHIP_SUCCESS;
+  return guarded([&] {
+    *ticket = submit_job(ctx, [ctx, copy] { return sig_verify_impl(ctx, &copy); });
+    return CORDAHIP_SUCCESS;
+  });
 }
 
 int cordahip_tx_submit(cordahip_ctx* ctx, const cordahip_signed_tx_batch* batch, uint64_t* ticket) {
   if (!ctx || !batch || !ticket) return CORDAHIP_ERR_INVALID_ARG;
   const cordahip_signed_tx_batch copy = *batch;
-  *ticket = submit_job(ctx, [ctx, copy] { return signed_tx_impl(ctx, &copy); });
-  return CORDAHIP_SUCCESS;
+  return guarded([&] {
+    *ticket = submit_job(ctx, [ctx, copy] { return signed_tx_impl(ctx, &copy); });
+    return CORDAHIP_SUCCESS;
+  });
 }
 
 int cordahip_txid_submit(cordahip_ctx* ctx, const cordahip_txid_batch* batch, uint64_t* ticket) {
   if (!ctx || !batch || !ticket) return CORDAHIP_ERR_INVALID_ARG;
   const cordahip_txid_batch copy = *batch;
-  *ticket = submit_job(ctx, [ctx, copy] { return tx_ids_impl(ctx, &copy); });
-  return CORDAHIP_SUCCESS;
+  return guarded([&] {
+    *ticket = submit_job(ctx, [ctx, copy] { return tx_ids_impl(ctx, &copy); });
+    return CORDAHIP_SUCCESS;
+  });
 }
 
 int cordahip_filtered_tx_submit(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch, uint64_t* ticket) {
   if (!ctx || !batch || !ticket) return CORDAHIP_ERR_INVALID_ARG;
   const cordahip_filtered_tx_batch copy = *batch;
-  *ticket = submit_job(ctx, [ctx, copy] { return filtered_tx_impl(ctx, &copy); });
-  return CORDAHIP_SUCCESS;
+  return guarded([&] {
+    *ticket = submit_job(ctx, [ctx, copy] { return filtered_tx_impl(ctx, &copy); });
+    return CORDAHIP_SUCCESS;
+  });
 }
 
 int cordahip_wait(cordahip_ctx* ctx, uint64_t ticket, int64_t timeout_ns) {
@@ -1022,23 +1072,29 @@ double cordahip_last_kernel_ms(cordahip_ctx* ctx, int device) {
   if (hipEventSynchronize(tc.b) != hipSuccess) return -1.0;
   float ms = -1.f;
   if (hipEventElapsedTime(&ms, tc.a, tc.b) != hipSuccess) return -1.0;
+  {
+    // a concurrent timed_begin may have re-recorded the slot's events between
+    // the check above and the read: then ms mixes two calls, so report none
+    std::lock_guard<std::mutex> g(d->tmu);
+    if (tc.gen != it->second.second) return -1.0;
+  }
   return ms;
 }
 
 int cordahip_ed25519_verify_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                                  uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict) {
   if (!ctx || (n && (!keys || !sigs || !status || (msg_len && !msgs)))) return CORDAHIP_ERR_INVALID_ARG;
-  return ed25519_dense_host(ctx, keys, sigs, msgs, msg_len, n, status, verdict);
+  return guarded([&] { return ed25519_dense_host(ctx, keys, sigs, msgs, msg_len, n, status, verdict); });
 }
 
 int cordahip_filtered_tx_verify(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch) {
   if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
-  return filtered_tx_impl(ctx, batch);
+  return guarded([&] { return filtered_tx_impl(ctx, batch); });
 }
 
 int cordahip_stream_verify(cordahip_ctx* ctx, const cordahip_stream_batch* batch) {
   if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
-  return stream_verify_impl(ctx, batch);
+  return guarded([&] { return stream_verify_impl(ctx, batch); });
 }
 
 int cordahip_ed25519_sign_device(cordahip_ctx* ctx, int device, const void* d_seeds, const void* d_msgs,
@@ -1068,12 +1124,12 @@ int cordahip_ecdsa_sign_device(cordahip_ctx* ctx, int device, const void* d_sche
 
 int cordahip_tx_ids(cordahip_ctx* ctx, const cordahip_txid_batch* batch) {
   if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
-  return tx_ids_impl(ctx, batch);
+  return guarded([&] { return tx_ids_impl(ctx, batch); });
 }
 
 int cordahip_signed_tx_verify(cordahip_ctx* ctx, const cordahip_signed_tx_batch* batch) {
   if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
-  return signed_tx_impl(ctx, batch);
+  return guarded([&] { return signed_tx_impl(ctx, batch); });
 }
 
 int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, const void* d_leaf_bytes,

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <unordered_map>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -322,6 +323,11 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
         P.ed.clear();
         P.ec = P.ec_bytes = 0;
         P.too_long = false;
+        // length -> group: the previous lane's group first (batches are mostly
+        // one message length), a hash map once a piece has many lengths, so a
+        // batch of adversarially varied lengths stays linear
+        std::unordered_map<uint64_t, uint32_t> gidx;
+        size_t last = 0;
         for (uint64_t r = q * kGrain; r < std::min(m, (q + 1) * kGrain); r++) {
           uint64_t mlen = 0;
           uint16_t c = classify(b, mv, a + r, mlen);
@@ -330,9 +336,23 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
             P.ec_bytes += mlen;
           } else if (c == kEdBase) {
             if (mlen > 0xffffffffull) P.too_long = true;
-            size_t j = 0;
-            while (j < P.ed.size() && P.ed[j].first != mlen) j++;
-            if (j == P.ed.size()) P.ed.push_back({mlen, 0});
+            size_t j = last;
+            if (j >= P.ed.size() || P.ed[j].first != mlen) {
+              if (P.ed.size() <= 8) {
+                j = 0;
+                while (j < P.ed.size() && P.ed[j].first != mlen) j++;
+              } else {
+                if (gidx.empty())
+                  for (size_t u = 0; u < P.ed.size(); u++) gidx.emplace(P.ed[u].first, (uint32_t)u);
+                auto it = gidx.find(mlen);
+                j = it == gidx.end() ? P.ed.size() : it->second;
+              }
+              if (j == P.ed.size()) {
+                P.ed.push_back({mlen, 0});
+                if (!gidx.empty()) gidx.emplace(mlen, (uint32_t)j);
+              }
+            }
+            last = j;
             P.ed[j].second++;
             c = (uint16_t)(kEdBase + j);
           }
@@ -360,13 +380,18 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
       for (size_t j = 0; j < P.ed.size(); j++)
         P.ed_global[j] = (uint32_t)(std::lower_bound(lens.begin(), lens.end(), P.ed[j].first) - lens.begin());
     }
-    for (size_t gi = 0; gi < ng; gi++) {  // rows of group gi, piece by piece
+    // rows of group gi, piece by piece: prow[q][gi] = lanes of group gi in
+    // pieces < q (then offset by the group's first row); O(pieces x groups)
+    for (uint64_t q = 0; q + 1 < np; q++)
+      for (size_t j = 0; j < pieces[q].ed.size(); j++) prow[q + 1][pieces[q].ed_global[j]] = pieces[q].ed[j].second;
+    for (size_t gi = 0; gi < ng; gi++) {
       uint64_t r = grow[gi];
       for (uint64_t q = 0; q < np; q++) {
+        r += prow[q][gi];  // lanes of piece q - 1
         prow[q][gi] = r;
-        for (size_t j = 0; j < pieces[q].ed.size(); j++)
-          if (pieces[q].ed_global[j] == gi) r += pieces[q].ed[j].second;
       }
+      for (size_t j = 0; j < pieces[np - 1].ed.size(); j++)
+        if (pieces[np - 1].ed_global[j] == gi) r += pieces[np - 1].ed[j].second;
       grow[gi + 1] = r;
       gmsg[gi + 1] = (gmsg[gi] + (r - grow[gi]) * lens[gi] + 15) / 16 * 16;
     }

@@ -321,9 +321,29 @@ int cordahip_filtered_tx_submit(cordahip_ctx* ctx, const cordahip_filtered_tx_ba
  *                  name, u8 key count, per key u16 LE registration id, u16 LE
  *                  length, key bytes; class_id = java.util.Arrays$ArrayList's
  *                  registration id (ArraysAsListSerializer); value = the nonce
+ *   CASH_STATE     TransactionState<Cash.State> -- the output of a cash issue
+ *                  (Cash.generateIssue, Cash.kt:166-167; Structures.kt:95-117,
+ *                  132,268; Cash.kt:35,62,92-103; Amount.kt:37): TransactionState
+ *                  (data, encumbrance, notary) > Cash.State (amount, contract =
+ *                  CASH_PROGRAM_ID, exitKeys = {owner key, issuer key},
+ *                  owner, participants = [owner]) > Amount(quantity,
+ *                  displayTokenSize = 10^-digits, Issued(PartyAndReference(
+ *                  issuer, reference), Currency)). data = issuer party, u8
+ *                  reference length, reference bytes, owner party, notary party,
+ *                  u8 currency-code length, the code (ASCII), i8 the currency's
+ *                  fraction digits, the 32-byte legalContractReference
+ *                  (SHA-256 of Cash's legal-prose URL), u8 flags (bit 0:
+ *                  encumbrance present), i32 LE encumbrance; a party = u16 LE key
+ *                  registration id, u16 LE key length, key bytes, u16 LE X.500
+ *                  name length, the name's DER (length 0 = AnonymousParty, e.g.
+ *                  CashIssueFlow's anonymised recipient; the notary must be a
+ *                  Party); class_id = X500Name's registration id; value = the
+ *                  quantity (pennies)
  * Field values go through OutputChunked (1024-byte chunks + a zero chunk) as
- * Kryo 4.0.0's CompatibleFieldSerializer writes them. PARTY / ISSUE_COMMAND are
- * restated from Kryo 4.0.0 / kryo-serializers 0.41 published sources: PARITY
+ * Kryo 4.0.0's CompatibleFieldSerializer writes them, nested serializers'
+ * flushes cutting the enclosing fields' chunks (kryo.cpp). PARTY / ISSUE_COMMAND
+ * / CASH_STATE are restated from Kryo 4.0.0 / kryo-serializers 0.41 published
+ * sources: PARITY
  * UNPINNED (no JVM here), except the Ed25519 key bytes inside them, which the
  * reference's own serialised keys pin (tests/golden/kryo_key_vectors.json).
  * class_id = kryo.getRegistration(cls).id on the node (registration order of
@@ -346,6 +366,7 @@ int cordahip_filtered_tx_submit(cordahip_ctx* ctx, const cordahip_filtered_tx_ba
 #define CORDAHIP_KRYO_KOTLIN_OBJECT 12
 #define CORDAHIP_KRYO_PARTY 13
 #define CORDAHIP_KRYO_ISSUE_COMMAND 14
+#define CORDAHIP_KRYO_CASH_STATE 15
 typedef struct {
   uint32_t kind;       /* CORDAHIP_KRYO_* */
   uint32_t class_id;   /* Kryo registration id (ED25519_KEY, PUBLIC_KEY) */

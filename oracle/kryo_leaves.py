@@ -23,12 +23,22 @@ Kryo's CompatibleFieldSerializer (the default serializer, EXTENDED cached field
 names: DefaultKryoCustomizer.kt:56-58) with OutputChunked field framing, and
 kryo-serializers 0.41's ArraysAsListSerializer (DefaultKryoCustomizer.kt:60).
 
+Object graphs (Party, the issue Command, TransactionState<Cash.State>) are
+written by a literal model of Kryo's buffered Output classes (class Output /
+OutputChunked below, method for method: require, writeBytes, flush,
+writeChunkSize, endChunks), so the framing of NESTED CompatibleFieldSerializers
+falls out of the same rules Kryo runs: an inner endChunks() flushes every
+enclosing OutputChunked (Output.flush() flushes its stream), cutting the
+enclosing field's chunk, and the inner 0 terminator opens a new one (ADVICE r03:
+an issue command's value field is [len A] A [01 00] [00], not one chunk).
+
 Pinning: the char leaves of PartialMerkleTreeTest.kt:22-25 are the derived fixture
 (tests/golden/merkle_vectors.json "ref_*"); the Ed25519 key leaf (class id 45 +
 writeBytesWithLength) is pinned by the reference's own serialised keys
 (tests/golden/kryo_key_vectors.json, samples/irs-demo/.../trade.json:3,25); every
-other kind -- Party, the issue Command -- is PARITY UNPINNED (no Kryo, no JVM
-here: the bytes follow the published format, unconfirmed).
+other kind -- Party, the issue Command, the cash TransactionState -- is PARITY
+UNPINNED (no Kryo, no JVM here: the bytes follow the published format,
+unconfirmed by any reference output).
 """
 import struct
 
@@ -96,54 +106,170 @@ def varlong_zigzag(x: int) -> bytes:
     return bytes(out)
 
 
-def chunked(data: bytes) -> bytes:
-    """OutputChunked(output, 1024) + endChunks(): <= 1024-byte chunks, each after
-    its varint length, then a zero-length chunk (CompatibleFieldSerializer's
-    per-field framing)."""
-    out = bytearray()
-    for p in range(0, len(data), 1024):
-        c = data[p:p + 1024]
-        out += varint(len(c)) + c
-    return bytes(out) + b"\x00"
+class Output:
+    """com.esotericsoftware.kryo.io.Output: a `capacity`-byte buffer over a stream.
+    The leaf's own Output (Kryo.kt:165-176: 64 KiB over a ByteArrayOutputStream)
+    flushes in order, so it is modelled unbounded (stream None)."""
+
+    def __init__(self, stream=None, capacity=None):
+        self.stream, self.capacity, self.buffer = stream, capacity, bytearray()
+
+    def require(self, required):
+        if self.capacity is None or self.capacity - len(self.buffer) >= required:
+            return
+        self.flush()
+
+    def write(self, value):  # Output.write(int) / writeByte
+        self.require(1)
+        self.buffer.append(value & 0xFF)
+
+    def write_atomic(self, data):  # writeVarInt / writeVarLong / fixed-width: require(n), then the bytes
+        self.require(len(data))
+        self.buffer += data
+
+    def write_bytes(self, data):  # Output.writeBytes: fill the buffer, flush, continue
+        data = bytes(data)
+        if self.capacity is None:
+            self.buffer += data
+            return
+        count, offset = len(data), 0
+        copy = min(self.capacity - len(self.buffer), count)
+        while True:
+            self.buffer += data[offset:offset + copy]
+            count -= copy
+            if count == 0:
+                return
+            offset += copy
+            copy = min(self.capacity, count)
+            self.require(copy)
+
+    def write_string(self, s):  # Output.writeString (Java String = UTF-16 code units)
+        units = s.encode("utf-16-le")
+        cu = [units[i] | (units[i + 1] << 8) for i in range(0, len(units), 2)]
+        n = len(cu)
+        if n == 0:
+            self.write(0x81)
+            return
+        if 1 < n < 64 and all(c <= 127 for c in cu):
+            self.write_bytes(bytes(cu))  # fits: one copy; else writeAscii_slow fills piecewise
+            self.buffer[-1] |= 0x80
+            return
+        self.write_atomic(utf8_length(n + 1))
+        i = 0
+        if self.capacity is None or self.capacity - len(self.buffer) >= n:
+            while i < n and cu[i] <= 127:
+                self.buffer.append(cu[i])
+                i += 1
+        while i < n:  # writeString_slow
+            if self.capacity is not None and len(self.buffer) == self.capacity:
+                self.require(min(self.capacity, n - i))
+            c = cu[i]
+            if c <= 0x7F:
+                self.buffer.append(c)
+            elif c > 0x7FF:
+                self.buffer.append(0xE0 | (c >> 12) & 0x0F)
+                self.require(2)
+                self.buffer += bytes([0x80 | (c >> 6) & 0x3F, 0x80 | c & 0x3F])
+            else:
+                self.buffer.append(0xC0 | (c >> 6) & 0x1F)
+                self.require(1)
+                self.buffer.append(0x80 | c & 0x3F)
+            i += 1
+
+    def flush(self):  # Output.flush: the buffer to the stream, then stream.flush()
+        if self.stream is None:
+            return
+        data = bytes(self.buffer)
+        self.stream.write_bytes(data)
+        self.stream.flush()
+        self.buffer.clear()
 
 
-def class_name(name_id: int, name: str) -> bytes:
-    """DefaultClassResolver.writeName: NAME + 2 (= 1), the graph's name id, the name."""
-    return varint(1) + varint(name_id) + write_string(name)
+class OutputChunked(Output):
+    """com.esotericsoftware.kryo.io.OutputChunked(stream, 1024)."""
+
+    def __init__(self, stream, size=1024):
+        super().__init__(stream, size)
+
+    def flush(self):
+        if len(self.buffer) > 0:
+            for b in varint(len(self.buffer)):  # writeChunkSize: stream.write(int) per byte
+                self.stream.write(b)
+            Output.flush(self)
+        Output.flush(self)
+
+    def end_chunks(self):
+        self.flush()
+        self.stream.write(0)  # the zero-length chunk
 
 
-def fields_header(names) -> bytes:
-    """CompatibleFieldSerializer's first write of a class in a graph: the field
-    count and the EXTENDED cached names ("DeclaringSimpleName.field"), sorted."""
-    names = sorted(names)
-    return varint(len(names)) + b"".join(write_string(n) for n in names)
+class Graph:
+    """One Kryo.writeClassAndObject object graph: DefaultClassResolver's name ids and
+    CompatibleFieldSerializer's header marks (graph context), both reset per leaf."""
+
+    def __init__(self):
+        self.name_ids, self.headers = {}, set()
+
+    @staticmethod
+    def write_class_id(out, reg_id):  # DefaultClassResolver.writeClass, registered
+        out.write_atomic(varint(reg_id + 2))
+
+    def write_class_name(self, out, name):  # DefaultClassResolver.writeName
+        out.write_atomic(varint(1))  # NAME + 2
+        if name in self.name_ids:
+            out.write_atomic(varint(self.name_ids[name]))
+            return
+        self.name_ids[name] = len(self.name_ids)
+        out.write_atomic(varint(self.name_ids[name]))
+        out.write_string(name)
+
+    def compatible_fields(self, out, cls, fields):
+        """CompatibleFieldSerializer.write: fields = [(EXTENDED name, writer(output))]."""
+        fields = sorted(fields, key=lambda f: f[0])
+        if cls not in self.headers:
+            self.headers.add(cls)
+            out.write_atomic(varint(len(fields)))
+            for name, _ in fields:
+                out.write_string(name)
+        chunked = OutputChunked(out, 1024)
+        for _, w in fields:
+            w(chunked)
+            chunked.end_chunks()
 
 
-def key_value(key_class: int, key: bytes) -> bytes:
-    """A key whose concrete class the field does not fix: class + writeBytesWithLength."""
-    return varint(key_class + 2) + varint(len(key)) + bytes(key)
+def _leaf(write) -> bytes:
+    out = Output()
+    out.write_bytes(HEADER)
+    write(out, Graph())
+    return bytes(out.buffer)
 
 
-def party_body(name_der: bytes, key: bytes, key_class: int, x500_class: int) -> bytes:
-    """net.corda.core.identity.Party (identity/Party.kt: name: X500Name,
-    AbstractParty.owningKey: PublicKey) through CompatibleFieldSerializer; the
-    name via X500NameSerializer (Kryo.kt:615-624: writeBytes(encoded))."""
-    return (class_name(0, "net.corda.core.identity.Party") + fields_header(["AbstractParty.owningKey", "Party.name"])
-            + chunked(key_value(key_class, key)) + chunked(varint(x500_class + 2) + bytes(name_der)))
+def write_key(out, key_class, key):
+    """A PublicKey of unknown concrete class: class id + writeBytesWithLength (Kryo.kt:305-308)."""
+    Graph.write_class_id(out, key_class)
+    out.write_atomic(varint(len(key)))
+    out.write_bytes(key)
 
 
-def issue_command_body(cls: str, nonce: int, keys, aal_class: int) -> bytes:
-    """Command(value = <cls>(nonce: Long), signers = Arrays.asList(PublicKey[]))
-    (Structures.kt:285, TransactionBuilder.kt:124, Cash.kt:148): fields sorted
-    Command.signers, Command.value; the list via ArraysAsListSerializer
-    (kryo-serializers 0.41: length, component class, elements); PublicKey and the
-    command class by implicit NAME registration (name ids 1, 2)."""
-    signers = (varint(aal_class + 2) + varint(len(keys)) + class_name(1, "java.security.PublicKey")
-               + b"".join(key_value(kc, k) for kc, k in keys))
-    simple = cls.replace("$", ".").rsplit(".", 1)[-1]
-    value = class_name(2, cls) + fields_header([simple + ".nonce"]) + chunked(varlong_zigzag(nonce))
-    return (class_name(0, "net.corda.core.contracts.Command") + fields_header(["Command.signers", "Command.value"])
-            + chunked(signers) + chunked(value))
+def write_party(out, g, party, x500_class, with_class=True):
+    """Party (name, owningKey) or, with an empty name, AnonymousParty(owningKey)
+    (identity/Party.kt, AnonymousParty.kt, AbstractParty.kt); the name through
+    X500NameSerializer (Kryo.kt:615-624: writeBytes(encoded))."""
+    name, key, key_class = party
+    cls = "net.corda.core.identity.Party" if name else "net.corda.core.identity.AnonymousParty"
+    if with_class:
+        g.write_class_name(out, cls)
+    fields = [("AbstractParty.owningKey", lambda o: write_key(o, key_class, key))]
+    if name:
+        fields.append(("Party.name", lambda o: (Graph.write_class_id(o, x500_class), o.write_bytes(name))))
+    g.compatible_fields(out, cls, fields)
+
+
+def write_opaque(out, g, cls, data):
+    """OpaqueBytes / SecureHash$SHA256: field OpaqueBytes.bytes, byte[] (final, accepts null)."""
+    g.write_class_name(out, cls)
+    g.compatible_fields(out, cls, [("OpaqueBytes.bytes",
+                                    lambda o: (o.write_atomic(varint(len(data) + 1)), o.write_bytes(data)))])
 
 
 def leaf(kind: str, value=None, class_id: int = 0) -> bytes:
@@ -163,10 +289,141 @@ def leaf(kind: str, value=None, class_id: int = 0) -> bytes:
         "ed25519_key": lambda: varint(class_id + 2) + varint(32) + bytes(value),
         "public_key": lambda: varint(class_id + 2) + varint(len(value)) + bytes(value),
         "kotlin_object": lambda: varint(1) + varint(0) + write_string(value),
-        "party": lambda: party_body(value[0], value[1], value[2], class_id),
-        "issue_command": lambda: issue_command_body(value[0], value[1], value[2], class_id),
-    }[kind]
-    return HEADER + body()
+    }.get(kind)
+    if body is not None:
+        return HEADER + body()
+    if kind == "party":
+        return _leaf(lambda out, g: write_party(out, g, value, class_id))
+    if kind == "issue_command":
+        return _leaf(lambda out, g: write_issue_command(out, g, value[0], value[1], value[2], class_id))
+    if kind == "cash_state":
+        return _leaf(lambda out, g: write_cash_state(out, g, value, class_id))
+    raise KeyError(kind)
+
+
+def write_issue_command(out, g, cls, nonce, keys, aal_class):
+    """Command(value = <cls>(nonce: Long), signers = Arrays.asList(PublicKey[]))
+    (Structures.kt:285, TransactionBuilder.kt:124, Cash.kt:148): fields
+    Command.signers, Command.value; the list via ArraysAsListSerializer
+    (kryo-serializers 0.41: length, component class, elements); PublicKey and the
+    command class by implicit NAME registration (name ids 1, 2); the command data's
+    own CompatibleFieldSerializer nests inside the value field."""
+    def signers(o):
+        Graph.write_class_id(o, aal_class)
+        o.write_atomic(varint(len(keys)))
+        g.write_class_name(o, "java.security.PublicKey")
+        for kc, k in keys:
+            write_key(o, kc, k)
+
+    simple = cls.replace("$", ".").rsplit(".", 1)[-1]
+
+    def value(o):
+        g.write_class_name(o, cls)
+        g.compatible_fields(o, cls, [(simple + ".nonce", lambda c: c.write_atomic(varlong_zigzag(nonce)))])
+
+    g.write_class_name(out, "net.corda.core.contracts.Command")
+    g.compatible_fields(out, "net.corda.core.contracts.Command",
+                        [("Command.signers", signers), ("Command.value", value)])
+
+
+def varint_zigzag(x: int) -> bytes:
+    """Output.writeVarInt(x, false) / writeInt(x, false)."""
+    return varint(((x << 1) ^ (x >> 31)) & 0xFFFFFFFF)
+
+
+def write_cash_state(out, g, d, x500_class):
+    """TransactionState<Cash.State> of a cash issue (Cash.generateIssue, Cash.kt:166-167):
+    TransactionState(data, notary, encumbrance) (Structures.kt:95-117) > Cash.State(amount,
+    owner) with backing fields exitKeys = setOf(owner key, issuer key), contract =
+    CASH_PROGRAM_ID, participants = listOf(owner) (Cash.kt:35,62,92-103) > Amount(quantity,
+    displayTokenSize, Issued(PartyAndReference(party, reference), Currency)) (Amount.kt:37,
+    Structures.kt:132,268). Final field classes (Amount, PartyAndReference, Cash, Party)
+    are written NOT_NULL + body, the others class + body; BigDecimal through Kryo's
+    BigDecimalSerializer (unscaled BigInteger bytes, zig-zag scale), Currency through
+    CurrencySerializer (its code), LinkedHashSet through CollectionSerializer,
+    Collections$SingletonList through CollectionsSingletonListSerializer."""
+    issuer, owner, notary = d["issuer"], d["owner"], d["notary"]
+
+    def amount(o):
+        o.write(1)  # NOT_NULL
+
+        def token(o3):
+            g.write_class_name(o3, "net.corda.core.contracts.Issued")
+
+            def issuer_field(o4):
+                o4.write(1)
+                g.compatible_fields(o4, "net.corda.core.contracts.PartyAndReference", [
+                    ("PartyAndReference.party", lambda o5: write_party(o5, g, issuer, x500_class)),
+                    ("PartyAndReference.reference",
+                     lambda o5: write_opaque(o5, g, "net.corda.core.utilities.OpaqueBytes", d["reference"]))])
+
+            def product(o4):
+                g.write_class_name(o4, "java.util.Currency")
+                o4.write_string(d["currency"])
+
+            g.compatible_fields(o3, "net.corda.core.contracts.Issued",
+                                [("Issued.issuer", issuer_field), ("Issued.product", product)])
+
+        def display(o3):
+            g.write_class_name(o3, "java.math.BigDecimal")
+            unscaled = (1).to_bytes(1, "big")  # BigInteger.ONE.toByteArray()
+            o3.write_atomic(varint(len(unscaled) + 1))
+            o3.write_bytes(unscaled)
+            o3.write_atomic(varint_zigzag(int(d["digits"])))  # scale of ONE.scaleByPowerOfTen(-digits)
+
+        g.compatible_fields(o, "net.corda.core.contracts.Amount", [
+            ("Amount.displayTokenSize", display),
+            ("Amount.quantity", lambda o3: o3.write_atomic(varlong_zigzag(int(d["quantity"])))),
+            ("Amount.token", token)])
+
+    def contract(o):
+        o.write(1)
+        g.compatible_fields(o, "net.corda.contracts.asset.Cash", [
+            ("Cash.legalContractReference",
+             lambda o3: write_opaque(o3, g, "net.corda.core.crypto.SecureHash$SHA256", d["legal_ref"]))])
+
+    def exit_keys(o):
+        g.write_class_name(o, "java.util.LinkedHashSet")
+        keys = []
+        for _, key, kc in (owner, issuer):  # insertion order; a set
+            if (kc, bytes(key)) not in keys:
+                keys.append((kc, bytes(key)))
+        o.write_atomic(varint(len(keys)))
+        for kc, key in keys:
+            write_key(o, kc, key)
+
+    def participants(o):
+        g.write_class_name(o, "java.util.Collections$SingletonList")
+        write_party(o, g, owner, x500_class)
+
+    def data(o):
+        g.write_class_name(o, "net.corda.contracts.asset.Cash$State")
+        g.compatible_fields(o, "net.corda.contracts.asset.Cash$State", [
+            ("State.amount", amount), ("State.contract", contract), ("State.exitKeys", exit_keys),
+            ("State.owner", lambda o2: write_party(o2, g, owner, x500_class)), ("State.participants", participants)])
+
+    def encumbrance(o):
+        if d.get("encumbrance") is None:
+            o.write(0)  # NULL
+        else:
+            o.write(1)
+            o.write_atomic(varint_zigzag(int(d["encumbrance"])))
+
+    def notary_field(o):
+        o.write(1)
+        write_party(o, g, notary, x500_class, with_class=False)
+
+    g.write_class_name(out, "net.corda.core.contracts.TransactionState")
+    g.compatible_fields(out, "net.corda.core.contracts.TransactionState", [
+        ("TransactionState.data", data), ("TransactionState.encumbrance", encumbrance),
+        ("TransactionState.notary", notary_field)])
+
+
+def cash_legal_ref() -> bytes:
+    """Cash.legalContractReference = SecureHash.sha256(<the legal prose URL>) (Cash.kt:62)."""
+    import hashlib
+    return hashlib.sha256(b"https://www.big-book-of-banking-law.gov/cash-claims.html").digest()
+
 
 
 TRANSACTION_TYPE_GENERAL = "net.corda.core.contracts.TransactionType$General"  # TransactionTypes.kt:64

@@ -125,3 +125,54 @@ def test_host_batch_small_chunks_subprocess():
                        timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert json.loads(r.stdout.strip().splitlines()[-1])["n"] == 3001
+
+
+def test_host_batch_many_message_lengths(engine, oracle):
+    """~300 distinct Ed25519 message lengths in one piece (the grouping's hash-map
+    path, ADVICE r03: linear in the lanes however varied the lengths) plus runs of
+    equal lengths (the previous-lane shortcut), every status against the oracle."""
+    rng = random.Random(77)
+    pub, sig = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+    rows = []
+    for i in range(3000):
+        ln = rng.randrange(0, 301) if i % 3 else 48 + (i // 300)
+        msg = bytes(rng.getrandbits(8) for _ in range(ln))
+        oracle.oracle_ed25519_sign(hashlib.sha256(b"ml%d" % (i % 40)).digest(), msg, len(msg), pub, sig)
+        s = bytearray(sig.raw)
+        if rng.random() < 0.1:
+            s[rng.randrange(64)] ^= 1 << rng.randrange(8)
+        rows.append((4, pub.raw, bytes(s), msg))
+    want = oracle_status(oracle, rows, False)
+    st, vd = engine.verify_batch(*zip(*rows))
+    assert [int(x) for x in st] == want
+    assert len({len(r[3]) for r in rows}) > 250
+
+
+def test_bench_verdict_packing_matches_library(engine, oracle):
+    """bench.py's C5 verdict words (statuses -> int64 words on the GPU, the operand
+    of the N > 1 all-gather) equal the verdict words the library's own kernels
+    build by wave ballot for the same statuses."""
+    import torch
+    sys.path.insert(0, ROOT)
+    from bench import _pack_verdict
+    n = 4096
+    rng = random.Random(3)
+    pub, sig = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+    k, s, m = bytearray(), bytearray(), bytearray()
+    for i in range(n):
+        msg = hashlib.sha256(b"pv%d" % i).digest()
+        oracle.oracle_ed25519_sign(hashlib.sha256(b"pvk%d" % (i % 16)).digest(), msg, 32, pub, sig)
+        b = bytearray(sig.raw)
+        if rng.random() < 0.2:
+            b[rng.randrange(64)] ^= 1
+        k += pub.raw
+        s += b
+        m += msg
+    dev = torch.device("cuda:0")
+    tk, ts, tm = (torch.frombuffer(bytes(x), dtype=torch.uint8).view(n, -1).to(dev) for x in (k, s, m))
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    vd = torch.empty(n // 64, dtype=torch.int64, device=dev)
+    engine.ed25519_verify_device(tk, ts, tm, st, vd, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(_pack_verdict(st), vd)
+    assert 0 < int((st != 0).sum()) < n

@@ -209,7 +209,10 @@ def test_issue_command_leaf_shape():
     leaf = _lib.kryo_encode([("issue_command", ("net.corda.contracts.asset.Cash$Commands$Issue", -1, [(45, A)]), 10)])[0]
     assert leaf.startswith(K.HEADER + b"\x01\x00" + K.write_string("net.corda.core.contracts.Command") + b"\x02")
     assert bytes([12, 1]) + b"\x01\x01" + K.write_string("java.security.PublicKey") + b"\x2f\x20" + A in leaf
-    assert leaf.endswith(K.write_string("Issue.nonce") + b"\x01\x01\x00\x00")  # zig-zag(-1) = 1, inner and outer end chunks
+    # zig-zag(-1) = 1 in the inner chunk [01 01]; the inner endChunks flushes the
+    # enclosing OutputChunked (its chunk ends there), so the inner 0 terminator is a
+    # 1-byte chunk [01 00] of the value field, then the field's own 0
+    assert leaf.endswith(K.write_string("Issue.nonce") + b"\x01\x01" + b"\x01\x00" + b"\x00")
 
 
 def test_bad_composite_items_are_rejected():
@@ -217,3 +220,79 @@ def test_bad_composite_items_are_rejected():
         _lib.kryo_encode([("party", (b"\x30\x40ab", b"k" * 32, 45), 50)])  # DER longer than the data
     with pytest.raises(_lib.EngineError):
         _lib.kryo_encode([("issue_command", ("net.corda.X$Issue", 1, []), 10)])  # no signers
+
+
+def _party(rng, ref_keys, anonymous=False, big=False):
+    name = b"" if anonymous else x500_der(
+        [(O, "Bank %d" % rng.randrange(10**6)), (L, rng.choice(["London", "New York", "Zurich"])),
+         (C, rng.choice(["GB", "US", "CH"]))] + ([(O, "y" * rng.randrange(900, 1500))] if big else []))
+    if rng.random() < 0.5:
+        return (name, rng.choice(ref_keys), 45)
+    return (name, bytes(rng.getrandbits(8) for _ in range(rng.choice((32, 32, 91)))), rng.randrange(20, 300))
+
+
+def _cash_state(rng, ref_keys, big=False):
+    issuer = _party(rng, ref_keys, anonymous=rng.random() < 0.1, big=big and rng.random() < 0.5)
+    owner = issuer if rng.random() < 0.2 else _party(rng, ref_keys, anonymous=rng.random() < 0.5,
+                                                         big=big and rng.random() < 0.5)
+    code, digits = rng.choice([("USD", 2), ("GBP", 2), ("JPY", 0), ("CHF", 2), ("BHD", 3), ("XAU", -1)])
+    return {"quantity": rng.choice([0, 1, 100, 12345, 2**40, 2**63 - 1, rng.randrange(2**63)]),
+            "currency": code, "digits": digits, "issuer": issuer,
+            "reference": bytes(rng.getrandbits(8) for _ in range(rng.choice((1, 1, 2, 8, 32, 200 if big else 3)))),
+            "owner": owner, "notary": _party(rng, ref_keys, big=big and rng.random() < 0.3),
+            "legal_ref": K.cash_legal_ref(), "encumbrance": None if rng.random() < 0.8 else rng.randrange(-5, 2**31)}
+
+
+def test_cash_state_leaf_matches_the_restatement():
+    """§8f-4's last leaf: TransactionState<Cash.State> natively (CORDAHIP_KRYO_CASH_STATE)
+    vs the Output/OutputChunked model of oracle/kryo_leaves.py, over Party and
+    AnonymousParty owners / issuers, equal owner and issuer keys (a one-element
+    exitKeys set), currencies with 0..3 and -1 fraction digits, encumbrances, and
+    X.500 names long enough that nested fields cross the 1024-byte chunk buffers.
+    PARITY UNPINNED beyond the key bytes inside (no Kryo here)."""
+    rng = random.Random(40)
+    ref_keys = [bytes.fromhex(v["A"]) for v in _key_vectors()]
+    items = [("cash_state", _cash_state(rng, ref_keys, big=i % 9 == 0), rng.randrange(20, 300)) for i in range(150)]
+    got = _lib.kryo_encode(items)
+    for (k, v, c), g in zip(items, got):
+        assert g == K.leaf(k, v, c), g.hex()
+    assert any(len(g) > 2100 for g in got)
+
+
+def test_cash_state_leaf_shape():
+    """The structure of one cash output leaf, read back field by field: class names in
+    graph order (TransactionState, Cash$State, BigDecimal, Issued, Party, OpaqueBytes,
+    Currency, SecureHash$SHA256, LinkedHashSet, SingletonList = name ids 0..9), the
+    pinned Ed25519 key serialisations inside, the amount and currency."""
+    vs = _key_vectors()
+    A0, A1 = (bytes.fromhex(v["A"]) for v in vs)
+    notary = (x500_der([(O, "Notary Service"), (L, "Zurich"), (C, "CH")]), A1, 45)
+    bank = (x500_der([(O, "Bank A"), (L, "London"), (C, "GB")]), A0, 45)
+    d = {"quantity": 100000, "currency": "USD", "digits": 2, "issuer": bank, "reference": b"\x01",
+         "owner": bank, "notary": notary, "legal_ref": K.cash_legal_ref(), "encumbrance": None}
+    leaf = _lib.kryo_encode([("cash_state", d, 52)])[0]
+    assert leaf == K.leaf("cash_state", d, 52)
+    names = ["net.corda.core.contracts.TransactionState", "net.corda.contracts.asset.Cash$State",
+             "java.math.BigDecimal", "net.corda.core.contracts.Issued", "net.corda.core.identity.Party",
+             "net.corda.core.utilities.OpaqueBytes", "java.util.Currency", "net.corda.core.crypto.SecureHash$SHA256",
+             "java.util.LinkedHashSet", "java.util.Collections$SingletonList"]
+    pos = [leaf.find(bytes([1, i]) + K.write_string(n)) for i, n in enumerate(names)]
+    assert all(p > 0 for p in pos) and pos == sorted(pos), pos
+    pinned = bytes.fromhex(vs[0]["leaf_without_references"])[8:]  # 2f 20 A0
+    assert leaf.count(pinned) == 4  # issuer party, exitKeys (owner = issuer: one element), owner, participants
+    assert leaf.count(bytes.fromhex(vs[1]["leaf_without_references"])[8:]) == 1  # the notary
+    assert K.write_string("USD") in leaf and bytes([0x02, 0x01, 0x04]) in leaf  # BigDecimal 1 x 10^-2
+    assert K.varlong_zigzag(100000) in leaf
+    assert leaf.count(bytes([1, 4])) >= 3  # Party re-used by name id 4 (owner, participants)
+    assert K.write_string("AbstractParty.owningKey") in leaf and leaf.count(K.write_string("Party.name")) == 1
+
+
+def test_bad_cash_state_is_rejected():
+    rng = random.Random(2)
+    ref_keys = [bytes.fromhex(v["A"]) for v in _key_vectors()]
+    d = _cash_state(rng, ref_keys)
+    _lib.kryo_encode([("cash_state", d, 52)])
+    for bad in (dict(d, notary=(b"", d["notary"][1], 45)), dict(d, reference=b""), dict(d, currency=""),
+                dict(d, owner=(b"\x30\x05ab", d["owner"][1], 45))):
+        with pytest.raises(_lib.EngineError):
+            _lib.kryo_encode([("cash_state", bad, 52)])

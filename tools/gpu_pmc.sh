@@ -5,7 +5,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/pmc_${TAG:-x}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-BENCH="python3 $R/bench.py --workload ${WL:-c2} --batch-log2 ${LOG2:-22} --c4-txs ${C4TXS:-262144} --steps 1 --warmup 0 --no-cpu-baseline"
+BENCH="python3 $R/bench.py --workload ${WL:-c2} --batch-log2 ${LOG2:-22} --c4-txs ${C4TXS:-262144} --steps 1 --warmup 0 --no-cpu-baseline --no-clock"
 i=0
 for grp in "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))

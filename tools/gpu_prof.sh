@@ -5,7 +5,7 @@ O=$R/gpurun_out/prof
 P=/tmp/prof_$TAG
 mkdir -p $O $P
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $P -o $TAG -- python3 $R/bench.py --workload ${WL:-c2} --steps 2 --warmup 1 --no-cpu-baseline > $O/$TAG.log 2>&1 || { echo "prof failed"; tail -20 $O/$TAG.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $P -o $TAG -- python3 $R/bench.py --workload ${WL:-c2} --steps 2 --warmup 1 --no-cpu-baseline --no-clock > $O/$TAG.log 2>&1 || { echo "prof failed"; tail -20 $O/$TAG.log; exit 1; }
 find $P -name "*kernel_stats.csv" -exec cp {} $O/${TAG}_kernel_stats.csv \;
 python3 - <<PY
 import csv
