@@ -372,16 +372,39 @@ class C4:
         g = torch.Generator(device=device)
         g.manual_seed(0xC0DA0004 + rank)
         nl = len(C4_LEAF_LENS)
-        per_tx = sum(C4_LEAF_LENS)
-        self.leaf_bytes = torch.randint(0, 256, (ntx * per_tx,), dtype=torch.uint8, device=device, generator=g)
-        lens = torch.tensor(C4_LEAF_LENS, dtype=torch.int64, device=device).repeat(ntx)
-        self.leaf_off = torch.zeros(ntx * nl + 1, dtype=torch.int64, device=device)
-        self.leaf_off[1:] = torch.cumsum(lens, 0)
-        self.tx_leaf_off = torch.arange(ntx + 1, dtype=torch.int64, device=device) * nl
+        self.native = bool(getattr(args, "native_leaves", False))
         nsig = torch.randint(1, 4, (ntx,), dtype=torch.int64, device=device, generator=g)
         self.tx_sig_off = torch.zeros(ntx + 1, dtype=torch.int64, device=device)
         self.tx_sig_off[1:] = torch.cumsum(nsig, 0)
         ns = int(self.tx_sig_off[-1])
+        seeds = torch.randint(0, 256, (ns, 32), dtype=torch.uint8, device=device, generator=g)
+        if self.native:
+            # real-shaped leaves: the five cash-issue components written by
+            # cordahip_kryo_encode; the issuer / command signer / mustSign key is the
+            # transaction's first signer, whose public key comes from a signing pass
+            from corda_amd.corpus import make_cash_issue_leaves
+            first = self.tx_sig_off[:-1]
+            pubs0 = torch.empty((ntx, 32), dtype=torch.uint8, device=device)
+            scratch = torch.empty((ntx, 64), dtype=torch.uint8, device=device)
+            eng.ed25519_sign_device(seeds[first].contiguous(), torch.zeros((ntx, 32), dtype=torch.uint8, device=device),
+                                    pubs0, scratch, stream=stream)
+            torch.cuda.synchronize(device)
+            rng = np.random.default_rng(0xC0DA0004 + rank)
+            blob, off = make_cash_issue_leaves(pubs0.cpu().numpy(), rng.integers(0, 256, (ntx, 32), dtype=np.uint8),
+                                               rng.integers(0, 256, 32, dtype=np.uint8).tobytes(),
+                                               rng.integers(1, 10**9, ntx), rng.integers(-2**63, 2**63 - 1, ntx),
+                                               threads=min(16, _cores()))
+            del pubs0, scratch
+            self.leaf_bytes = torch.from_numpy(blob).to(device)
+            self.leaf_off = torch.from_numpy(off.astype(np.int64)).to(device)
+            del blob, off
+        else:
+            per_tx = sum(C4_LEAF_LENS)
+            self.leaf_bytes = torch.randint(0, 256, (ntx * per_tx,), dtype=torch.uint8, device=device, generator=g)
+            lens = torch.tensor(C4_LEAF_LENS, dtype=torch.int64, device=device).repeat(ntx)
+            self.leaf_off = torch.zeros(ntx * nl + 1, dtype=torch.int64, device=device)
+            self.leaf_off[1:] = torch.cumsum(lens, 0)
+        self.tx_leaf_off = torch.arange(ntx + 1, dtype=torch.int64, device=device) * nl
         self.keys = torch.zeros((ns, 32), dtype=torch.uint8, device=device)
         self.sigs = torch.zeros((ns, 64), dtype=torch.uint8, device=device)
         self.txid = torch.empty((ntx, 32), dtype=torch.uint8, device=device)
@@ -391,7 +414,6 @@ class C4:
         C4.step(self)  # computes the ids (signatures still blank)
         torch.cuda.synchronize(device)
         tx_of_sig = torch.repeat_interleave(torch.arange(ntx, device=device), nsig)
-        seeds = torch.randint(0, 256, (ns, 32), dtype=torch.uint8, device=device, generator=g)
         msgs = self.txid[tx_of_sig].contiguous()
         eng.ed25519_sign_device(seeds, msgs, self.keys, self.sigs, stream=stream)
         torch.cuda.synchronize(device)
@@ -408,19 +430,26 @@ class C4:
         self.exp_bad.scatter_reduce_(0, t_bad, idx_in_tx, reduce="amin", include_self=False)
         bad_tx = torch.randperm(ntx, device=device, generator=g)[:max(1, ntx // 200)]
         pos = self.leaf_off[bad_tx * nl] + torch.randint(0, C4_LEAF_LENS[0], (bad_tx.numel(),), device=device,
-                                                         generator=g)
+                                                         generator=g)  # inside the output leaf (>= 450 B either way)
         self.leaf_bytes[pos] ^= 1
         self.exp_status[bad_tx] = 1
         self.exp_bad[bad_tx] = 0
         self.ntx, self.ns = ntx, ns
         self.units = ns
         self.macs = LIMB_MACS["ed25519"]
+        leaves = ("native Kryo leaves (cordahip_kryo_encode: TransactionState<Cash.State>, issue Command, notary "
+                  "Party, mustSign key, TransactionType; %.0f B per tx)" % (self.leaf_bytes.numel() / ntx)
+                  if self.native else "5 leaves of %s B" % list(C4_LEAF_LENS))
         self.workload = ("C4: SignedTransaction.verifySignatures on %d synthetic cash-issue txs per GPU "
-                         "(5 leaves of %s B, 1-3 Ed25519 signers; leaf SHA-256 + Merkle id + sigs + per-tx reduce)"
-                         % (ntx, list(C4_LEAF_LENS)))
-        self.data = ("synthetic: seeded random leaf bytes (real Kryo bytes not producible here), signatures made "
-                     "on the GPU over the GPU-computed ids; 0.5% sigs and 0.5% txs corrupted")
-        self.config = {"txs_per_gpu": ntx, "sigs_per_gpu": ns, "leaf_lens": list(C4_LEAF_LENS)}
+                         "(%s, 1-3 Ed25519 signers; leaf SHA-256 + Merkle id + sigs + per-tx reduce)" % (ntx, leaves))
+        self.data = (("synthetic: seeded cash-issue components serialised natively (Kryo 4 restatement, parity "
+                      "unpinned beyond the key bytes)" if self.native else
+                      "synthetic: seeded random leaf bytes of the SURVEY §8(d) C4 lengths") +
+                     ", signatures made on the GPU over the GPU-computed ids; 0.5% sigs and 0.5% txs corrupted")
+        self.config = {"txs_per_gpu": ntx, "sigs_per_gpu": ns,
+                       "leaf_bytes_per_tx": round(self.leaf_bytes.numel() / ntx, 1), "native_leaves": self.native}
+        if not self.native:
+            self.config["leaf_lens"] = list(C4_LEAF_LENS)
 
     def step(self):
         self.eng.signed_tx_verify_ed25519_device(self.leaf_bytes, self.leaf_off, self.tx_leaf_off, self.tx_sig_off,
@@ -873,6 +902,8 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--batch-log2", type=int, default=None, help="lanes per GPU (default 2^20 for c1, 2^24 otherwise)")
     ap.add_argument("--c4-txs", type=int, default=10_000_000 // 8)
+    ap.add_argument("--native-leaves", action="store_true",
+                    help="c4 / c4h: real-shaped cash-issue leaves from the native Kryo encoder (SURVEY 8f-4)")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock sampling step")

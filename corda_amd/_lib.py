@@ -8,6 +8,8 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libcordahip.so")
 
@@ -179,6 +181,30 @@ def shard_range(n: int, nshards: int, shard: int, align: int = 64):
     lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
     lib().cordahip_shard_range(n, nshards, shard, align, ctypes.byref(lo), ctypes.byref(hi))
     return lo.value, hi.value
+
+
+# numpy image of cordahip_kryo_item (natural alignment: 32 bytes)
+KRYO_ITEM_DTYPE = np.dtype([("kind", "<u4"), ("class_id", "<u4"), ("value", "<i8"), ("data", "<u8"), ("len", "<u8")])
+
+
+def kryo_encode_array(items):
+    """cordahip_kryo_encode over a contiguous KRYO_ITEM_DTYPE array whose data pointers
+    the caller keeps alive; returns (leaf bytes uint8, off uint64[n + 1])."""
+    n = len(items)
+    items = np.ascontiguousarray(items)
+    assert items.dtype == KRYO_ITEM_DTYPE and KRYO_ITEM_DTYPE.itemsize == ctypes.sizeof(KryoItem)
+    off = np.zeros(n + 1, np.uint64)
+    cap = int(items["len"].sum()) * 3 + 256 * n + 64
+    out = np.zeros(cap, np.uint8)
+    rc = lib().cordahip_kryo_encode(ctypes.cast(items.ctypes.data, ctypes.POINTER(KryoItem)), n, out.ctypes.data, cap,
+                                    off.ctypes.data)
+    if rc == ERR_BUFFER_TOO_SMALL:
+        cap = int(off[n])
+        out = np.zeros(cap, np.uint8)
+        rc = lib().cordahip_kryo_encode(ctypes.cast(items.ctypes.data, ctypes.POINTER(KryoItem)), n, out.ctypes.data, cap,
+                                    off.ctypes.data)
+    check(rc, "cordahip_kryo_encode")
+    return out[:int(off[n])], off
 
 
 def _pack_party(p):

@@ -272,3 +272,97 @@ def corrupt_c3(scheme, keys, key_len, sigs, sig_len, msgs, seed: int, g, corrupt
         key_len[comp] = 33
     cats["compressed_valid"] = comp
     return expected, cats
+
+
+# ---- C4 with native Kryo leaves ------------------------------------
+# The five components of a cash-issue WireTransaction in availableComponents
+# order (MerkleTransaction.kt:51-62; CashIssueFlow.kt:52-54): the
+# TransactionState<Cash.State> output, the issue Command, the notary Party, the
+# mustSign key, TransactionType.General -- written by cordahip_kryo_encode, no JVM.
+KRYO_IDS = {"ed25519_key": 45, "x500_name": 52, "arrays_as_list": 10}  # registration ids on the node (parameters)
+TRANSACTION_TYPE_GENERAL = "net.corda.core.contracts.TransactionType$General"  # TransactionTypes.kt:64
+CASH_ISSUE_COMMAND = "net.corda.contracts.asset.Cash$Commands$Issue"  # Cash.kt:148
+
+
+def _der(tag: int, body: bytes) -> bytes:
+    n = len(body)
+    if n < 128:
+        return bytes([tag, n]) + body
+    nb = n.to_bytes((n.bit_length() + 7) // 8, "big")
+    return bytes([tag, 0x80 | len(nb)]) + nb + body
+
+
+def x500_name(org: str, locality: str, country: str) -> bytes:
+    """DER of O=<org>, L=<locality>, C=<country> (UTF8String / PrintableString values)."""
+    out = b""
+    for oid, val, tag in ((b"\x55\x04\x0a", org, 0x0C), (b"\x55\x04\x07", locality, 0x0C), (b"\x55\x04\x06", country, 0x13)):
+        out += _der(0x31, _der(0x30, _der(0x06, oid) + _der(tag, val.encode())))
+    return _der(0x30, out)
+
+
+def make_cash_issue_leaves(issuer_keys: np.ndarray, owner_keys: np.ndarray, notary_key: bytes,
+                           quantities: np.ndarray, nonces: np.ndarray, threads: int = 8):
+    """CSR leaf bytes of ntx cash-issue transactions: issuer_keys[t] (Ed25519 A) issues
+    quantities[t] USD cents (issue reference 01) to the anonymised owner_keys[t]
+    (an AnonymousParty, as CashIssueFlow's default confidential recipient), notary
+    "Notary Service, Zurich, CH"; the command signer and mustSign key = the issuer key.
+    Returns (leaf_bytes uint8, leaf_off uint64[5 * ntx + 1])."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+
+    from corda_amd import _lib
+    ntx = len(issuer_keys)
+    ik = np.ascontiguousarray(issuer_keys, np.uint8).reshape(ntx, 32)
+    ok = np.ascontiguousarray(owner_keys, np.uint8).reshape(ntx, 32)
+    bank = x500_name("Bank A", "London", "GB")
+    notary = x500_name("Notary Service", "Zurich", "CH")
+    legal = __import__("hashlib").sha256(b"https://www.big-book-of-banking-law.gov/cash-claims.html").digest()
+    ed = KRYO_IDS["ed25519_key"]
+    mark_i, mark_o = b"\xa5" * 32, b"\x5a" * 32
+    cash_t = np.frombuffer(_lib.pack_cash_state(
+        {"issuer": (bank, mark_i, ed), "reference": b"\x01", "owner": (b"", mark_o, ed), "notary": (notary, notary_key, ed),
+         "currency": "USD", "digits": 2, "legal_ref": legal, "encumbrance": None}), np.uint8)
+    nm = CASH_ISSUE_COMMAND.encode()
+    cmd_t = np.frombuffer(bytes([len(nm)]) + nm + bytes([1]) + ed.to_bytes(2, "little") + (32).to_bytes(2, "little")
+                          + mark_i, np.uint8)
+    oi = bytes(cash_t).index(mark_i)
+    oo = bytes(cash_t).index(mark_o)
+    oc = bytes(cmd_t).index(mark_i)
+    cash = np.tile(cash_t, (ntx, 1))
+    cash[:, oi:oi + 32] = ik
+    cash[:, oo:oo + 32] = ok
+    cmd = np.tile(cmd_t, (ntx, 1))
+    cmd[:, oc:oc + 32] = ik
+    party = np.frombuffer(notary + bytes(notary_key), np.uint8).copy()
+    gen = np.frombuffer(TRANSACTION_TYPE_GENERAL.encode("utf-16-le"), np.uint8).copy()
+    items = np.zeros((ntx, 5), _lib.KRYO_ITEM_DTYPE)
+    kinds = [_lib.KRYO_KINDS[k] for k in ("cash_state", "issue_command", "party", "ed25519_key", "kotlin_object")]
+    items["kind"] = kinds
+    items["class_id"] = [KRYO_IDS["x500_name"], KRYO_IDS["arrays_as_list"], KRYO_IDS["x500_name"], ed, 0]
+    items["value"][:, 0] = quantities
+    items["value"][:, 1] = nonces
+    items["value"][:, 2] = ed  # the notary key's class
+    t = np.arange(ntx, dtype=np.uint64)
+    items["data"][:, 0] = cash.ctypes.data + t * cash.shape[1]
+    items["len"][:, 0] = cash.shape[1]
+    items["data"][:, 1] = cmd.ctypes.data + t * cmd.shape[1]
+    items["len"][:, 1] = cmd.shape[1]
+    items["data"][:, 2] = party.ctypes.data
+    items["len"][:, 2] = party.size
+    items["data"][:, 3] = ik.ctypes.data + t * 32
+    items["len"][:, 3] = 32
+    items["data"][:, 4] = gen.ctypes.data
+    items["len"][:, 4] = gen.size // 2
+    flat = items.reshape(-1)
+    per = max(1, -(-ntx // (threads * 4)))
+    parts = [(a * 5, min(ntx, a + per) * 5) for a in range(0, ntx, per)]
+    with ThreadPoolExecutor(threads) as ex:
+        outs = list(ex.map(lambda r: _lib.kryo_encode_array(flat[r[0]:r[1]]), parts))
+    blob = np.concatenate([b for b, _ in outs]) if outs else np.zeros(0, np.uint8)
+    off = np.zeros(5 * ntx + 1, np.uint64)
+    base = 0
+    for (a, b), (bb, oo_) in zip(parts, outs):
+        off[a + 1:b + 1] = oo_[1:] + base
+        base += len(bb)
+    del cash, cmd, party, gen  # the encoder copied everything
+    return blob, off

@@ -200,29 +200,37 @@ def test_kryo_leaves_feed_tx_ids(engine, oracle):
 
 
 def test_native_cash_issue_leaves_feed_tx_ids(engine, oracle):
-    """§8f-4 for the C4 cash-issue shape (CashIssueFlow.kt:52-54): the command
-    (ISSUE_COMMAND), notary Party (PARTY), mustSign key (ED25519_KEY, pinned by
-    the reference's own key serialisations) and TransactionType (KOTLIN_OBJECT)
-    leaves made natively; only the TransactionState output leaf stays a RAW JVM
-    serialisation. Leaves in availableComponents order (MerkleTransaction.kt:51-62);
-    tx ids from cordahip_tx_ids equal the oracle's over the same bytes."""
+    """§8f-4 for the C4 cash-issue shape (CashIssueFlow.kt:52-54), ALL FIVE leaves
+    made natively: the TransactionState<Cash.State> output (CASH_STATE), the
+    command (ISSUE_COMMAND), notary Party (PARTY), mustSign key (ED25519_KEY,
+    pinned by the reference's own key serialisations) and TransactionType
+    (KOTLIN_OBJECT) -- no JVM re-serialisation. Leaves in availableComponents order
+    (MerkleTransaction.kt:51-62); every leaf equals oracle/kryo_leaves.py's, and the
+    tx ids from cordahip_tx_ids equal the C oracle's over the same bytes."""
     from corda_amd import _lib
     import kryo_leaves as K
     from test_kryo import C, L, O, x500_der, _key_vectors
     rng = random.Random(21)
     ref = [bytes.fromhex(v["A"]) for v in _key_vectors()]
     txs = []
+    notary_name = x500_der([(O, "Notary Service"), (L, "Zurich"), (C, "CH")])
     for t in range(64):
         issuer = ref[t % 2] if t % 4 < 2 else bytes(rng.getrandbits(8) for _ in range(32))
-        notary = x500_der([(O, "Notary Service"), (L, "Zurich"), (C, "CH")])
-        items = [("raw", b"corda\x00\x00\x01" + bytes(rng.getrandbits(8) for _ in range(440)), 0),
+        bank = (x500_der([(O, "Bank %d" % (t % 5)), (L, "London"), (C, "GB")]), issuer, 45)
+        owner = (b"", bytes(rng.getrandbits(8) for _ in range(32)), 45) if t % 3 else bank  # anonymised recipient
+        notary = (notary_name, ref[(t + 1) % 2], 45)
+        state = {"quantity": rng.randrange(1, 10**9), "currency": rng.choice(["USD", "GBP", "JPY"]), "digits": 2,
+                 "issuer": bank, "reference": bytes([t % 256]), "owner": owner, "notary": notary,
+                 "legal_ref": K.cash_legal_ref(), "encumbrance": None}
+        state["digits"] = 0 if state["currency"] == "JPY" else 2
+        items = [("cash_state", state, 52),
                  ("issue_command", ("net.corda.contracts.asset.Cash$Commands$Issue", rng.randrange(-2**63, 2**63),
                                     [(45, issuer)]), 10),
-                 ("party", (notary, ref[(t + 1) % 2], 45), 52),
+                 ("party", (notary_name, notary[1], 45), 52),
                  ("ed25519_key", issuer, 45),
                  ("kotlin_object", K.TRANSACTION_TYPE_GENERAL, 0)]
         leaves = _lib.kryo_encode(items)
-        assert leaves[1:] == [K.leaf(k, v, c) for k, v, c in items[1:]]
+        assert leaves == [K.leaf(k, v, c) for k, v, c in items]
         txs.append(leaves)
     ids, st = engine.tx_ids(txs)
     assert (st == 0).all()
