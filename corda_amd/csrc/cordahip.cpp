@@ -371,7 +371,8 @@ int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
 // earlier slices hash (in one stream, each slice's copy waited for the previous
 // slice's kernels and D2H: ~0.4 ms of idle PCIe per slice, profiles/r03_trace_c4h).
 hipError_t tx_ids_enqueue_slices(Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound,
-                                 std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& cev) {
+                                 std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& cev,
+                                 std::vector<hipEvent_t>& kev) {
   const uint64_t t0 = bound.front(), t1 = bound.back(), ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
   const uint64_t b0 = b->leaf_off[l0], b1 = b->leaf_off[l1];
@@ -398,6 +399,7 @@ hipError_t tx_ids_enqueue_slices(Device& d, const cordahip_txid_batch* b, const 
                                      w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
     e = e ? e : launch_merkle_root(hash_base, w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), ts1 - ts0,
                                    w.txid.as<uint8_t>() + (ts0 - t0) * 32, w.tx_status.as<uint8_t>() + (ts0 - t0), s);
+    e = e ? e : hipEventRecord(kev[j], s);  // the slice's ids are in HBM: its signatures may gather them
     if (ts1 > ts0) {
       e = e ? e : hipMemcpyAsync(b->txid + ts0 * 32, w.txid.as<uint8_t>() + (ts0 - t0) * 32, (ts1 - ts0) * 32, d2h, s);
       e = e ? e : hipMemcpyAsync(b->tx_status + ts0, w.tx_status.as<uint8_t>() + (ts0 - t0), ts1 - ts0, d2h, s);
@@ -409,13 +411,76 @@ hipError_t tx_ids_enqueue_slices(Device& d, const cordahip_txid_batch* b, const 
 
 // SignedTransaction.checkSignaturesAreValid over the batch: tx ids (K3/K4),
 // every signature over its tx's id (the generic signature pipeline), then the
-// per-tx first failing signature. Every device's tx ids are enqueued at once in
-// 16 slices on its context stream (tx_ids_enqueue_slices); one waiter thread
-// per device follows the slice events and raises that device's watermark,
-// while ONE signature pipeline over all signatures (d.pb_mu, the pipeline
-// streams) packs each chunk as soon as the ids of its transactions are on the
-// host (MsgView::ready): the 1.05 GB of leaf bytes of C4's 1.25 M transactions
-// cross PCIe while the GPU verifies the signatures of earlier transactions.
+// per-tx first failing signature. Each device takes a contiguous shard of the
+// transactions AND their signatures (a transaction's leaves and signatures stay
+// on one GPU). Its ids are enqueued at once in slices on the context
+// stream (tx_ids_enqueue_slices: slice j + 1's leaf bytes cross PCIe on their own
+// stream while slice j hashes), each slice marking an event when its ids are in
+// HBM. The signature pipeline runs over the shard's signatures in chunks of one
+// or more whole slices: it packs and copies keys and signatures at once -- they
+// do not depend on the ids -- plus each row's id index, and the GPU gathers the
+// message rows from the ids in HBM after the slice's event (gather_rows32). The
+// ids go to the caller (txid) on the side; no signature waits for an id to
+// reach the host. (r03 waited for each slice's ids on the host and copied them
+// back as messages: the GPU sat idle ~5 ms per C4 step until the first
+// signatures were packed.)
+int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b,
+                     const std::vector<uint64_t>& tx_of, uint64_t lo, uint64_t hi, uint64_t slices) {
+  std::lock_guard<std::mutex> g(d.tx_mu);  // d.tx (the ids) stays ours until every gather has run
+  int r = tx_acquire_host(d);
+  if (r == CORDAHIP_SUCCESS && ensure_streams(d) != hipSuccess) r = CORDAHIP_ERR_HIP;
+  if (r != CORDAHIP_SUCCESS) return r;
+  DeviceIds di;
+  slices = std::max<uint64_t>(1, std::min<uint64_t>(slices, hi - lo));
+  for (uint64_t q = 0; q <= slices; q++) di.tx_bound.push_back(lo + (hi - lo) * q / slices);
+  std::vector<hipEvent_t> ev(slices, nullptr), cev(slices, nullptr);
+  di.ready.assign(slices, nullptr);
+  struct Events {  // destroyed on every exit
+    std::vector<hipEvent_t>* v[3];
+    ~Events() {
+      for (auto* x : v)
+        for (hipEvent_t e : *x)
+          if (e) (void)hipEventDestroy(e);
+    }
+  } events{{&ev, &cev, &di.ready}};
+  for (auto* v : {&ev, &cev, &di.ready})
+    for (auto& e : *v)
+      if (r == CORDAHIP_SUCCESS && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) r = CORDAHIP_ERR_HIP;
+  if (r == CORDAHIP_SUCCESS && tx_ids_enqueue_slices(d, &b->tx, di.tx_bound, ev, cev, di.ready) != hipSuccess)
+    r = CORDAHIP_ERR_HIP;
+  const uint64_t s0 = b->tx_sig_off[lo], s1 = b->tx_sig_off[hi];
+  if (r == CORDAHIP_SUCCESS && s1 > s0) {
+    di.txid = d.tx.txid.as<uint8_t>();
+    di.t0 = lo;
+    // chunks of whole slices, at least kMinChunk signatures each (a 2^17-lane
+    // chunk is one full-occupancy round of the Ed25519 ladder)
+    uint64_t min_chunk = 1u << 17;
+    if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) min_chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
+    di.chunk_bound.push_back(s0);
+    for (uint64_t q = 1; q <= slices; q++) {
+      const uint64_t sq = b->tx_sig_off[di.tx_bound[q]];
+      if (q == slices || sq - di.chunk_bound.back() >= min_chunk) di.chunk_bound.push_back(sq);
+    }
+    if (di.chunk_bound.back() != s1) di.chunk_bound.push_back(s1);
+    MsgView mv{b->tx.txid, nullptr, tx_of.data()};
+    mv.dev = &di;
+    // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
+    cordahip_sig_batch sb{b->tx_sig_off[b->tx.ntx], b->scheme, b->key, b->key_off, b->sig, b->sig_off, b->tx.txid,
+                          nullptr, b->sig_status, nullptr, 0u};
+    try {
+      r = sig_verify_range(ctx, d, &sb, mv, s0, s1);
+    } catch (const std::bad_alloc&) {
+      r = CORDAHIP_ERR_OUT_OF_MEMORY;
+    } catch (...) {
+      r = CORDAHIP_ERR_HIP;
+    }
+  }
+  // every slice writes the caller's txid / tx_status: drain before returning, errors included
+  const hipError_t e1 = hipStreamSynchronize(d.s_idcopy ? d.s_idcopy : d.stream), e2 = hipStreamSynchronize(d.stream);
+  if (r == CORDAHIP_SUCCESS && (e1 != hipSuccess || e2 != hipSuccess)) r = CORDAHIP_ERR_HIP;
+  return r;
+}
+
 int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   const uint64_t ntx = b->tx.ntx;
   if (ntx == 0) return CORDAHIP_SUCCESS;
@@ -426,143 +491,24 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   if (nsig && (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off)) return CORDAHIP_ERR_INVALID_ARG;
   const double t0 = tracing() ? now_ms() : 0;
   // each signature signs its transaction's id (SignedTransaction.kt:98): the
-  // pipeline reads it from txid through tx_of, no per-signature copies
+  // pipeline finds it through tx_of
   std::vector<uint64_t> tx_of(nsig);
   ctx->host->parallel_for(ntx, 4096, [&](uint64_t x, uint64_t y) {
     for (uint64_t t = x; t < y; t++)
       for (uint64_t s = b->tx_sig_off[t]; s < b->tx_sig_off[t + 1]; s++) tx_of[s] = t;
   });
-  // per device: its contiguous tx shard [lo, hi) in slices (CORDAHIP_TX_SLICES,
-  // default 16 from 65,536 transactions; each lands ~1/16 of the leaf bytes)
-  const uint64_t nd = ctx->devs.size();
+  // per device: its contiguous tx shard in slices (CORDAHIP_TX_SLICES, default 16
+  // from 65,536 transactions; each lands ~1/16 of the leaf bytes)
   uint64_t slices = ntx >= (1u << 16) ? 16 : 1;
   if (const char* v = getenv("CORDAHIP_TX_SLICES")) slices = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
-  struct Shard {
-    uint64_t lo = 0, hi = 0, done = 0;  // ids of [lo, done) are on the host
-    std::vector<uint64_t> bound;
-    std::vector<hipEvent_t> ev, cev;  // per slice: ids on the host; leaf bytes on the device
-  };
-  std::vector<Shard> sh(nd);
-  std::mutex wm_mu;
-  std::condition_variable wm_cv;
-  int ids_rc = CORDAHIP_SUCCESS;
-  auto fail = [&](int r) {
-    std::lock_guard<std::mutex> g(wm_mu);
-    if (ids_rc == CORDAHIP_SUCCESS) ids_rc = r;
-    wm_cv.notify_all();
-  };
-  for (uint64_t i = 0; i < nd; i++) {
-    shard_range(ntx, nd, i, 1, sh[i].lo, sh[i].hi);
-    sh[i].done = sh[i].lo;
-  }
-  std::vector<std::thread> waiters;
-  // Every exit joins the waiters and frees the slice events, exceptions included
-  // (std::bad_alloc from the pipeline's host vectors, std::system_error from a
-  // thread start): a joinable std::thread destroyed by unwinding would call
-  // std::terminate in the caller's process (the JVM).
-  struct Cleanup {
-    std::vector<std::thread>& waiters;
-    std::vector<Shard>& sh;
-    cordahip_ctx* ctx;
-    ~Cleanup() {
-      for (auto& t : waiters)
-        if (t.joinable()) t.join();
-      for (uint64_t i = 0; i < sh.size(); i++) {
-        (void)hipSetDevice(ctx->devs[i]->id);
-        for (auto* v : {&sh[i].ev, &sh[i].cev})
-          for (hipEvent_t& e : *v)
-            if (e) {
-              (void)hipEventDestroy(e);
-              e = nullptr;
-            }
-      }
-    }
-  } cleanup{waiters, sh, ctx};
-  for (uint64_t i = 0; i < nd; i++) {
-    Shard& S = sh[i];
-    if (S.lo >= S.hi) continue;
-    for (uint64_t q = 0; q <= slices; q++) S.bound.push_back(S.lo + (S.hi - S.lo) * q / slices);
-    S.ev.assign(slices, nullptr);
-    S.cev.assign(slices, nullptr);
-    Device& d = *ctx->devs[i];
-    int r = CORDAHIP_SUCCESS;
-    {
-      std::lock_guard<std::mutex> g(d.tx_mu);
-      r = tx_acquire_host(d);
-      if (r == CORDAHIP_SUCCESS && ensure_streams(d) != hipSuccess) r = CORDAHIP_ERR_HIP;
-      for (auto* v : {&S.ev, &S.cev})
-        for (auto& e : *v)
-          if (r == CORDAHIP_SUCCESS && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
-            r = CORDAHIP_ERR_HIP;
-      if (r == CORDAHIP_SUCCESS && tx_ids_enqueue_slices(d, &b->tx, S.bound, S.ev, S.cev) != hipSuccess)
-        r = CORDAHIP_ERR_HIP;
-    }
-    if (r != CORDAHIP_SUCCESS) {
-      // slices already enqueued on this device still write into the caller's
-      // txid / tx_status: let them finish before the call returns
-      for (hipStream_t st : {d.s_idcopy, d.stream})
-        if (st) (void)hipStreamSynchronize(st);
-      fail(r);
-      break;
-    }
-    waiters.emplace_back([&, i] {
-      Shard& W = sh[i];
-      (void)hipSetDevice(ctx->devs[i]->id);
-      for (size_t j = 0; j < W.ev.size(); j++) {
-        if (hipEventSynchronize(W.ev[j]) != hipSuccess) {
-          fail(CORDAHIP_ERR_HIP);
-          return;
-        }
-        std::lock_guard<std::mutex> g(wm_mu);
-        W.done = W.bound[j + 1];
-        wm_cv.notify_all();
-      }
-    });
-  }
-  // lanes [a, e) may be packed once every tx they sign has its id on the host
-  const std::function<bool(uint64_t, uint64_t)> ready = [&](uint64_t a, uint64_t e) {
-    if (a >= e) return true;
-    const uint64_t x = tx_of[a], y = tx_of[e - 1] + 1;
-    std::unique_lock<std::mutex> g(wm_mu);
-    wm_cv.wait(g, [&] {
-      if (ids_rc != CORDAHIP_SUCCESS) return true;
-      for (const Shard& S : sh)
-        if (S.lo < y && x < S.hi && S.done < std::min(S.hi, y)) return false;
-      return true;
-    });
-    return ids_rc == CORDAHIP_SUCCESS;
-  };
-  int rc = CORDAHIP_SUCCESS;
-  if (nsig && ids_rc == CORDAHIP_SUCCESS) {
-    MsgView mv{b->tx.txid, nullptr, tx_of.data()};
-    mv.ready = &ready;
-    // chunks of about one id slice's signatures, in whole multiples of 2^17
-    // lanes (one full-occupancy round of the Ed25519 ladder: 2 waves x 1024
-    // SIMDs x 64): each chunk is ready soon after its slice's ids land, and
-    // after the last slice the GPU drains ~one slice's signatures instead of a
-    // 2^19-lane chunk. c4h on one box: 2^17 64.8 / 64.1, 2^18 65.2 / 63.0,
-    // 156,224 (a slice, 1.2 ladder rounds) 60.3 / 53.3, 2^19 57.9 M sigs/s
-    if (slices > 1)
-      mv.chunk = (1u << 17) * std::min<uint64_t>(4, std::max<uint64_t>(1, nsig / nd / slices >> 17));
-    if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) mv.chunk = std::max<uint64_t>(64, strtoull(v, nullptr, 10));
-    // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
-    cordahip_sig_batch sb{nsig, b->scheme, b->key, b->key_off, b->sig, b->sig_off, b->tx.txid, nullptr,
-                          b->sig_status, nullptr, 0u};
-    try {
-      rc = sig_verify_msgs(ctx, &sb, mv);
-    } catch (const std::bad_alloc&) {
-      rc = CORDAHIP_ERR_OUT_OF_MEMORY;
-    } catch (...) {
-      rc = CORDAHIP_ERR_HIP;
-    }
-  }
-  for (auto& t : waiters) t.join();
+  const int rc = for_shards(ctx->devs, ntx, 1, [&](Device& d, uint64_t lo, uint64_t hi) {
+    return signed_tx_device(ctx, d, b, tx_of, lo, hi, slices);
+  });
   const double t_ids = tracing() ? now_ms() : 0;
-  if (ids_rc != CORDAHIP_SUCCESS) return ids_rc;
   if (rc != CORDAHIP_SUCCESS) return rc;
   const double t2 = tracing() ? now_ms() : 0;
-  ctx->host->parallel_for(ntx, 4096, [&](uint64_t t0, uint64_t t1) {
-    for (uint64_t t = t0; t < t1; t++) {
+  ctx->host->parallel_for(ntx, 4096, [&](uint64_t x, uint64_t y) {
+    for (uint64_t t = x; t < y; t++) {
       const uint64_t lo = b->tx_sig_off[t], hi = b->tx_sig_off[t + 1];
       b->first_bad_sig[t] = -1;
       if (lo == hi) {  // require(sigs.isNotEmpty()) in the constructor (SignedTransaction.kt:37-39) precedes tx.id

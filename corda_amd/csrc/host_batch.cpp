@@ -61,22 +61,27 @@ struct Unit {
   uint32_t mlen = 0;  // Ed25519 units: the message length of every lane
 };
 
-// Chunks [a, b) of the units' lanes: the section's first chunks ramp up
-// (chunk/16, chunk/4, then chunk) so the GPU starts after a short first pack
-// and copy instead of a whole chunk's.
+// Chunks [a, b) of the units' lanes: the first chunk is chunk/16 lanes so the
+// GPU starts after a short first pack and copy, and each next one is up to 4x
+// the previous, to at most 4 x chunk (2^18, 2^20, 2^22, 2^24 by default): the
+// host packs a chunk (copy groups overlapping PCIe) ~4x faster than the GPU
+// verifies the one before it, and fewer, larger launches pay fewer end-of-grid
+// tails (C2 through cordahip_sig_verify ran 6 launch pairs of 2^18..2^22 lanes
+// at 158.6 ms of kernels per 2^24 lanes against 153 for one launch pair,
+// profiles/r04_b trace).
 struct Chunk {
   uint32_t unit;
   uint64_t a, b;
 };
 std::vector<Chunk> make_chunks(const std::vector<Unit>& units, uint64_t chunk) {
   std::vector<Chunk> out;
-  int k = 0;
+  uint64_t sz = std::max<uint64_t>(64, chunk / 16 / 64 * 64);  // multiples of 64: chunks start word-aligned
   for (uint32_t u = 0; u < units.size(); u++)
-    for (uint64_t a = units[u].lo; a < units[u].hi; k++) {
-      const uint64_t sz = std::max<uint64_t>(64, k == 0 ? chunk / 16 : k == 1 ? chunk / 4 : chunk);
+    for (uint64_t a = units[u].lo; a < units[u].hi;) {
       const uint64_t b = std::min(units[u].hi, a + sz);
       out.push_back({u, a, b});
       a = b;
+      sz = std::min<uint64_t>(std::max<uint64_t>(64, 4 * chunk), 4 * sz);
     }
   return out;
 }
@@ -94,6 +99,7 @@ inline void pack_ed_row(const cordahip_sig_batch* b, const MsgView& mv, bool do_
   if (st == CORDAHIP_STATUS_OK) std::memcpy(sig, b->sig + b->sig_off[i], 64);
   else std::memset(sig, 0, 64);
   *pre = st;
+  if (!msg) return;  // device-side message (MsgView::dev): gathered on the GPU
   if (L == 32) std::memcpy(msg, mv.ptr(i), 32);
   else if (L) std::memcpy(msg, mv.ptr(i), L);
 }
@@ -223,7 +229,7 @@ struct PieceInfo {
 // ECDSA slot packing of lane i into row r (messages CSR at *mo)
 inline void pack_ec_row(const cordahip_sig_batch* b, const MsgView& mv, bool do_verify, uint64_t i, uint64_t r, uint8_t* hsc, uint8_t* hk,
                         uint8_t* hkl, uint8_t* hs, uint8_t* hsl, uint8_t* hm, uint64_t* hmo, uint8_t* hp,
-                        uint64_t& mo) {
+                        uint64_t& mo, uint32_t* hidx) {
   hsc[r] = b->scheme[i];
   const uint64_t kl = b->key_off[i + 1] - b->key_off[i];  // 33 or 65 (classified)
   std::memcpy(hk + r * 65, b->key + b->key_off[i], kl);
@@ -250,7 +256,8 @@ inline void pack_ec_row(const cordahip_sig_batch* b, const MsgView& mv, bool do_
   }
   hp[r] = pre;
   hmo[r] = mo;
-  std::memcpy(hm + mo, mv.ptr(i), ml);
+  if (hidx) hidx[r] = (uint32_t)(mv.tx_of[i] - mv.dev->t0);  // the row is gathered on the device
+  else std::memcpy(hm + mo, mv.ptr(i), ml);
   mo += ml;
 }
 
@@ -271,7 +278,16 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
   std::vector<Unit> units(1);
   units[0].lo = lo;
   units[0].hi = hi;
-  const std::vector<Chunk> chunks = make_chunks(units, mv.chunk ? mv.chunk : chunk_lanes("CORDAHIP_HOST_CHUNK", kEdChunk));
+  std::vector<Chunk> chunks;
+  const DeviceIds* dev = mv.dev;
+  if (dev && !dev->chunk_bound.empty()) {  // signed-tx batches: chunk boundaries at id-slice boundaries
+    for (size_t j = 0; j + 1 < dev->chunk_bound.size(); j++) {
+      const uint64_t x = std::max(lo, dev->chunk_bound[j]), y = std::min(hi, dev->chunk_bound[j + 1]);
+      if (x < y) chunks.push_back({0, x, y});
+    }
+  } else {
+    chunks = make_chunks(units, mv.chunk ? mv.chunk : chunk_lanes("CORDAHIP_HOST_CHUNK", kEdChunk));
+  }
   const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
   std::lock_guard<std::mutex> g(d.pb_mu);
   if (hipSetDevice(d.id) != hipSuccess || ensure_streams(d) != hipSuccess) return CORDAHIP_ERR_HIP;
@@ -293,6 +309,18 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
         else b->status[st.ec_lanes[r - ne]] = sc[r - ne];
       }
     });
+    // the chunk's verdict words now (its lanes' statuses are final: the direct
+    // ones were written at classification), overlapped with later chunks' GPU
+    // work; chunks start 64-aligned (shard starts and chunk sizes are)
+    if (b->verdict)
+      pool.parallel_for((st.b - st.a + 63) / 64, 1024, [&](uint64_t x, uint64_t y) {
+        for (uint64_t w = st.a / 64 + x; w < st.a / 64 + y; w++) {
+          uint64_t v = 0;
+          for (uint64_t l = 0; l < 64 && w * 64 + l < st.b; l++)
+            if (b->status[w * 64 + l] == CORDAHIP_STATUS_OK) v |= 1ull << l;
+          b->verdict[w] = v;
+        }
+      });
     return hipSuccess;
   };
   std::vector<uint16_t> cls;
@@ -309,10 +337,6 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     if (e != hipSuccess) break;
     const double t1 = tracing() ? now_ms() : 0;
     const uint64_t a = chunks[k].a, m = chunks[k].b - a;
-    if (mv.ready && !(*mv.ready)(chunks[k].a, chunks[k].b)) {  // this chunk's messages are not there yet: wait for them
-      rc = CORDAHIP_ERR_HIP;  // their producer failed (its own error is what the caller returns)
-      break;
-    }
     const uint64_t np = (m + kGrain - 1) / kGrain;
     cls.resize(m);
     pieces.resize(np);
@@ -404,50 +428,108 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     const uint64_t ne = grow[ng], nc = ec_row0[np], mb = ec_mo0[np];
     const size_t sz[14] = {ne * 32, ne * 64, std::max<uint64_t>(gmsg[ng], 16), ne, ne,
                            nc, nc * 65, nc, nc * 72, nc, std::max<uint64_t>(mb, 16), (nc + 1) * 8, nc, nc};
-    for (int q = 0; q < 14; q++)
-      if (sz[q] && (st.h[q].ensure(sz[q]) != hipSuccess || st.d[q].ensure(sz[q]) != hipSuccess))
+    for (int q = 0; q < 14; q++) {
+      const bool host = !(dev && (q == 2 || q == 10));  // device-id messages have no host rows
+      if (sz[q] && ((host && st.h[q].ensure(sz[q]) != hipSuccess) || st.d[q].ensure(sz[q]) != hipSuccess))
         rc = CORDAHIP_ERR_OUT_OF_MEMORY;
+    }
+    if (dev)
+      for (int q = 0; q < 2; q++) {
+        const uint64_t rows = std::max<uint64_t>(q ? nc : ne, 1);
+        if (st.hidx[q].ensure(rows * 4) != hipSuccess || st.didx[q].ensure(rows * 4) != hipSuccess)
+          rc = CORDAHIP_ERR_OUT_OF_MEMORY;
+      }
     if (rc != CORDAHIP_SUCCESS) break;
     st.ed_lanes.resize(ne);
     st.ec_lanes.resize(nc);
-    // (3) pack every lane into its row
-    pool.parallel_for(np, 1, [&](uint64_t x, uint64_t y) {
-      std::vector<uint64_t> row;
-      for (uint64_t q = x; q < y; q++) {
-        const PieceInfo& P = pieces[q];
-        row.assign(P.ed.size(), 0);
-        for (size_t j = 0; j < P.ed.size(); j++) row[j] = prow[q][P.ed_global[j]];
-        uint64_t er = ec_row0[q], mo = ec_mo0[q];
-        for (uint64_t r = q * kGrain; r < std::min(m, (q + 1) * kGrain); r++) {
-          const uint16_t c = cls[r];
-          const uint64_t i = a + r;
-          if (c == kEc) {
-            st.ec_lanes[er] = i;
-            pack_ec_row(b, mv, do_verify, i, er, st.h[5].as<uint8_t>(), st.h[6].as<uint8_t>(), st.h[7].as<uint8_t>(),
-                        st.h[8].as<uint8_t>(), st.h[9].as<uint8_t>(), st.h[10].as<uint8_t>(), st.h[11].as<uint64_t>(),
-                        st.h[12].as<uint8_t>(), mo);
-            er++;
-          } else if (c >= kEdBase) {
-            const size_t j = c - kEdBase, gi = P.ed_global[j];
-            const uint64_t rr = row[j]++;
-            st.ed_lanes[rr] = i;
-            // group gi's messages start at gmsg[gi]
-            pack_ed_row(b, mv, do_verify, i, (uint32_t)lens[gi], st.h[0].as<uint8_t>() + rr * 32,
-                        st.h[1].as<uint8_t>() + rr * 64,
-                        st.h[2].as<uint8_t>() + gmsg[gi] + (rr - grow[gi]) * lens[gi], st.h[3].as<uint8_t>() + rr);
+    if (nc) st.h[11].as<uint64_t>()[nc] = mb;
+    // (3) pack every lane into its row, in copy groups of pieces, each group's
+    // rows going H2D as soon as they are packed: the rows of a length group are
+    // allocated piece by piece, so a range of pieces is a row range in every
+    // group (and in the ECDSA section), and PCIe carries group g while the pool
+    // packs group g + 1 -- a chunk's inputs land ~one copy group after its pack
+    // instead of a whole pack plus a whole copy later
+    const uint64_t ncg = std::min<uint64_t>(np, m >= (1u << 20) ? 8 : 1);
+    const double t3 = tracing() ? now_ms() : 0;
+    auto h2d = [&](int q, uint64_t off, uint64_t bytes) {
+      if (bytes) e = e ? e : hipMemcpyAsync(st.d[q].as<uint8_t>() + off, st.h[q].as<uint8_t>() + off, bytes,
+                                            hipMemcpyHostToDevice, d.s_copy);
+    };
+    for (uint64_t cg = 0; cg < ncg && e == hipSuccess; cg++) {
+      const uint64_t q0 = np * cg / ncg, q1 = np * (cg + 1) / ncg;
+      pool.parallel_for(q1 - q0, 1, [&](uint64_t x, uint64_t y) {
+        std::vector<uint64_t> row;
+        for (uint64_t q = q0 + x; q < q0 + y; q++) {
+          const PieceInfo& P = pieces[q];
+          row.assign(P.ed.size(), 0);
+          for (size_t j = 0; j < P.ed.size(); j++) row[j] = prow[q][P.ed_global[j]];
+          uint64_t er = ec_row0[q], mo = ec_mo0[q];
+          for (uint64_t r = q * kGrain; r < std::min(m, (q + 1) * kGrain); r++) {
+            const uint16_t c = cls[r];
+            const uint64_t i = a + r;
+            if (c == kEc) {
+              st.ec_lanes[er] = i;
+              pack_ec_row(b, mv, do_verify, i, er, st.h[5].as<uint8_t>(), st.h[6].as<uint8_t>(),
+                          st.h[7].as<uint8_t>(), st.h[8].as<uint8_t>(), st.h[9].as<uint8_t>(), st.h[10].as<uint8_t>(),
+                          st.h[11].as<uint64_t>(), st.h[12].as<uint8_t>(), mo,
+                          dev ? st.hidx[1].as<uint32_t>() : nullptr);
+              er++;
+            } else if (c >= kEdBase) {
+              const size_t j = c - kEdBase, gi = P.ed_global[j];
+              const uint64_t rr = row[j]++;
+              st.ed_lanes[rr] = i;
+              // group gi's messages start at gmsg[gi]; device-id messages: all 32
+              // bytes, one group, row rr's message at rr * 32 once gathered
+              if (dev) st.hidx[0].as<uint32_t>()[rr] = (uint32_t)(mv.tx_of[i] - dev->t0);
+              pack_ed_row(b, mv, do_verify, i, (uint32_t)lens[gi], st.h[0].as<uint8_t>() + rr * 32,
+                          st.h[1].as<uint8_t>() + rr * 64,
+                          dev ? nullptr : st.h[2].as<uint8_t>() + gmsg[gi] + (rr - grow[gi]) * lens[gi],
+                          st.h[3].as<uint8_t>() + rr);
+            }
           }
         }
+      });
+      // this copy group's rows: [prow[q0][g], prow[q1][g]) of each Ed25519 group,
+      // [ec_row0[q0], ec_row0[q1]) of the ECDSA section
+      for (size_t gi = 0; gi < ng; gi++) {
+        const uint64_t r0 = prow[q0][gi], r1 = q1 < np ? prow[q1][gi] : grow[gi + 1];
+        h2d(0, r0 * 32, (r1 - r0) * 32);
+        h2d(1, r0 * 64, (r1 - r0) * 64);
+        h2d(3, r0, r1 - r0);
+        if (dev) {
+          if (r1 > r0)
+            e = e ? e : hipMemcpyAsync(st.didx[0].as<uint32_t>() + r0, st.hidx[0].as<uint32_t>() + r0, (r1 - r0) * 4,
+                                       hipMemcpyHostToDevice, d.s_copy);
+        } else {
+          h2d(2, gmsg[gi] + (r0 - grow[gi]) * lens[gi], (r1 - r0) * lens[gi]);
+        }
       }
-    });
-    if (nc) st.h[11].as<uint64_t>()[nc] = mb;
-    const double t3 = tracing() ? now_ms() : 0;
-    // (4) copies and launches
-    for (int q = 0; q < 14; q++) {
-      const size_t bytes = q == 2 ? gmsg[ng] : q == 10 ? mb : q == 4 || q == 13 ? 0 : sz[q];
-      if (bytes) e = e ? e : hipMemcpyAsync(st.d[q].p, st.h[q].p, bytes, hipMemcpyHostToDevice, d.s_copy);
+      const uint64_t c0 = ec_row0[q0], c1 = ec_row0[q1];
+      h2d(5, c0, c1 - c0);
+      h2d(6, c0 * 65, (c1 - c0) * 65);
+      h2d(7, c0, c1 - c0);
+      h2d(8, c0 * 72, (c1 - c0) * 72);
+      h2d(9, c0, c1 - c0);
+      h2d(11, c0 * 8, (c1 - c0 + (q1 == np && nc ? 1 : 0)) * 8);  // the last group carries off[nc]
+      h2d(12, c0, c1 - c0);
+      if (dev) {
+        if (c1 > c0)
+          e = e ? e : hipMemcpyAsync(st.didx[1].as<uint32_t>() + c0, st.hidx[1].as<uint32_t>() + c0, (c1 - c0) * 4,
+                                     hipMemcpyHostToDevice, d.s_copy);
+      } else {
+        h2d(10, ec_mo0[q0], ec_mo0[q1] - ec_mo0[q0]);
+      }
     }
+    // (4) launches
     e = e ? e : hipEventRecord(st.copied, d.s_copy);
     e = e ? e : hipStreamWaitEvent(d.s_ed, st.copied, 0);
+    // device-id messages: each section's stream waits for the id slice holding
+    // the chunk's last transaction, then gathers its rows from the ids in HBM
+    const hipEvent_t ids_ready = dev ? dev->wait_for(mv.tx_of[a + m - 1]) : nullptr;
+    if (dev && ne) {
+      e = e ? e : hipStreamWaitEvent(d.s_ed, ids_ready, 0);
+      e = e ? e : launch_gather_rows32(dev->txid, st.didx[0].as<uint32_t>(), ne, st.d[2].as<uint8_t>(), d.s_ed);
+    }
     for (size_t gi = 0; gi < ng && e == hipSuccess; gi++) {
       const uint64_t r0 = grow[gi], cnt = grow[gi + 1] - r0;
       if (cnt)
@@ -458,6 +540,10 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     if (ne) e = e ? e : hipMemcpyAsync(st.h[4].p, st.d[4].p, ne, hipMemcpyDeviceToHost, d.s_ed);
     e = e ? e : hipEventRecord(st.ed_done, d.s_ed);
     e = e ? e : hipStreamWaitEvent(d.s_ec, st.copied, 0);
+    if (dev && nc) {
+      e = e ? e : hipStreamWaitEvent(d.s_ec, ids_ready, 0);
+      e = e ? e : launch_gather_rows32(dev->txid, st.didx[1].as<uint32_t>(), nc, st.d[10].as<uint8_t>(), d.s_ec);
+    }
     if (nc && e == hipSuccess) {
       std::lock_guard<std::mutex> ge(d.ec_mu);
       e = ec_verify_enqueue(d, st.d[5].as<uint8_t>(), st.d[6].as<uint8_t>(), st.d[7].as<uint8_t>(),
@@ -467,7 +553,11 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     }
     if (nc) e = e ? e : hipMemcpyAsync(st.h[13].p, st.d[13].p, nc, hipMemcpyDeviceToHost, d.s_ec);
     e = e ? e : hipEventRecord(st.ec_done, d.s_ec);
-    if (e == hipSuccess) st.pending = true;
+    if (e == hipSuccess) {
+      st.pending = true;
+      st.a = a;
+      st.b = a + m;
+    }
     if (tracing())
       fprintf(stderr, "[cordahip] dev %d chunk %zu: %llu lanes (%llu ed, %llu ec) at %.1f ms: wait %.2f classify %.2f "
                       "pack %.2f enqueue %.2f ms\n", d.id, k, (unsigned long long)m, (unsigned long long)ne,
@@ -505,10 +595,13 @@ int sig_verify_msgs(cordahip_ctx* ctx, const cordahip_sig_batch* b, const MsgVie
   const int rc = for_shards(ctx->devs, n, 64,
                             [&](Device& d, uint64_t lo, uint64_t hi) { return sig_pipeline(ctx, d, b, mv, lo, hi); });
   if (rc != CORDAHIP_SUCCESS) return rc;
-  const double tv = tracing() ? now_ms() : 0;
-  if (b->verdict) verdict_from_status(ctx, b->status, n, b->verdict);
-  if (tracing()) fprintf(stderr, "[cordahip] verdict words: %.2f ms\n", now_ms() - tv);
+  // verdict words: built per chunk by the pipelines (sig_pipeline's finish)
   return CORDAHIP_SUCCESS;
+}
+
+int sig_verify_range(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, const MsgView& mv, uint64_t lo,
+                     uint64_t hi) {
+  return sig_pipeline(ctx, d, b, mv, lo, hi);
 }
 
 int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {

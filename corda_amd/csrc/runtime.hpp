@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -37,6 +38,7 @@ hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uin
                               uint8_t* tx_status, hipStream_t s);
 hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
                               hipStream_t s);
+hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s);
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
                             uint8_t* tx_status, hipStream_t s);
 hipError_t launch_pmt_verify(const uint32_t* leaf_hashes, const uint64_t* tx_leaf_off, const uint8_t* tok,
@@ -136,7 +138,10 @@ struct BatchStage {
   hipEvent_t copied = nullptr, ed_done = nullptr, ec_done = nullptr;
   PinBuf h[14];
   DevBuf d[14];
+  PinBuf hidx[2];  // device-id messages (MsgView::dev): per Ed25519 / ECDSA row, its tx's id index
+  DevBuf didx[2];
   std::vector<uint64_t> ed_lanes, ec_lanes;
+  uint64_t a = 0, b = 0;  // the chunk's lanes [a, b) (per-chunk verdict words)
   bool pending = false;
 };
 
@@ -313,17 +318,31 @@ struct cordahip_ctx {
 
 namespace cordahip {
 namespace rt {
+// The ids of one device's transaction shard as its id slices leave them in HBM
+// (signed-tx batches): txid[t - t0] is transaction t's id once the event of the
+// slice holding t has completed; the signatures are verified in chunks whose
+// message rows the device gathers from there (no host round trip for the ids).
+struct DeviceIds {
+  const uint8_t* txid = nullptr;           // device pointer, the shard's ids
+  uint64_t t0 = 0;                         // the shard's first transaction
+  std::vector<uint64_t> tx_bound;          // slice j = transactions [tx_bound[j], tx_bound[j + 1])
+  std::vector<hipEvent_t> ready;           // ready[j]: slice j's ids are in txid (recorded on the id stream)
+  std::vector<uint64_t> chunk_bound;       // the signature pipeline's chunk boundaries (signature indices)
+  hipEvent_t wait_for(uint64_t tx) const {  // the event after which transaction tx's id is on the device
+    const size_t j = (size_t)(std::upper_bound(tx_bound.begin(), tx_bound.end(), tx) - tx_bound.begin());
+    return ready[j ? j - 1 : 0];
+  }
+};
+
 // Where lane i's message is: the batch's CSR (msg + msg_off), or -- for the
 // signatures of a transaction batch, each over its transaction's id
-// (SignedTransaction.kt:98) -- the 32-byte id of transaction tx_of[i].
+// (SignedTransaction.kt:98) -- the 32-byte id of transaction tx_of[i]: on the
+// host at base (dev == nullptr) or on the device (dev).
 struct MsgView {
   const uint8_t* base;
   const uint64_t* off;
   const uint64_t* tx_of;
-  // optional: blocks until the messages of lanes [begin, end) exist (a
-  // producer -- the tx-id slices of a signed-tx batch -- is still writing
-  // them); false = the producer failed
-  const std::function<bool(uint64_t begin, uint64_t end)>* ready = nullptr;
+  const DeviceIds* dev = nullptr;
   uint64_t chunk = 0;  // lanes per pipeline chunk (0: the default, CORDAHIP_HOST_CHUNK)
   const uint8_t* ptr(uint64_t i) const { return tx_of ? base + 32 * tx_of[i] : base + off[i]; }
   uint64_t len(uint64_t i) const { return tx_of ? 32 : off[i + 1] - off[i]; }
@@ -332,6 +351,9 @@ struct MsgView {
 // from mv instead of b->msg / b->msg_off
 int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b);
 int sig_verify_msgs(cordahip_ctx* ctx, const cordahip_sig_batch* b, const MsgView& mv);
+// lanes [lo, hi) of b on device d only (the signed-tx path's per-device signatures)
+int sig_verify_range(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, const MsgView& mv, uint64_t lo,
+                     uint64_t hi);
 // dense Ed25519 rows in host memory through the packed pipeline (host_batch.cpp)
 int ed25519_dense_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                        uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict);

@@ -157,6 +157,19 @@ __global__ void __launch_bounds__(256) gather_txid_kernel(const uint8_t* __restr
   }
 }
 
+// Host signed-tx batches: the message rows of a pipeline chunk gathered on the
+// device from the ids the id slices left in HBM (row r = txid[idx[r]]), so the
+// signatures never wait for the ids to cross PCIe twice (D2H, then H2D as
+// messages). Two lanes per row, one 16-byte load and store each.
+__global__ void __launch_bounds__(256) gather_rows32_kernel(const uint8_t* __restrict__ txid,
+                                                            const uint32_t* __restrict__ idx, uint64_t n,
+                                                            uint8_t* __restrict__ rows) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * n) return;
+  const uint64_t r = t >> 1, h = t & 1;
+  reinterpret_cast<uint4*>(rows + r * 32)[h] = reinterpret_cast<const uint4*>(txid + (uint64_t)idx[r] * 32)[h];
+}
+
 // K5: checkSignaturesAreValid order — the first non-OK signature (list order)
 // decides the tx outcome; -1 when every signature verified.
 __global__ void __launch_bounds__(256) tx_reduce_kernel(const uint8_t* __restrict__ sig_status,
@@ -315,6 +328,11 @@ hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, u
   if (!ntx) return hipSuccess;
   hipLaunchKernelGGL(gather_txid_kernel, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, s, txid, tx_sig_off,
                      ntx, msgs);
+  return hipGetLastError();
+}
+hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(gather_rows32_kernel, dim3((uint32_t)((2 * n + 255) / 256)), dim3(256), 0, s, txid, idx, n, rows);
   return hipGetLastError();
 }
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
