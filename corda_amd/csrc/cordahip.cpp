@@ -360,19 +360,17 @@ int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
                     [&](Device& d, uint64_t t0, uint64_t t1) { return tx_ids_shard(ctx, d, b, t0, t1); });
 }
 
-// The tx ids of one device's shard, in slices, ALL enqueued at once on the
-// device's context stream (d.tx_mu held, the previous users of d.tx finished):
-// slice j's leaf bytes and offsets go H2D into their region of whole-shard
-// buffers (offset arrays unchanged, shifted base pointers), its SHA-256 and
-// Merkle kernels run, its ids and statuses come back, then ev[j] is recorded.
-// The host waits on the events in order -- no round trip per slice. The
-// slices' H2D copies go on d.s_idcopy, each followed by its event cev[j] that
-// the kernels wait on: the copies stream back to back at the PCIe rate while
-// earlier slices hash (in one stream, each slice's copy waited for the previous
-// slice's kernels and D2H: ~0.4 ms of idle PCIe per slice, profiles/r03_trace_c4h).
-hipError_t tx_ids_enqueue_slices(Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound,
-                                 std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& cev,
-                                 std::vector<hipEvent_t>& kev) {
+// The tx ids of one device's shard, in slices on the device's context stream
+// (d.tx_mu held, the previous users of d.tx finished): slice j's leaf bytes and
+// offsets go H2D into their region of whole-shard buffers (offset arrays
+// unchanged, shifted base pointers) on d.s_idcopy, followed by cev[j]; its
+// SHA-256 and Merkle kernels run on the context stream behind cev[j], then
+// kev[j] marks its ids in HBM, its ids and statuses come back, and ev[j] marks
+// them on the host. tx_ids_prepare sizes the buffers once; tx_ids_enqueue
+// enqueues slices [j0, j1) (the signed-tx path releases them a few at a time,
+// interleaved with the signature chunks' copies, because H2D copies of all
+// streams leave through the DMA engine in submission order).
+hipError_t tx_ids_prepare(Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound) {
   const uint64_t t0 = bound.front(), t1 = bound.back(), ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
   const uint64_t b0 = b->leaf_off[l0], b1 = b->leaf_off[l1];
@@ -381,12 +379,21 @@ hipError_t tx_ids_enqueue_slices(Device& d, const cordahip_txid_batch* b, const 
       w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
       w.txid.ensure(std::max<uint64_t>(ntx, 1) * 32) || w.tx_status.ensure(std::max<uint64_t>(ntx, 1)))
     return hipErrorOutOfMemory;
+  return hipSuccess;
+}
+
+hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound, size_t j0,
+                          size_t j1, std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& cev,
+                          std::vector<hipEvent_t>& kev) {
+  const uint64_t t0 = bound.front();
+  const uint64_t l0 = b->tx_leaf_off[t0], b0 = b->leaf_off[l0];
+  TxWork& w = d.tx;
   hipStream_t s = d.stream, sc = d.s_idcopy ? d.s_idcopy : d.stream;
   const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
   const uint8_t* bytes_base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(w.leaf_bytes.p) - b0);
   uint32_t* hash_base = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(w.hashes.p) - l0 * 32);
   hipError_t e = hipSuccess;
-  for (size_t j = 0; j + 1 < bound.size() && e == hipSuccess; j++) {
+  for (size_t j = j0; j < j1 && e == hipSuccess; j++) {
     const uint64_t ts0 = bound[j], ts1 = bound[j + 1];
     const uint64_t ls0 = b->tx_leaf_off[ts0], ls1 = b->tx_leaf_off[ts1];
     const uint64_t bs0 = b->leaf_off[ls0], bs1 = b->leaf_off[ls1];
@@ -406,24 +413,28 @@ hipError_t tx_ids_enqueue_slices(Device& d, const cordahip_txid_batch* b, const 
     }
     e = e ? e : hipEventRecord(ev[j], s);
   }
-  return e ? e : hipEventRecord(d.tx_ev, s);
+  if (e == hipSuccess && j1 + 1 == bound.size()) e = hipEventRecord(d.tx_ev, s);  // the last slice: fence d.tx
+  return e;
 }
 
 // SignedTransaction.checkSignaturesAreValid over the batch: tx ids (K3/K4),
 // every signature over its tx's id (the generic signature pipeline), then the
 // per-tx first failing signature. Each device takes a contiguous shard of the
 // transactions AND their signatures (a transaction's leaves and signatures stay
-// on one GPU). Its ids are enqueued at once in slices on the context
-// stream (tx_ids_enqueue_slices: slice j + 1's leaf bytes cross PCIe on their own
-// stream while slice j hashes), each slice marking an event when its ids are in
-// HBM. The signature pipeline runs over the shard's signatures in chunks of one
-// or more whole slices: it packs and copies keys and signatures at once -- they
-// do not depend on the ids -- plus each row's id index, and the GPU gathers the
-// message rows from the ids in HBM after the slice's event (gather_rows32). The
-// ids go to the caller (txid) on the side; no signature waits for an id to
-// reach the host. (r03 waited for each slice's ids on the host and copied them
-// back as messages: the GPU sat idle ~5 ms per C4 step until the first
-// signatures were packed.)
+// on one GPU). Its ids are computed in slices (tx_ids_enqueue: slice
+// j + 1's leaf bytes cross PCIe on their own stream while slice j hashes), each
+// slice marking an event when its ids are in HBM. The signature pipeline runs
+// over the shard's signatures in chunks of one or more whole slices: it packs
+// and copies keys and signatures without waiting for any id -- they do not
+// depend on the ids -- plus each row's id index, and the GPU gathers the message
+// rows from the ids in HBM after the slice's event (gather_rows32). Slices are
+// released just ahead of the chunk that needs them and `lookahead` more after
+// its copies (DeviceIds::advance), so the DMA engine, which serves H2D copies in
+// submission order, interleaves leaf bytes and signature chunks. The ids go to
+// the caller (txid) on the side; no signature waits for an id to reach the
+// host. (r03 waited for each slice's ids on the host and copied them back as
+// messages: the GPU sat idle ~5 ms per C4 step until the first signatures were
+// packed.)
 int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b,
                      const std::vector<uint64_t>& tx_of, uint64_t lo, uint64_t hi, uint64_t slices) {
   std::lock_guard<std::mutex> g(d.tx_mu);  // d.tx (the ids) stays ours until every gather has run
@@ -446,8 +457,22 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   for (auto* v : {&ev, &cev, &di.ready})
     for (auto& e : *v)
       if (r == CORDAHIP_SUCCESS && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) r = CORDAHIP_ERR_HIP;
-  if (r == CORDAHIP_SUCCESS && tx_ids_enqueue_slices(d, &b->tx, di.tx_bound, ev, cev, di.ready) != hipSuccess)
-    r = CORDAHIP_ERR_HIP;
+  // slices go out a few ahead of the signature chunk that needs them (the
+  // chunk's own H2D follows them through the DMA engine in submission order):
+  // with every slice enqueued first, r04's first signature copies waited ~20 ms
+  // behind all of C4's 1.05 GB of leaf bytes
+  size_t issued = 0;
+  uint64_t lookahead = 2;
+  if (const char* v = getenv("CORDAHIP_TX_SLICE_AHEAD")) lookahead = strtoull(v, nullptr, 10);
+  auto issue_through = [&](size_t j) -> hipError_t {  // enqueue slices [issued, j]
+    const size_t j1 = std::min<size_t>(slices, j + 1);
+    hipError_t e = hipSuccess;
+    if (j1 > issued) e = tx_ids_enqueue(d, &b->tx, di.tx_bound, issued, j1, ev, cev, di.ready);
+    issued = std::max(issued, j1);
+    return e;
+  };
+  if (r == CORDAHIP_SUCCESS && tx_ids_prepare(d, &b->tx, di.tx_bound) != hipSuccess) r = CORDAHIP_ERR_OUT_OF_MEMORY;
+  if (r == CORDAHIP_SUCCESS && issue_through(0) != hipSuccess) r = CORDAHIP_ERR_HIP;
   const uint64_t s0 = b->tx_sig_off[lo], s1 = b->tx_sig_off[hi];
   if (r == CORDAHIP_SUCCESS && s1 > s0) {
     di.txid = d.tx.txid.as<uint8_t>();
@@ -462,6 +487,13 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
       if (q == slices || sq - di.chunk_bound.back() >= min_chunk) di.chunk_bound.push_back(sq);
     }
     if (di.chunk_bound.back() != s1) di.chunk_bound.push_back(s1);
+    // before a chunk's copies: the slices it needs; after them: `lookahead` more,
+    // so PCIe carries leaf bytes while the GPU verifies the chunk
+    di.advance = [&](uint64_t sig_end, bool after) {
+      const uint64_t tx = tx_of[sig_end - 1];
+      const size_t j = (size_t)(std::upper_bound(di.tx_bound.begin(), di.tx_bound.end(), tx) - di.tx_bound.begin()) - 1;
+      return issue_through(j + (after ? lookahead : 0));
+    };
     MsgView mv{b->tx.txid, nullptr, tx_of.data()};
     mv.dev = &di;
     // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
@@ -475,6 +507,8 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
       r = CORDAHIP_ERR_HIP;
     }
   }
+  // slices no signature asked for (transactions without signatures at the end)
+  if (r == CORDAHIP_SUCCESS && issue_through(slices) != hipSuccess) r = CORDAHIP_ERR_HIP;
   // every slice writes the caller's txid / tx_status: drain before returning, errors included
   const hipError_t e1 = hipStreamSynchronize(d.s_idcopy ? d.s_idcopy : d.stream), e2 = hipStreamSynchronize(d.stream);
   if (r == CORDAHIP_SUCCESS && (e1 != hipSuccess || e2 != hipSuccess)) r = CORDAHIP_ERR_HIP;
@@ -727,6 +761,9 @@ void free_device(Device& d) {
   for (BatchStage& st : d.pb) {
     for (auto& b : st.h) b.release();
     for (auto& b : st.d) b.release();
+    for (auto& b : st.hidx) b.release();
+    for (auto& b : st.didx) b.release();
+    st.dverdict.release();
     for (hipEvent_t ev : {st.copied, st.ed_done, st.ec_done})
       if (ev) (void)hipEventDestroy(ev);
   }

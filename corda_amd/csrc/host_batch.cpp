@@ -295,12 +295,28 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     for (hipEvent_t* pe : {&st.copied, &st.ed_done, &st.ec_done})
       if (!*pe && hipEventCreateWithFlags(pe, hipEventDisableTiming) != hipSuccess) return CORDAHIP_ERR_HIP;
   HostPool& pool = *ctx->host;
+  // Chunks whose rows are the lanes in order (one message length, Ed25519 only:
+  // the common JVM batch) skip the host scatter: the statuses go D2H straight
+  // into the caller's status array and the kernel's wave-ballot verdict words
+  // into its verdict array -- when those are pinned (a DMA into pageable memory
+  // would block this thread); the last, largest chunk's scatter was the exposed
+  // tail of the call.
+  auto pinned = [](const void* p) {
+    hipPointerAttribute_t at;
+    if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return at.type == hipMemoryTypeHost;
+  };
+  const bool out_pinned = !dev && pinned(b->status) && (!b->verdict || pinned(b->verdict));
   auto finish = [&](BatchStage& st) -> hipError_t {  // wait for the stage's chunk, scatter its statuses
     if (!st.pending) return hipSuccess;
     st.pending = false;
     hipError_t e = hipEventSynchronize(st.ed_done);
     e = e ? e : hipEventSynchronize(st.ec_done);
     if (e != hipSuccess) return e;
+    if (st.direct) return hipSuccess;  // statuses and verdict words are already in the caller's arrays
     const uint8_t *se = st.h[4].as<uint8_t>(), *sc = st.h[13].as<uint8_t>();
     const uint64_t ne = st.ed_lanes.size(), nc = st.ec_lanes.size();
     pool.parallel_for(ne + nc, kGrain * 4, [&](uint64_t x, uint64_t y) {
@@ -337,6 +353,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     if (e != hipSuccess) break;
     const double t1 = tracing() ? now_ms() : 0;
     const uint64_t a = chunks[k].a, m = chunks[k].b - a;
+    if (dev && dev->advance && (e = dev->advance(a + m, false)) != hipSuccess) break;
     const uint64_t np = (m + kGrain - 1) / kGrain;
     cls.resize(m);
     pieces.resize(np);
@@ -520,6 +537,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
         h2d(10, ec_mo0[q0], ec_mo0[q1] - ec_mo0[q0]);
       }
     }
+    if (dev && dev->advance) e = e ? e : dev->advance(a + m, true);
     // (4) launches
     e = e ? e : hipEventRecord(st.copied, d.s_copy);
     e = e ? e : hipStreamWaitEvent(d.s_ed, st.copied, 0);
@@ -530,14 +548,24 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
       e = e ? e : hipStreamWaitEvent(d.s_ed, ids_ready, 0);
       e = e ? e : launch_gather_rows32(dev->txid, st.didx[0].as<uint32_t>(), ne, st.d[2].as<uint8_t>(), d.s_ed);
     }
+    st.direct = out_pinned && ng == 1 && ne == m && nc == 0 && a % 64 == 0;
+    const uint64_t words = (m + 63) / 64;
+    if (st.direct && b->verdict && st.dverdict.ensure(words * 8) != hipSuccess) st.direct = false;
     for (size_t gi = 0; gi < ng && e == hipSuccess; gi++) {
       const uint64_t r0 = grow[gi], cnt = grow[gi + 1] - r0;
       if (cnt)
         e = ed_verify_enqueue(d, st.d[0].as<uint8_t>() + r0 * 32, st.d[1].as<uint8_t>() + r0 * 64,
                               st.d[2].as<uint8_t>() + gmsg[gi], (uint32_t)lens[gi], cnt, st.d[3].as<uint8_t>() + r0,
-                              st.d[4].as<uint8_t>() + r0, nullptr, b->flags, d.s_ed);
+                              st.d[4].as<uint8_t>() + r0,
+                              st.direct && b->verdict ? st.dverdict.as<unsigned long long>() : nullptr, b->flags,
+                              d.s_ed);
     }
-    if (ne) e = e ? e : hipMemcpyAsync(st.h[4].p, st.d[4].p, ne, hipMemcpyDeviceToHost, d.s_ed);
+    if (st.direct) {
+      e = e ? e : hipMemcpyAsync(b->status + a, st.d[4].p, m, hipMemcpyDeviceToHost, d.s_ed);
+      if (b->verdict) e = e ? e : hipMemcpyAsync(b->verdict + a / 64, st.dverdict.p, words * 8, hipMemcpyDeviceToHost, d.s_ed);
+    } else if (ne) {
+      e = e ? e : hipMemcpyAsync(st.h[4].p, st.d[4].p, ne, hipMemcpyDeviceToHost, d.s_ed);
+    }
     e = e ? e : hipEventRecord(st.ed_done, d.s_ed);
     e = e ? e : hipStreamWaitEvent(d.s_ec, st.copied, 0);
     if (dev && nc) {

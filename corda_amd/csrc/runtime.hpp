@@ -142,6 +142,8 @@ struct BatchStage {
   DevBuf didx[2];
   std::vector<uint64_t> ed_lanes, ec_lanes;
   uint64_t a = 0, b = 0;  // the chunk's lanes [a, b) (per-chunk verdict words)
+  bool direct = false;    // rows == lanes: statuses / verdict words went straight to the caller's pinned arrays
+  DevBuf dverdict;        // the direct chunks' verdict words (wave ballots of the Ed25519 kernel)
   bool pending = false;
 };
 
@@ -328,6 +330,9 @@ struct DeviceIds {
   std::vector<uint64_t> tx_bound;          // slice j = transactions [tx_bound[j], tx_bound[j + 1])
   std::vector<hipEvent_t> ready;           // ready[j]: slice j's ids are in txid (recorded on the id stream)
   std::vector<uint64_t> chunk_bound;       // the signature pipeline's chunk boundaries (signature indices)
+  // called before a chunk's copies are enqueued (after = false: the id slices
+  // the chunk ending at sig_end needs) and after them (after = true: a few more)
+  std::function<hipError_t(uint64_t sig_end, bool after)> advance;
   hipEvent_t wait_for(uint64_t tx) const {  // the event after which transaction tx's id is on the device
     const size_t j = (size_t)(std::upper_bound(tx_bound.begin(), tx_bound.end(), tx) - tx_bound.begin());
     return ready[j ? j - 1 : 0];
