@@ -442,6 +442,10 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   if (r == CORDAHIP_SUCCESS && ensure_streams(d) != hipSuccess) r = CORDAHIP_ERR_HIP;
   if (r != CORDAHIP_SUCCESS) return r;
   DeviceIds di;
+  if (slices == 0) {  // default: about one slice per 2^17 signatures (one ladder round), at least 16
+    const uint64_t ns = b->tx_sig_off[hi] - b->tx_sig_off[lo];
+    slices = hi - lo >= (1u << 16) ? std::max<uint64_t>(16, (ns + (1u << 17) - 1) >> 17) : 1;
+  }
   slices = std::max<uint64_t>(1, std::min<uint64_t>(slices, hi - lo));
   for (uint64_t q = 0; q <= slices; q++) di.tx_bound.push_back(lo + (hi - lo) * q / slices);
   std::vector<hipEvent_t> ev(slices, nullptr), cev(slices, nullptr);
@@ -477,16 +481,15 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   if (r == CORDAHIP_SUCCESS && s1 > s0) {
     di.txid = d.tx.txid.as<uint8_t>();
     di.t0 = lo;
-    // chunks of whole slices, at least kMinChunk signatures each (a 2^17-lane
-    // chunk is one full-occupancy round of the Ed25519 ladder)
-    uint64_t min_chunk = 1u << 17;
-    if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) min_chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
-    di.chunk_bound.push_back(s0);
-    for (uint64_t q = 1; q <= slices; q++) {
-      const uint64_t sq = b->tx_sig_off[di.tx_bound[q]];
-      if (q == slices || sq - di.chunk_bound.back() >= min_chunk) di.chunk_bound.push_back(sq);
-    }
-    if (di.chunk_bound.back() != s1) di.chunk_bound.push_back(s1);
+    // chunks of exactly one full-occupancy round of the Ed25519 ladder (2^17
+    // lanes: 2 waves x 1,024 SIMDs x 64), each waiting on device for the slice
+    // that holds its last transaction. Slice-aligned chunks of ~156K C4
+    // signatures ran 1.19 ladder rounds each, the second at 19% occupancy:
+    // 12.8 ns per signature against ~10 for whole rounds (profiles/r04_i trace).
+    uint64_t chunk = 1u << 17;
+    if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
+    for (uint64_t x = s0; x < s1; x += chunk) di.chunk_bound.push_back(x);
+    di.chunk_bound.push_back(s1);
     // before a chunk's copies: the slices it needs; after them: `lookahead` more,
     // so PCIe carries leaf bytes while the GPU verifies the chunk
     di.advance = [&](uint64_t sig_end, bool after) {
@@ -531,9 +534,9 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
     for (uint64_t t = x; t < y; t++)
       for (uint64_t s = b->tx_sig_off[t]; s < b->tx_sig_off[t + 1]; s++) tx_of[s] = t;
   });
-  // per device: its contiguous tx shard in slices (CORDAHIP_TX_SLICES, default 16
-  // from 65,536 transactions; each lands ~1/16 of the leaf bytes)
-  uint64_t slices = ntx >= (1u << 16) ? 16 : 1;
+  // per device: its contiguous tx shard in slices (CORDAHIP_TX_SLICES; default:
+  // from 65,536 transactions, one slice per ~2^17 signatures, at least 16)
+  uint64_t slices = 0;
   if (const char* v = getenv("CORDAHIP_TX_SLICES")) slices = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
   const int rc = for_shards(ctx->devs, ntx, 1, [&](Device& d, uint64_t lo, uint64_t hi) {
     return signed_tx_device(ctx, d, b, tx_of, lo, hi, slices);

@@ -309,7 +309,16 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     }
     return at.type == hipMemoryTypeHost;
   };
-  const bool out_pinned = !dev && pinned(b->status) && (!b->verdict || pinned(b->verdict));
+  // the kernels store into the caller's arrays through their device mapping
+  uint8_t* dst_status = nullptr;
+  uint64_t* dst_verdict = nullptr;
+  bool out_pinned = !dev && pinned(b->status) && (!b->verdict || pinned(b->verdict));
+  if (out_pinned && hipHostGetDevicePointer(reinterpret_cast<void**>(&dst_status), b->status, 0) != hipSuccess)
+    out_pinned = false;
+  if (out_pinned && b->verdict &&
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&dst_verdict), b->verdict, 0) != hipSuccess)
+    out_pinned = false;
+  (void)hipGetLastError();
   auto finish = [&](BatchStage& st) -> hipError_t {  // wait for the stage's chunk, scatter its statuses
     if (!st.pending) return hipSuccess;
     st.pending = false;
@@ -354,6 +363,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     const double t1 = tracing() ? now_ms() : 0;
     const uint64_t a = chunks[k].a, m = chunks[k].b - a;
     if (dev && dev->advance && (e = dev->advance(a + m, false)) != hipSuccess) break;
+    const double t1b = tracing() ? now_ms() : 0;
     const uint64_t np = (m + kGrain - 1) / kGrain;
     cls.resize(m);
     pieces.resize(np);
@@ -537,7 +547,9 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
         h2d(10, ec_mo0[q0], ec_mo0[q1] - ec_mo0[q0]);
       }
     }
+    const double t3b = tracing() ? now_ms() : 0;
     if (dev && dev->advance) e = e ? e : dev->advance(a + m, true);
+    const double t3c = tracing() ? now_ms() : 0;
     // (4) launches
     e = e ? e : hipEventRecord(st.copied, d.s_copy);
     e = e ? e : hipStreamWaitEvent(d.s_ed, st.copied, 0);
@@ -561,10 +573,10 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
                               d.s_ed);
     }
     if (st.direct) {
-      e = e ? e : hipMemcpyAsync(b->status + a, st.d[4].p, m, hipMemcpyDeviceToHost, d.s_ed);
-      if (b->verdict) e = e ? e : hipMemcpyAsync(b->verdict + a / 64, st.dverdict.p, words * 8, hipMemcpyDeviceToHost, d.s_ed);
+      e = e ? e : launch_store_to_host(st.d[4].p, dst_status + a, m, d.s_ed);
+      if (b->verdict) e = e ? e : launch_store_to_host(st.dverdict.p, dst_verdict + a / 64, words * 8, d.s_ed);
     } else if (ne) {
-      e = e ? e : hipMemcpyAsync(st.h[4].p, st.d[4].p, ne, hipMemcpyDeviceToHost, d.s_ed);
+      e = e ? e : launch_store_to_host(st.d[4].p, st.h[4].p, ne, d.s_ed);
     }
     e = e ? e : hipEventRecord(st.ed_done, d.s_ed);
     e = e ? e : hipStreamWaitEvent(d.s_ec, st.copied, 0);
@@ -579,7 +591,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
                             st.d[11].as<uint64_t>(), 0, nc, st.d[12].as<uint8_t>(), st.d[13].as<uint8_t>(), nullptr,
                             b->flags, d.s_ec);
     }
-    if (nc) e = e ? e : hipMemcpyAsync(st.h[13].p, st.d[13].p, nc, hipMemcpyDeviceToHost, d.s_ec);
+    if (nc) e = e ? e : launch_store_to_host(st.d[13].p, st.h[13].p, nc, d.s_ec);
     e = e ? e : hipEventRecord(st.ec_done, d.s_ec);
     if (e == hipSuccess) {
       st.pending = true;
@@ -587,9 +599,10 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
       st.b = a + m;
     }
     if (tracing())
-      fprintf(stderr, "[cordahip] dev %d chunk %zu: %llu lanes (%llu ed, %llu ec) at %.1f ms: wait %.2f classify %.2f "
-                      "pack %.2f enqueue %.2f ms\n", d.id, k, (unsigned long long)m, (unsigned long long)ne,
-              (unsigned long long)nc, t0 - t_start, t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
+      fprintf(stderr, "[cordahip] dev %d chunk %zu: %llu lanes (%llu ed, %llu ec) at %.1f ms: wait %.2f ids-ahead %.2f "
+                      "classify %.2f layout %.2f pack+copy %.2f ids-after %.2f launch %.2f ms\n", d.id, k,
+              (unsigned long long)m, (unsigned long long)ne, (unsigned long long)nc, t0 - t_start, t1 - t0,
+              t1b - t1, t2 - t1b, t3 - t2, t3b - t3, t3c - t3b, now_ms() - t3c);
   }
   // drain every stage even after an error, so no queued work outlives the call
   for (int k = 0; k < kPackStages; k++) {

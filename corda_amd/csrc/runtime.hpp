@@ -38,6 +38,7 @@ hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uin
                               uint8_t* tx_status, hipStream_t s);
 hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
                               hipStream_t s);
+hipError_t launch_store_to_host(const void* src, void* dst, uint64_t n, hipStream_t s);
 hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s);
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
                             uint8_t* tx_status, hipStream_t s);

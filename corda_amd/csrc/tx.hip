@@ -12,6 +12,8 @@
 //   SignedTransaction.checkSignaturesAreValid: sigs verified in list order,
 //   the first failure throws                                   SignedTransaction.kt:95-100
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "sha2_device.hpp"
@@ -168,6 +170,25 @@ __global__ void __launch_bounds__(256) gather_rows32_kernel(const uint8_t* __res
   if (t >= 2 * n) return;
   const uint64_t r = t >> 1, h = t & 1;
   reinterpret_cast<uint4*>(rows + r * 32)[h] = reinterpret_cast<const uint4*>(txid + (uint64_t)idx[r] * 32)[h];
+}
+
+// Device -> pinned host bytes by kernel stores (the host buffer is mapped, so
+// the kernel writes it across PCIe directly): the pipelines' status returns.
+// An SDMA hipMemcpyAsync D2H behind a compute stream's kernels held the
+// enqueuing host thread ~7-18 ms whenever the DMA engine was busy with another
+// stream's H2D (CORDAHIP_TRACE "launch" phase, profiles/r04_h), which stalled
+// every later chunk's enqueue; a store kernel is ordered by the stream alone.
+// 16 bytes per lane where both ends allow it, the ragged head/tail bytewise.
+__global__ void __launch_bounds__(256) store_to_host_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                            uint64_t n) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    if (t < n / 16) reinterpret_cast<uint4*>(dst)[t] = reinterpret_cast<const uint4*>(src)[t];
+    const uint64_t tail = n & ~15ull;
+    if (t < n - tail) dst[tail + t] = src[tail + t];
+  } else if (t < n) {
+    dst[t] = src[t];
+  }
 }
 
 // K5: checkSignaturesAreValid order — the first non-OK signature (list order)
@@ -328,6 +349,14 @@ hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, u
   if (!ntx) return hipSuccess;
   hipLaunchKernelGGL(gather_txid_kernel, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, s, txid, tx_sig_off,
                      ntx, msgs);
+  return hipGetLastError();
+}
+hipError_t launch_store_to_host(const void* src, void* dst, uint64_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
+  const uint64_t threads = vec ? std::max<uint64_t>(n / 16, 16) : n;
+  hipLaunchKernelGGL(store_to_host_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s,
+                     static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), n);
   return hipGetLastError();
 }
 hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s) {

@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_multi_device_context(replicas):
     env = dict(os.environ, CORDAHIP_TEST_DEVICE_REPLICAS=str(replicas), CORDAHIP_HOST_CHUNK="256",
                CORDAHIP_STREAM_CHUNK="512", CORDAHIP_TX_SLICES="5",
-               CORDAHIP_TX_SIG_CHUNK="1")
+               CORDAHIP_TX_SIG_CHUNK="5")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "multidev_worker.py")], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

@@ -84,12 +84,13 @@ def test_signed_tx_semantics(engine, oracle):
 def test_signed_tx_id_slices(engine, oracle, slices, monkeypatch):
     """cordahip_signed_tx_verify with the tx ids in asynchronous slices that feed
     the signature pipeline (CORDAHIP_TX_SLICES; the default is 16 from 65,536
-    transactions), each slice's signatures a pipeline chunk of their own
-    (CORDAHIP_TX_SIG_CHUNK=1) whose message rows the GPU gathers from the slice's
-    ids in HBM: results must not depend on the slicing, including slices with no
-    transactions and transactions without signatures or components."""
+    transactions), the signatures in 7-lane pipeline chunks (CORDAHIP_TX_SIG_CHUNK)
+    that end mid-slice, each gathering its message rows on the GPU from the ids
+    in HBM after the slice holding its last transaction: results must not depend
+    on the slicing, including slices with no transactions and transactions
+    without signatures or components."""
     monkeypatch.setenv("CORDAHIP_TX_SLICES", slices)
-    monkeypatch.setenv("CORDAHIP_TX_SIG_CHUNK", "1")
+    monkeypatch.setenv("CORDAHIP_TX_SIG_CHUNK", "7")
     rng = random.Random(31)
     txs = [[bytes(rng.getrandbits(8) for _ in range(n)) for n in (120, 60, 43)] for _ in range(150)]
     ids, _ = engine.tx_ids(txs)

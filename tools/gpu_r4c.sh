@@ -3,7 +3,7 @@
 # ab_libs/r4before (b736408: host-side id round trip, 2^22 chunks) vs the tree.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r4_c
+O=$R/gpurun_out/r4_${TAG:-c}
 mkdir -p $O
 cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -n 40 $O/pytest.log; exit 1; }
