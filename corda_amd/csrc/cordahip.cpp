@@ -175,17 +175,19 @@ hipError_t ensure_streams(Device& d) {
   e = e ? e : hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d.id);
   std::vector<uint32_t> all((std::max(ncu, 1) + 31) / 32, 0xffffffffu);
   auto dedicated = [&](hipStream_t* st) { return hipExtStreamCreateWithCUMask(st, (uint32_t)all.size(), all.data()); };
-  hipStream_t c = nullptr, x = nullptr, y = nullptr, z = nullptr;
+  hipStream_t c = nullptr, x = nullptr, y = nullptr, z = nullptr, x2 = nullptr;
   e = e ? e : dedicated(&c);
   e = e ? e : dedicated(&x);
   e = e ? e : hipStreamCreateWithPriority(&y, hipStreamNonBlocking, hi);
   e = e ? e : dedicated(&z);
+  e = e ? e : dedicated(&x2);
   if (e != hipSuccess) {
-    for (hipStream_t s : {c, x, y, z})
+    for (hipStream_t s : {c, x, y, z, x2})
       if (s) (void)hipStreamDestroy(s);
     return e;
   }
   d.s_ed = x;
+  d.s_ed2 = x2;
   d.s_ec = y;
   d.s_idcopy = z;
   d.s_copy = c;
@@ -240,24 +242,25 @@ hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* ke
 // Enqueue Ed25519 verification of n dense lanes on stream s (device already current).
 hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
-                             unsigned long long* verdict, uint32_t flags, hipStream_t s) {
-  std::lock_guard<std::mutex> g(d.ed_mu);
+                             unsigned long long* verdict, uint32_t flags, hipStream_t s, int slot) {
+  std::lock_guard<std::mutex> g(d.ed_mu[slot]);
+  DevBuf& ws = d.ed_ws[slot];
+  hipEvent_t& ev = d.ed_ev[slot];
   static const uint64_t ws_lanes = env_lanes("CORDAHIP_ED25519_WS_LANES", kEdWsLanes);
   const uint64_t lanes = std::min<uint64_t>(ws_lanes, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
-  if (d.ed_ws.cap < lanes * ed25519_ws_lane_bytes()) {
+  if (ws.cap < lanes * ed25519_ws_lane_bytes()) {
     // a smaller buffer may still be in use by an earlier stream
-    hipError_t e = d.ed_ev ? hipEventSynchronize(d.ed_ev) : hipSuccess;
+    hipError_t e = ev ? hipEventSynchronize(ev) : hipSuccess;
     if (e != hipSuccess) return e;
-    e = d.ed_ws.ensure(std::max<uint64_t>(lanes, std::min<uint64_t>(ws_lanes, kWsMinLanes)) *
-                       ed25519_ws_lane_bytes());
+    e = ws.ensure(std::max<uint64_t>(lanes, std::min<uint64_t>(ws_lanes, kWsMinLanes)) * ed25519_ws_lane_bytes());
     if (e != hipSuccess) return e;
   }
-  if (!d.ed_ev && hipEventCreateWithFlags(&d.ed_ev, hipEventDisableTiming) != hipSuccess) return hipErrorUnknown;
-  hipError_t e = hipStreamWaitEvent(s, d.ed_ev, 0);
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return hipErrorUnknown;
+  hipError_t e = hipStreamWaitEvent(s, ev, 0);
   e = e ? e
-        : launch_ed25519_verify(keys, sigs, msgs, msg_len, n, d.btab, pre, status, verdict, d.ed_ws.as<uint32_t>(),
-                                d.ed_ws.cap / ed25519_ws_lane_bytes() / 64 * 64, flags, s);
-  e = e ? e : hipEventRecord(d.ed_ev, s);
+        : launch_ed25519_verify(keys, sigs, msgs, msg_len, n, d.btab, pre, status, verdict, ws.as<uint32_t>(),
+                                ws.cap / ed25519_ws_lane_bytes() / 64 * 64, flags, s);
+  e = e ? e : hipEventRecord(ev, s);
   return e;
 }
 
@@ -486,16 +489,23 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
     // that holds its last transaction. Slice-aligned chunks of ~156K C4
     // signatures ran 1.19 ladder rounds each, the second at 19% occupancy:
     // 12.8 ns per signature against ~10 for whole rounds (profiles/r04_i trace).
+    // The first chunk is one round (the GPU starts after one slice); the rest
+    // are two (half the end-of-grid tails per signature: a one-round launch pair
+    // ran 1.6 ms per 2^17 signatures against 1.2 at full efficiency, r04_k
+    // trace); the leaf bytes of 2^18 signatures cross PCIe in ~2 ms, faster
+    // than the GPU verifies them, so the ids stay ahead.
     uint64_t chunk = 1u << 17;
     if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
-    for (uint64_t x = s0; x < s1; x += chunk) di.chunk_bound.push_back(x);
+    for (uint64_t x = s0; x < s1; x += (x == s0 ? chunk : 2 * chunk)) di.chunk_bound.push_back(x);
     di.chunk_bound.push_back(s1);
     // before a chunk's copies: the slices it needs; after them: `lookahead` more,
     // so PCIe carries leaf bytes while the GPU verifies the chunk
     di.advance = [&](uint64_t sig_end, bool after) {
-      const uint64_t tx = tx_of[sig_end - 1];
+      // after: the slices of the next `lookahead` chunks' signatures
+      const uint64_t e = after ? std::min(s1, sig_end + lookahead * 2 * chunk) : sig_end;
+      const uint64_t tx = tx_of[e - 1];
       const size_t j = (size_t)(std::upper_bound(di.tx_bound.begin(), di.tx_bound.end(), tx) - di.tx_bound.begin()) - 1;
-      return issue_through(j + (after ? lookahead : 0));
+      return issue_through(j);
     };
     MsgView mv{b->tx.txid, nullptr, tx_of.data()};
     mv.dev = &di;
@@ -567,7 +577,7 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   if (tracing())
     fprintf(stderr, "[cordahip] signed tx batch: %llu txs, %llu sigs, %llu id slices per device: ids and "
             "signatures done at %.2f ms, reduce %.2f ms\n", (unsigned long long)ntx, (unsigned long long)nsig,
-            (unsigned long long)slices, t_ids - t0, now_ms() - t2);
+            (unsigned long long)slices, t_ids - t0, now_ms() - t2);  // slices 0: the per-device default
   return CORDAHIP_SUCCESS;
 }
 
@@ -777,15 +787,15 @@ void free_device(Device& d) {
     for (hipEvent_t ev : {st.ed_copied, st.ec_copied, st.ed_done, st.ec_done})
       if (ev) (void)hipEventDestroy(ev);
   }
-  for (hipStream_t ss : {d.s_copy, d.s_ed, d.s_ec, d.s_idcopy})
+  for (hipStream_t ss : {d.s_copy, d.s_ed, d.s_ec, d.s_idcopy, d.s_ed2})
     if (ss) (void)hipStreamDestroy(ss);
   for (DevBuf* b : {&d.tx.leaf_bytes, &d.tx.leaf_off, &d.tx.tx_leaf_off, &d.tx.hashes, &d.tx.txid, &d.tx.tx_status,
                     &d.tx.tx_sig_off, &d.tx.msgs, &d.tx.tok, &d.tx.tok_hash, &d.tx.tx_tok_off, &d.tx.root,
                     &d.tx.stack})
     b->release();
   for (DevBuf* b : {&d.ec.counters, &d.ec.perm, &d.ec.ws}) b->release();
-  d.ed_ws.release();
-  for (hipEvent_t ev : {d.ec.ev, d.ed_ev, d.tx_ev})
+  for (auto& w : d.ed_ws) w.release();
+  for (hipEvent_t ev : {d.ec.ev, d.ed_ev[0], d.ed_ev[1], d.tx_ev})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& tc : d.ring)
     for (hipEvent_t ev : {tc.a, tc.b})

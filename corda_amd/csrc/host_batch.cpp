@@ -551,14 +551,18 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     if (dev && dev->advance) e = e ? e : dev->advance(a + m, true);
     const double t3c = tracing() ? now_ms() : 0;
     // (4) launches
+    // consecutive chunks alternate between s_ed / s_ed2 and the two Ed25519
+    // workspace slots: chunk k + 1's kernels overlap chunk k's end-of-grid tail
+    const int slot = (int)(k & 1);
+    hipStream_t es = slot ? d.s_ed2 : d.s_ed;
     e = e ? e : hipEventRecord(st.copied, d.s_copy);
-    e = e ? e : hipStreamWaitEvent(d.s_ed, st.copied, 0);
+    e = e ? e : hipStreamWaitEvent(es, st.copied, 0);
     // device-id messages: each section's stream waits for the id slice holding
     // the chunk's last transaction, then gathers its rows from the ids in HBM
     const hipEvent_t ids_ready = dev ? dev->wait_for(mv.tx_of[a + m - 1]) : nullptr;
     if (dev && ne) {
-      e = e ? e : hipStreamWaitEvent(d.s_ed, ids_ready, 0);
-      e = e ? e : launch_gather_rows32(dev->txid, st.didx[0].as<uint32_t>(), ne, st.d[2].as<uint8_t>(), d.s_ed);
+      e = e ? e : hipStreamWaitEvent(es, ids_ready, 0);
+      e = e ? e : launch_gather_rows32(dev->txid, st.didx[0].as<uint32_t>(), ne, st.d[2].as<uint8_t>(), es);
     }
     st.direct = out_pinned && ng == 1 && ne == m && nc == 0 && a % 64 == 0;
     const uint64_t words = (m + 63) / 64;
@@ -570,15 +574,15 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
                               st.d[2].as<uint8_t>() + gmsg[gi], (uint32_t)lens[gi], cnt, st.d[3].as<uint8_t>() + r0,
                               st.d[4].as<uint8_t>() + r0,
                               st.direct && b->verdict ? st.dverdict.as<unsigned long long>() : nullptr, b->flags,
-                              d.s_ed);
+                              es, slot);
     }
     if (st.direct) {
-      e = e ? e : launch_store_to_host(st.d[4].p, dst_status + a, m, d.s_ed);
-      if (b->verdict) e = e ? e : launch_store_to_host(st.dverdict.p, dst_verdict + a / 64, words * 8, d.s_ed);
+      e = e ? e : launch_store_to_host(st.d[4].p, dst_status + a, m, es);
+      if (b->verdict) e = e ? e : launch_store_to_host(st.dverdict.p, dst_verdict + a / 64, words * 8, es);
     } else if (ne) {
-      e = e ? e : launch_store_to_host(st.d[4].p, st.h[4].p, ne, d.s_ed);
+      e = e ? e : launch_store_to_host(st.d[4].p, st.h[4].p, ne, es);
     }
-    e = e ? e : hipEventRecord(st.ed_done, d.s_ed);
+    e = e ? e : hipEventRecord(st.ed_done, es);
     e = e ? e : hipStreamWaitEvent(d.s_ec, st.copied, 0);
     if (dev && nc) {
       e = e ? e : hipStreamWaitEvent(d.s_ec, ids_ready, 0);
@@ -610,10 +614,11 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     d.pb[k].pending = false;
   }
   const hipError_t e1 = hipStreamSynchronize(d.s_copy), e2 = hipStreamSynchronize(d.s_ed),
+                   e2b = hipStreamSynchronize(d.s_ed2),
                    e3 = hipStreamSynchronize(d.s_ec);
   if (tracing()) fprintf(stderr, "[cordahip] dev %d: shard done at %.1f ms\n", d.id, now_ms() - t_start);
   if (rc != CORDAHIP_SUCCESS) return rc;
-  return (e || e1 || e2 || e3) ? CORDAHIP_ERR_HIP : CORDAHIP_SUCCESS;
+  return (e || e1 || e2 || e2b || e3) ? CORDAHIP_ERR_HIP : CORDAHIP_SUCCESS;
 }
 
 }  // namespace

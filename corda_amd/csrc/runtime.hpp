@@ -189,9 +189,12 @@ struct Device {
   // Ed25519 split-kernel workspace, shared by every stream that verifies on
   // this device: ed_mu orders the enqueues, ed_ev makes each user's stream
   // wait for the previous user's kernels before it reuses the buffer.
-  std::mutex ed_mu;
-  DevBuf ed_ws;
-  hipEvent_t ed_ev = nullptr;
+  // Two workspace slots: the host pipelines alternate consecutive chunks between
+  // them and between s_ed / s_ed2, so chunk k + 1's kernels fill the CUs chunk
+  // k's end-of-grid tail leaves idle (slot 0 alone serves the device paths).
+  std::mutex ed_mu[2];
+  DevBuf ed_ws[2];
+  hipEvent_t ed_ev[2] = {nullptr, nullptr};
   // The pipelines' three streams, created together and shared by the C5 drain
   // and the packed host pipelines: every H2D on s_copy (PCIe in chunk order),
   // each section's kernels + status D2H on its own stream. Three active
@@ -199,7 +202,7 @@ struct Device {
   // GPU_MAX_HW_QUEUES (4) hardware queues, and streams sharing a queue
   // serialise (with 6 stage streams C5 ran 90.6 M/s at 4 queues, 93.4 at 8).
   std::mutex streams_mu;
-  hipStream_t s_copy = nullptr, s_ed = nullptr, s_ec = nullptr;
+  hipStream_t s_copy = nullptr, s_ed = nullptr, s_ec = nullptr, s_ed2 = nullptr;
   // signed-tx batches: the id slices' leaf-byte H2D on a stream of its own, so
   // slice j + 1's bytes cross PCIe while slice j hashes (d.stream)
   hipStream_t s_idcopy = nullptr;
@@ -276,7 +279,7 @@ int hip_err(hipError_t e);
 hipError_t ensure_streams(Device& d);
 hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
-                             unsigned long long* verdict, uint32_t flags, hipStream_t s);
+                             unsigned long long* verdict, uint32_t flags, hipStream_t s, int slot = 0);
 // d.ec_mu must be held
 hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
                              const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs, const uint64_t* msg_off,
