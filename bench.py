@@ -154,7 +154,7 @@ class C2:
     # reduction -> per-lane workspace) + ladder, one launch pair for the whole
     # 2^24-lane batch (the workspace holds 2^24 lanes, cordahip.cpp kEdWsLanes)
     kernel = "ed25519_prep_half_kernel + ed25519_ladder_half_kernel"
-    pmc = "r02_pmc_ed25519_split.json"
+    pmc = "r04_pmc_ed25519_split.json"
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -1035,13 +1035,20 @@ def main():
         achieved = wl.macs * wl.units / (kernel_ms * 1e-3) / 1e12
         # HBM bytes per step from the committed PMC passes (tools/gpu_pmc.sh:
         # FETCH_SIZE and WRITE_SIZE in separate passes), scaled to this step
-        traffic, traffic_src = None, None
+        traffic, traffic_src, traffic_fabric, traffic_kind = None, None, None, None
         pmc_file = os.path.join(ROOT, "profiles", wl.pmc) if wl.pmc else None
         if pmc_file and os.path.exists(pmc_file):
             with open(pmc_file) as f:
-                per_unit = json.load(f).get("hbm_bytes_per_unit")
+                pmc = json.load(f)
+            per_unit = pmc.get("hbm_bytes_per_unit")
             traffic = per_unit * wl.units if per_unit else None
             traffic_src = "profiles/%s (bytes per unit x units per step)" % wl.pmc
+            if pmc.get("l2_fabric_bytes_per_unit"):
+                traffic_fabric = pmc["l2_fabric_bytes_per_unit"] * wl.units
+                traffic_kind = ("HBM: FETCH_SIZE/WRITE_SIZE with the ladder's Infinity-Cache hits removed by the "
+                                "calibrated model of tools/mall_sim.cpp (traffic_l2_fabric: the counters as read)")
+            else:
+                traffic_kind = "L2-to-fabric bytes (FETCH_SIZE/WRITE_SIZE): Infinity-Cache hits included, an upper bound"
         out = {
             "metric": METRIC,
             "value": value,
@@ -1065,7 +1072,8 @@ def main():
                            **wl.config),
             "roofline": {"bound": "valu", "achieved": achieved, "peak": INT_MAC_PEAK_T,
                          "unit": "Tlimb-MAC/s", "frac": achieved / INT_MAC_PEAK_T, "traffic": traffic,
-                         "traffic_source": traffic_src,
+                         "traffic_source": traffic_src, "traffic_kind": traffic_kind,
+                         "traffic_l2_fabric": traffic_fabric,
                          "kernel": wl.kernel, "kernel_ms": kernel_ms,
                          "work_per_unit": "%d limb-MACs per verification (SURVEY §8d)" % wl.macs},
             "int_alu_peak_frac": achieved / INT_MAC_PEAK_T,
