@@ -47,7 +47,7 @@ def ecdsa_csr(sc, K, KL, S, SL, M):
     return kb, ko, sb, so, np.ascontiguousarray(M), mo
 
 
-def _log(args, scheme, b, n, checked, mism_c, mism_o, got, want, rejected):
+def _log(args, scheme, b, n, checked, mism_c, mism_o, got, want, rejected, **extra):
     """One JSON line per batch: counts plus SHA-256 digests of the GPU's and the
     oracle's status bytes over the oracle-checked lanes (equal iff they agree)."""
     import hashlib
@@ -57,6 +57,7 @@ def _log(args, scheme, b, n, checked, mism_c, mism_o, got, want, rejected):
            "oracle_mismatches": mism_o, "rejected": rejected,
            "gpu_status_sha256": hashlib.sha256(got.tobytes()).hexdigest(),
            "oracle_status_sha256": hashlib.sha256(want.tobytes()).hexdigest()}
+    rec.update(extra)
     with open(args.log, "a") as f:
         f.write(json.dumps(rec) + "\n")
 
@@ -73,6 +74,10 @@ def main():
                     help="oracle-check EVERY lane of every batch (not only the open lanes and a sample)")
     ap.add_argument("--first", type=int, default=0, help="index of the first batch (seeds are per batch index)")
     ap.add_argument("--log", default=None, help="append one JSON line per batch to this file")
+    ap.add_argument("--stream-first", type=int, default=None, help="index of the first stream batch (default --first)")
+    ap.add_argument("--stream", type=int, default=0,
+                    help="C5 verifier-queue batches through cordahip_stream_verify (80%% Ed25519, 10%% P-256, "
+                         "10%% secp256k1, pinned host memory), every lane oracle-checked")
     args = ap.parse_args()
 
     import torch
@@ -87,8 +92,23 @@ def main():
     torch.cuda.set_stream(stream)
     n = 1 << args.log2
     smp = 1 << args.sample_log2
-    tot = {"ed25519": dict(lanes=0, construction_checked=0, oracle_checked=0, mismatches=0, rejected=0),
-           "ecdsa": dict(lanes=0, construction_checked=0, oracle_checked=0, mismatches=0, rejected=0)}
+    tot = {k: dict(lanes=0, construction_checked=0, oracle_checked=0, mismatches=0, rejected=0)
+           for k in ("ed25519", "ecdsa", "stream")}
+
+    def ec_oracle(sc, K, KL, S, SL, M, label):
+        """C oracle statuses of slot-layout ECDSA lanes (CPU tensors), in 2^20-lane
+        pieces with a progress line each (a silent 4-minute oracle call looks hung)."""
+        kb, ko, sb, so, Mc, mo = ecdsa_csr(sc.numpy(), K.numpy(), KL.numpy(), S.numpy(), SL.numpy(), M.numpy())
+        sch = np.ascontiguousarray(sc.numpy())
+        want = np.zeros(len(sch), np.uint8)
+        step = 1 << 20
+        for p0 in range(0, len(sch), step):
+            p1 = min(len(sch), p0 + step)
+            orc.oracle_ecdsa_verify_batch(p1 - p0, sch[p0:].ctypes.data, kb.ctypes.data, ko[p0:].ctypes.data,
+                                          sb.ctypes.data, so[p0:].ctypes.data, Mc.ctypes.data, mo[p0:].ctypes.data,
+                                          want[p0:].ctypes.data, args.threads)
+            print("  %s: oracle %d/%d ECDSA lanes (%.0f s)" % (label, p1, len(sch), time.time() - t0), flush=True)
+        return want
     t0 = time.time()
     gpu_s = 0.0
     with Engine(1) as eng:
@@ -167,8 +187,53 @@ def main():
             print("ecdsa batch %d/%d: %d lanes, construction mism %d, oracle-checked %d mism %d (%.0f s)"
                   % (b + 1, args.ec, n, mism, len(idx), mism_o, time.time() - t0), flush=True)
             del sc, K, KL, S, SL, M, exp, st
-    lanes = tot["ed25519"]["lanes"] + tot["ecdsa"]["lanes"]
-    out = {"lanes": lanes, "mismatches": tot["ed25519"]["mismatches"] + tot["ecdsa"]["mismatches"],
+        # C5 verifier-queue batches: the stream drain (chunked H2D / kernels / D2H
+        # through three buffer sets, both sections side by side) over pinned host
+        # memory, as bench.py --workload c5 runs it
+        sf = args.first if args.stream_first is None else args.stream_first
+        for b in range(sf, sf + args.stream):
+            n_ec = n // 5
+            n_ed = n - n_ec
+            pubs, sigs, msgs, exp_ed, _ = make_c2_corpus(eng, n_ed, 0xA9C50000 + b, dev, stream=stream)
+            (sc, K, KL, S, SL, M, exp_ec, _) = make_c3_corpus(eng, n_ec, 0xA9C51000 + b, dev, stream=stream)
+            torch.cuda.synchronize(dev)
+            pin = lambda x: x.cpu().contiguous().pin_memory()  # noqa: E731
+            ed = [pin(x) for x in (pubs, sigs, msgs)] + [torch.full((n_ed,), 0xEE, dtype=torch.uint8).pin_memory()]
+            ec = [pin(x) for x in (sc, K, KL, S, SL, M)] + [torch.full((n_ec,), 0xEE, dtype=torch.uint8).pin_memory()]
+            exp_ed, exp_ec = exp_ed.cpu(), exp_ec.cpu()
+            del pubs, sigs, msgs, sc, K, KL, S, SL, M
+            t1 = time.time()
+            eng.stream_verify(ed, ec)
+            gpu_s += time.time() - t1
+            st_ed, st_ec = ed[3].numpy(), ec[6].numpy()
+            k = (exp_ed >= 0).numpy()
+            ex = (exp_ec >= 0).numpy()
+            anyrej = (exp_ec == REJECT_ANY).numpy()
+            mism = int((st_ed[k] != exp_ed.numpy()[k]).sum()) + int((st_ec[ex] != exp_ec.numpy()[ex]).sum()) \
+                + int((st_ec[anyrej] == 0).sum())
+            want_ed = np.zeros(n_ed, np.uint8)
+            orc.oracle_ed25519_verify_batch(n_ed, ed[0].numpy().ctypes.data, ed[1].numpy().ctypes.data,
+                                            ed[2].numpy().ctypes.data, 32, want_ed.ctypes.data, args.threads)
+            print("  stream batch %d: oracle %d Ed25519 lanes (%.0f s)" % (b, n_ed, time.time() - t0), flush=True)
+            want_ec = ec_oracle(*ec[:6], "stream batch %d" % b)
+            got = np.concatenate([st_ed, st_ec])
+            want = np.concatenate([want_ed, want_ec])
+            mism_o = int((got != want).sum())
+            rej = int((got != 0).sum())
+            _log(args, "stream", b, n, n, mism, mism_o, got, want, rej, ed25519_lanes=n_ed, ecdsa_lanes=n_ec,
+                 ed25519_oracle_mismatches=int((st_ed != want_ed).sum()),
+                 ecdsa_oracle_mismatches=int((st_ec != want_ec).sum()))
+            r = tot["stream"]
+            r["lanes"] += n
+            r["construction_checked"] += int(k.sum() + ex.sum() + anyrej.sum())
+            r["oracle_checked"] += n
+            r["mismatches"] += mism + mism_o
+            r["rejected"] += rej
+            print("stream batch %d/%d: %d lanes (%d Ed25519, %d ECDSA), construction mism %d, oracle mism %d (%.0f s)"
+                  % (b + 1, args.stream, n, n_ed, n_ec, mism, mism_o, time.time() - t0), flush=True)
+            del ed, ec, exp_ed, exp_ec
+    lanes = sum(t["lanes"] for t in tot.values())
+    out = {"lanes": lanes, "mismatches": sum(t["mismatches"] for t in tot.values()),
            "per_scheme": tot, "gpu_verify_s": gpu_s, "wall_s": time.time() - t0,
            "batch": n, "oracle_sample_per_batch": smp,
            "note": "every lane's status vs the corpus construction where it fixes the status; every open lane "
