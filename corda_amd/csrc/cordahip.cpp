@@ -400,24 +400,61 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
     const uint64_t ts0 = bound[j], ts1 = bound[j + 1];
     const uint64_t ls0 = b->tx_leaf_off[ts0], ls1 = b->tx_leaf_off[ts1];
     const uint64_t bs0 = b->leaf_off[ls0], bs1 = b->leaf_off[ls1];
-    if (bs1 > bs0) e = hipMemcpyAsync(w.leaf_bytes.as<uint8_t>() + (bs0 - b0), b->leaf_bytes + bs0, bs1 - bs0, h2d, sc);
+    if (bs1 > bs0)
+      e = blocked("leaf-bytes H2D", [&] {
+        return hipMemcpyAsync(w.leaf_bytes.as<uint8_t>() + (bs0 - b0), b->leaf_bytes + bs0, bs1 - bs0, h2d, sc);
+      });
     e = e ? e : hipMemcpyAsync(w.leaf_off.as<uint64_t>() + (ls0 - l0), b->leaf_off + ls0, (ls1 - ls0 + 1) * 8, h2d, sc);
     e = e ? e : hipMemcpyAsync(w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), b->tx_leaf_off + ts0, (ts1 - ts0 + 1) * 8, h2d, sc);
     e = e ? e : hipEventRecord(cev[j], sc);
     e = e ? e : hipStreamWaitEvent(s, cev[j], 0);
-    e = e ? e : launch_sha256_leaves(bytes_base, w.leaf_off.as<uint64_t>() + (ls0 - l0), ls1 - ls0,
-                                     w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
+    e = e ? e : blocked("sha256_leaves launch", [&] {
+      return launch_sha256_leaves(bytes_base, w.leaf_off.as<uint64_t>() + (ls0 - l0), ls1 - ls0,
+                                  w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
+    });
     e = e ? e : launch_merkle_root(hash_base, w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), ts1 - ts0,
                                    w.txid.as<uint8_t>() + (ts0 - t0) * 32, w.tx_status.as<uint8_t>() + (ts0 - t0), s);
     e = e ? e : hipEventRecord(kev[j], s);  // the slice's ids are in HBM: its signatures may gather them
     if (ts1 > ts0) {
-      e = e ? e : hipMemcpyAsync(b->txid + ts0 * 32, w.txid.as<uint8_t>() + (ts0 - t0) * 32, (ts1 - ts0) * 32, d2h, s);
-      e = e ? e : hipMemcpyAsync(b->tx_status + ts0, w.tx_status.as<uint8_t>() + (ts0 - t0), ts1 - ts0, d2h, s);
+      e = e ? e : blocked("ids D2H", [&] {
+        return hipMemcpyAsync(b->txid + ts0 * 32, w.txid.as<uint8_t>() + (ts0 - t0) * 32, (ts1 - ts0) * 32, d2h, s);
+      });
+      e = e ? e : blocked("id status D2H", [&] {
+        return hipMemcpyAsync(b->tx_status + ts0, w.tx_status.as<uint8_t>() + (ts0 - t0), ts1 - ts0, d2h, s);
+      });
     }
     e = e ? e : hipEventRecord(ev[j], s);
   }
   if (e == hipSuccess && j1 + 1 == bound.size()) e = hipEventRecord(d.tx_ev, s);  // the last slice: fence d.tx
   return e;
+}
+
+// The per-transaction verdict of txs [t0, t1) from their id statuses and
+// signature statuses (SignedTransaction.verifySignaturesExcept -> the first
+// signature that fails, SignedTransaction.kt:95-100): first_bad_sig, and the
+// tx status becomes that signature's status.
+void reduce_txs(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b, uint64_t t0, uint64_t t1) {
+  if (t0 >= t1) return;
+  ctx->host->parallel_for(t1 - t0, 4096, [&](uint64_t x, uint64_t y) {
+    for (uint64_t t = t0 + x; t < t0 + y; t++) {
+      const uint64_t lo = b->tx_sig_off[t], hi = b->tx_sig_off[t + 1];
+      b->first_bad_sig[t] = -1;
+      if (lo == hi) {  // require(sigs.isNotEmpty()) in the constructor (SignedTransaction.kt:37-39) precedes tx.id
+        b->tx.tx_status[t] = CORDAHIP_TX_NO_SIGNATURES;
+        continue;
+      }
+      if (b->tx.tx_status[t] != CORDAHIP_STATUS_OK) {  // tx.id threw before any signature was checked
+        for (uint64_t s = lo; s < hi; s++) b->sig_status[s] = b->tx.tx_status[t];
+        continue;
+      }
+      for (uint64_t s = lo; s < hi; s++)
+        if (b->sig_status[s] != CORDAHIP_STATUS_OK) {
+          b->first_bad_sig[t] = (int64_t)(s - lo);
+          b->tx.tx_status[t] = b->sig_status[s];
+          break;
+        }
+    }
+  });
 }
 
 // SignedTransaction.checkSignaturesAreValid over the batch: tx ids (K3/K4),
@@ -438,19 +475,44 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
 // host. (r03 waited for each slice's ids on the host and copied them back as
 // messages: the GPU sat idle ~5 ms per C4 step until the first signatures were
 // packed.)
-int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b,
-                     const std::vector<uint64_t>& tx_of, uint64_t lo, uint64_t hi, uint64_t slices) {
+int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b, const uint64_t* tx_of,
+                     uint64_t lo, uint64_t hi, uint64_t slices) {
   std::lock_guard<std::mutex> g(d.tx_mu);  // d.tx (the ids) stays ours until every gather has run
   int r = tx_acquire_host(d);
   if (r == CORDAHIP_SUCCESS && ensure_streams(d) != hipSuccess) r = CORDAHIP_ERR_HIP;
   if (r != CORDAHIP_SUCCESS) return r;
   DeviceIds di;
-  if (slices == 0) {  // default: about one slice per 2^17 signatures (one ladder round), at least 16
-    const uint64_t ns = b->tx_sig_off[hi] - b->tx_sig_off[lo];
-    slices = hi - lo >= (1u << 16) ? std::max<uint64_t>(16, (ns + (1u << 17) - 1) >> 17) : 1;
+  const uint64_t s0 = b->tx_sig_off[lo], s1 = b->tx_sig_off[hi];
+  // signature chunks of whole full-occupancy rounds of the Ed25519 ladder
+  // (2^17 lanes: 2 waves x 1,024 SIMDs x 64), each waiting on device for the
+  // slice that holds its last transaction. Slice-aligned chunks of ~156K C4
+  // signatures ran 1.19 ladder rounds each, the second at 19% occupancy:
+  // 12.8 ns per signature against ~10 for whole rounds (profiles/r04_i trace).
+  // The first chunk is half a round (the GPU starts after the leaf bytes of
+  // 2^16 signatures' transactions, ~0.5 ms of PCIe), the rest one round, the
+  // two Ed25519 streams overlapping one chunk's end-of-grid tail with the
+  // next chunk (r04_o: 73.6 M/s against 71.4 for 2^17 / 2^18 chunks).
+  uint64_t chunk = 1u << 16;
+  if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
+  for (uint64_t x = s0; x < s1; x += (x == s0 ? chunk : 2 * chunk)) di.chunk_bound.push_back(x);
+  di.chunk_bound.push_back(s1);
+  if (slices == 0 && s1 > s0) {
+    // default: the id slices follow the chunks -- slice k ends with chunk k's
+    // last transaction, so chunk k waits for exactly its own ids, and the first
+    // slice's leaf bytes (what the GPU waits for before its first ladder) are
+    // one round's worth, not a sixteenth of the shard (r04_n trace: 1.1 ms of
+    // PCIe before the first kernel)
+    di.tx_bound.push_back(lo);
+    for (size_t c = 1; c + 1 < di.chunk_bound.size(); c++) {
+      const uint64_t t = tx_of[di.chunk_bound[c] - 1] + 1;
+      if (t > di.tx_bound.back() && t < hi) di.tx_bound.push_back(t);
+    }
+    di.tx_bound.push_back(hi);
+    slices = di.tx_bound.size() - 1;
+  } else {  // CORDAHIP_TX_SLICES, or no signatures: uniform slices
+    slices = std::max<uint64_t>(1, std::min<uint64_t>(slices ? slices : 1, hi - lo));
+    for (uint64_t q = 0; q <= slices; q++) di.tx_bound.push_back(lo + (hi - lo) * q / slices);
   }
-  slices = std::max<uint64_t>(1, std::min<uint64_t>(slices, hi - lo));
-  for (uint64_t q = 0; q <= slices; q++) di.tx_bound.push_back(lo + (hi - lo) * q / slices);
   std::vector<hipEvent_t> ev(slices, nullptr), cev(slices, nullptr);
   di.ready.assign(slices, nullptr);
   struct Events {  // destroyed on every exit
@@ -469,7 +531,7 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   // with every slice enqueued first, r04's first signature copies waited ~20 ms
   // behind all of C4's 1.05 GB of leaf bytes
   size_t issued = 0;
-  uint64_t lookahead = 2;
+  uint64_t lookahead = 1;  // r04_o: 1 slice ahead 73.6 M/s, 2 ahead 73.1
   if (const char* v = getenv("CORDAHIP_TX_SLICE_AHEAD")) lookahead = strtoull(v, nullptr, 10);
   auto issue_through = [&](size_t j) -> hipError_t {  // enqueue slices [issued, j]
     const size_t j1 = std::min<size_t>(slices, j + 1);
@@ -480,24 +542,10 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   };
   if (r == CORDAHIP_SUCCESS && tx_ids_prepare(d, &b->tx, di.tx_bound) != hipSuccess) r = CORDAHIP_ERR_OUT_OF_MEMORY;
   if (r == CORDAHIP_SUCCESS && issue_through(0) != hipSuccess) r = CORDAHIP_ERR_HIP;
-  const uint64_t s0 = b->tx_sig_off[lo], s1 = b->tx_sig_off[hi];
+  std::vector<std::pair<uint64_t, uint64_t>> reduced;  // tx ranges the chunks reduced
   if (r == CORDAHIP_SUCCESS && s1 > s0) {
     di.txid = d.tx.txid.as<uint8_t>();
     di.t0 = lo;
-    // chunks of exactly one full-occupancy round of the Ed25519 ladder (2^17
-    // lanes: 2 waves x 1,024 SIMDs x 64), each waiting on device for the slice
-    // that holds its last transaction. Slice-aligned chunks of ~156K C4
-    // signatures ran 1.19 ladder rounds each, the second at 19% occupancy:
-    // 12.8 ns per signature against ~10 for whole rounds (profiles/r04_i trace).
-    // The first chunk is one round (the GPU starts after one slice); the rest
-    // are two (half the end-of-grid tails per signature: a one-round launch pair
-    // ran 1.6 ms per 2^17 signatures against 1.2 at full efficiency, r04_k
-    // trace); the leaf bytes of 2^18 signatures cross PCIe in ~2 ms, faster
-    // than the GPU verifies them, so the ids stay ahead.
-    uint64_t chunk = 1u << 17;
-    if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
-    for (uint64_t x = s0; x < s1; x += (x == s0 ? chunk : 2 * chunk)) di.chunk_bound.push_back(x);
-    di.chunk_bound.push_back(s1);
     // before a chunk's copies: the slices it needs; after them: `lookahead` more,
     // so PCIe carries leaf bytes while the GPU verifies the chunk
     di.advance = [&](uint64_t sig_end, bool after) {
@@ -507,7 +555,29 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
       const size_t j = (size_t)(std::upper_bound(di.tx_bound.begin(), di.tx_bound.end(), tx) - di.tx_bound.begin()) - 1;
       return issue_through(j);
     };
-    MsgView mv{b->tx.txid, nullptr, tx_of.data()};
+    // each finished chunk reduces the transactions whose signatures it holds
+    // entirely (once their ids are on the host), overlapped with later chunks'
+    // GPU work: the whole-batch pass after the drain was ~0.55 ms of a 32 ms
+    // C4 call with the GPU idle; edge transactions are reduced after the drain
+    di.done = [&](uint64_t a, uint64_t e) -> hipError_t {
+      uint64_t t0 = tx_of[a], t1 = tx_of[e - 1];
+      if (b->tx_sig_off[t0] != a) t0++;       // starts in an earlier chunk
+      if (b->tx_sig_off[t1 + 1] == e) t1++;   // ends here: included
+      if (t0 >= t1) return hipSuccess;
+      const size_t j0 = (size_t)(std::upper_bound(di.tx_bound.begin(), di.tx_bound.end(), t0) - di.tx_bound.begin()) - 1;
+      const size_t j1 = (size_t)(std::upper_bound(di.tx_bound.begin(), di.tx_bound.end(), t1 - 1) - di.tx_bound.begin());
+      for (size_t j = j0; j < j1; j++) {  // their slices' ids and statuses are back (issued: the chunk needed them)
+        if (j >= issued) return hipErrorInvalidValue;
+        if (hipError_t x = blocked("ids on the host", [&] { return hipEventSynchronize(ev[j]); })) return x;
+      }
+      const double tr = tracing() ? now_ms() : 0;
+      reduce_txs(ctx, b, t0, t1);
+      if (tracing() && now_ms() - tr > 1.0) fprintf(stderr, "[cordahip] reduce of %llu txs %.2f ms\n",
+                                                    (unsigned long long)(t1 - t0), now_ms() - tr);
+      reduced.push_back({t0, t1});
+      return hipSuccess;
+    };
+    MsgView mv{b->tx.txid, nullptr, tx_of};
     mv.dev = &di;
     // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
     cordahip_sig_batch sb{b->tx_sig_off[b->tx.ntx], b->scheme, b->key, b->key_off, b->sig, b->sig_off, b->tx.txid,
@@ -525,6 +595,15 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   // every slice writes the caller's txid / tx_status: drain before returning, errors included
   const hipError_t e1 = hipStreamSynchronize(d.s_idcopy ? d.s_idcopy : d.stream), e2 = hipStreamSynchronize(d.stream);
   if (r == CORDAHIP_SUCCESS && (e1 != hipSuccess || e2 != hipSuccess)) r = CORDAHIP_ERR_HIP;
+  if (r != CORDAHIP_SUCCESS) return r;
+  // the transactions no chunk reduced: chunk-edge ones, those without signatures
+  std::sort(reduced.begin(), reduced.end());
+  uint64_t t = lo;
+  for (const auto& rg : reduced) {
+    reduce_txs(ctx, b, t, rg.first);
+    t = std::max(t, rg.second);
+  }
+  reduce_txs(ctx, b, t, hi);
   return r;
 }
 
@@ -538,14 +617,25 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   if (nsig && (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off)) return CORDAHIP_ERR_INVALID_ARG;
   const double t0 = tracing() ? now_ms() : 0;
   // each signature signs its transaction's id (SignedTransaction.kt:98): the
-  // pipeline finds it through tx_of
-  std::vector<uint64_t> tx_of(nsig);
+  // pipeline finds it through tx_of -- a per-thread buffer kept across calls
+  // (a fresh 20 MB vector per C4 call page-faulted for ~0.8 ms, 3.9 ms on the
+  // first calls)
+  thread_local std::unique_ptr<uint64_t[]> tl_tx_of;
+  thread_local uint64_t tl_tx_of_cap = 0;
+  if (nsig > tl_tx_of_cap) {
+    tl_tx_of.reset();
+    tl_tx_of.reset(new uint64_t[nsig]);
+    tl_tx_of_cap = nsig;
+  }
+  uint64_t* tx_of = tl_tx_of.get();
   ctx->host->parallel_for(ntx, 4096, [&](uint64_t x, uint64_t y) {
     for (uint64_t t = x; t < y; t++)
       for (uint64_t s = b->tx_sig_off[t]; s < b->tx_sig_off[t + 1]; s++) tx_of[s] = t;
   });
+  const double t_of = tracing() ? now_ms() : 0;
   // per device: its contiguous tx shard in slices (CORDAHIP_TX_SLICES; default:
-  // from 65,536 transactions, one slice per ~2^17 signatures, at least 16)
+  // one slice per signature chunk) and, chunk by
+  // chunk and after the drain, the per-transaction reduce (reduce_txs)
   uint64_t slices = 0;
   if (const char* v = getenv("CORDAHIP_TX_SLICES")) slices = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
   const int rc = for_shards(ctx->devs, ntx, 1, [&](Device& d, uint64_t lo, uint64_t hi) {
@@ -553,31 +643,10 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   });
   const double t_ids = tracing() ? now_ms() : 0;
   if (rc != CORDAHIP_SUCCESS) return rc;
-  const double t2 = tracing() ? now_ms() : 0;
-  ctx->host->parallel_for(ntx, 4096, [&](uint64_t x, uint64_t y) {
-    for (uint64_t t = x; t < y; t++) {
-      const uint64_t lo = b->tx_sig_off[t], hi = b->tx_sig_off[t + 1];
-      b->first_bad_sig[t] = -1;
-      if (lo == hi) {  // require(sigs.isNotEmpty()) in the constructor (SignedTransaction.kt:37-39) precedes tx.id
-        b->tx.tx_status[t] = CORDAHIP_TX_NO_SIGNATURES;
-        continue;
-      }
-      if (b->tx.tx_status[t] != CORDAHIP_STATUS_OK) {  // tx.id threw before any signature was checked
-        for (uint64_t s = lo; s < hi; s++) b->sig_status[s] = b->tx.tx_status[t];
-        continue;
-      }
-      for (uint64_t s = lo; s < hi; s++)
-        if (b->sig_status[s] != CORDAHIP_STATUS_OK) {
-          b->first_bad_sig[t] = (int64_t)(s - lo);
-          b->tx.tx_status[t] = b->sig_status[s];
-          break;
-        }
-    }
-  });
   if (tracing())
-    fprintf(stderr, "[cordahip] signed tx batch: %llu txs, %llu sigs, %llu id slices per device: ids and "
-            "signatures done at %.2f ms, reduce %.2f ms\n", (unsigned long long)ntx, (unsigned long long)nsig,
-            (unsigned long long)slices, t_ids - t0, now_ms() - t2);  // slices 0: the per-device default
+    fprintf(stderr, "[cordahip] signed tx batch: %llu txs, %llu sigs, %llu id slices per device: tx_of %.2f ms, "
+            "ids, signatures and reduce done at %.2f ms\n", (unsigned long long)ntx, (unsigned long long)nsig,
+            (unsigned long long)slices, t_of - t0, t_ids - t0);  // slices 0: the per-device default
   return CORDAHIP_SUCCESS;
 }
 

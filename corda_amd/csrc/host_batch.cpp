@@ -322,7 +322,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
   auto finish = [&](BatchStage& st) -> hipError_t {  // wait for the stage's chunk, scatter its statuses
     if (!st.pending) return hipSuccess;
     st.pending = false;
-    hipError_t e = hipEventSynchronize(st.ed_done);
+    hipError_t e = blocked("chunk verified", [&] { return hipEventSynchronize(st.ed_done); });
     e = e ? e : hipEventSynchronize(st.ec_done);
     if (e != hipSuccess) return e;
     if (st.direct) return hipSuccess;  // statuses and verdict words are already in the caller's arrays
@@ -337,6 +337,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     // the chunk's verdict words now (its lanes' statuses are final: the direct
     // ones were written at classification), overlapped with later chunks' GPU
     // work; chunks start 64-aligned (shard starts and chunk sizes are)
+    if (dev && dev->done && (e = dev->done(st.a, st.b)) != hipSuccess) return e;
     if (b->verdict)
       pool.parallel_for((st.b - st.a + 63) / 64, 1024, [&](uint64_t x, uint64_t y) {
         for (uint64_t w = st.a / 64 + x; w < st.a / 64 + y; w++) {

@@ -274,6 +274,16 @@ inline bool tracing() {
   static const bool on = getenv("CORDAHIP_TRACE") != nullptr;
   return on;
 }
+// under CORDAHIP_TRACE: report a HIP call that held the host for over 1 ms
+template <class F>
+hipError_t blocked(const char* what, F&& f) {
+  if (!tracing()) return f();
+  const double t = now_ms();
+  const hipError_t e = f();
+  const double dt = now_ms() - t;
+  if (dt > 1.0) fprintf(stderr, "[cordahip] %s held the host %.2f ms\n", what, dt);
+  return e;
+}
 
 int hip_err(hipError_t e);
 hipError_t ensure_streams(Device& d);
@@ -337,6 +347,10 @@ struct DeviceIds {
   // called before a chunk's copies are enqueued (after = false: the id slices
   // the chunk ending at sig_end needs) and after them (after = true: a few more)
   std::function<hipError_t(uint64_t sig_end, bool after)> advance;
+  // called when the statuses of signatures [a, b) are final on the host (a
+  // chunk has finished): the per-transaction reduce of the transactions whose
+  // signatures all lie in [a, b) runs there, while later chunks verify
+  std::function<hipError_t(uint64_t a, uint64_t b)> done;
   hipEvent_t wait_for(uint64_t tx) const {  // the event after which transaction tx's id is on the device
     const size_t j = (size_t)(std::upper_bound(tx_bound.begin(), tx_bound.end(), tx) - tx_bound.begin());
     return ready[j ? j - 1 : 0];

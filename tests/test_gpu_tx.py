@@ -80,16 +80,20 @@ def test_signed_tx_semantics(engine, oracle):
     assert len(sig_st) == len(flat)
 
 
-@pytest.mark.parametrize("slices", ["1", "3", "16"])
+@pytest.mark.parametrize("slices", ["default", "1", "3", "16"])
 def test_signed_tx_id_slices(engine, oracle, slices, monkeypatch):
     """cordahip_signed_tx_verify with the tx ids in asynchronous slices that feed
-    the signature pipeline (CORDAHIP_TX_SLICES; the default is 16 from 65,536
-    transactions), the signatures in 7-lane pipeline chunks (CORDAHIP_TX_SIG_CHUNK)
-    that end mid-slice, each gathering its message rows on the GPU from the ids
-    in HBM after the slice holding its last transaction: results must not depend
-    on the slicing, including slices with no transactions and transactions
-    without signatures or components."""
-    monkeypatch.setenv("CORDAHIP_TX_SLICES", slices)
+    the signature pipeline (CORDAHIP_TX_SLICES uniform slices; the default is one
+    slice per signature chunk), the signatures in 7-lane pipeline chunks
+    (CORDAHIP_TX_SIG_CHUNK) that end mid-slice and mid-transaction, each gathering
+    its message rows on the GPU from the ids in HBM after the slice holding its
+    last transaction, each finished chunk reducing the transactions it holds
+    whole: results must not depend on the slicing, including slices with no
+    transactions and transactions without signatures or components."""
+    if slices == "default":
+        monkeypatch.delenv("CORDAHIP_TX_SLICES", raising=False)
+    else:
+        monkeypatch.setenv("CORDAHIP_TX_SLICES", slices)
     monkeypatch.setenv("CORDAHIP_TX_SIG_CHUNK", "7")
     rng = random.Random(31)
     txs = [[bytes(rng.getrandbits(8) for _ in range(n)) for n in (120, 60, 43)] for _ in range(150)]
