@@ -387,7 +387,7 @@ hipError_t tx_ids_prepare(Device& d, const cordahip_txid_batch* b, const std::ve
 
 hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound, size_t j0,
                           size_t j1, std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& cev,
-                          std::vector<hipEvent_t>& kev) {
+                          std::vector<hipEvent_t>& kev, uint8_t* map_txid, uint8_t* map_status) {
   const uint64_t t0 = bound.front();
   const uint64_t l0 = b->tx_leaf_off[t0], b0 = b->leaf_off[l0];
   TxWork& w = d.tx;
@@ -415,7 +415,10 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
     e = e ? e : launch_merkle_root(hash_base, w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), ts1 - ts0,
                                    w.txid.as<uint8_t>() + (ts0 - t0) * 32, w.tx_status.as<uint8_t>() + (ts0 - t0), s);
     e = e ? e : hipEventRecord(kev[j], s);  // the slice's ids are in HBM: its signatures may gather them
-    if (ts1 > ts0) {
+    if (ts1 > ts0 && map_txid && map_status) {  // pinned caller arrays: stored by a kernel
+      e = e ? e : launch_store_to_host(w.txid.as<uint8_t>() + (ts0 - t0) * 32, map_txid + ts0 * 32, (ts1 - ts0) * 32, s);
+      e = e ? e : launch_store_to_host(w.tx_status.as<uint8_t>() + (ts0 - t0), map_status + ts0, ts1 - ts0, s);
+    } else if (ts1 > ts0) {
       e = e ? e : blocked("ids D2H", [&] {
         return hipMemcpyAsync(b->txid + ts0 * 32, w.txid.as<uint8_t>() + (ts0 - t0) * 32, (ts1 - ts0) * 32, d2h, s);
       });
@@ -531,12 +534,14 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   // with every slice enqueued first, r04's first signature copies waited ~20 ms
   // behind all of C4's 1.05 GB of leaf bytes
   size_t issued = 0;
+  uint8_t* map_txid = static_cast<uint8_t*>(host_mapped(b->tx.txid));
+  uint8_t* map_status = static_cast<uint8_t*>(host_mapped(b->tx.tx_status));
   uint64_t lookahead = 1;  // r04_o: 1 slice ahead 73.6 M/s, 2 ahead 73.1
   if (const char* v = getenv("CORDAHIP_TX_SLICE_AHEAD")) lookahead = strtoull(v, nullptr, 10);
   auto issue_through = [&](size_t j) -> hipError_t {  // enqueue slices [issued, j]
     const size_t j1 = std::min<size_t>(slices, j + 1);
     hipError_t e = hipSuccess;
-    if (j1 > issued) e = tx_ids_enqueue(d, &b->tx, di.tx_bound, issued, j1, ev, cev, di.ready);
+    if (j1 > issued) e = tx_ids_enqueue(d, &b->tx, di.tx_bound, issued, j1, ev, cev, di.ready, map_txid, map_status);
     issued = std::max(issued, j1);
     return e;
   };

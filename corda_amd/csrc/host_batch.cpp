@@ -296,29 +296,17 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
       if (!*pe && hipEventCreateWithFlags(pe, hipEventDisableTiming) != hipSuccess) return CORDAHIP_ERR_HIP;
   HostPool& pool = *ctx->host;
   // Chunks whose rows are the lanes in order (one message length, Ed25519 only:
-  // the common JVM batch) skip the host scatter: the statuses go D2H straight
-  // into the caller's status array and the kernel's wave-ballot verdict words
-  // into its verdict array -- when those are pinned (a DMA into pageable memory
-  // would block this thread); the last, largest chunk's scatter was the exposed
-  // tail of the call.
-  auto pinned = [](const void* p) {
-    hipPointerAttribute_t at;
-    if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    return at.type == hipMemoryTypeHost;
-  };
-  // the kernels store into the caller's arrays through their device mapping
+  // the common JVM batch) skip the host scatter: a kernel stores the statuses
+  // straight into the caller's status array and the wave-ballot verdict words
+  // into its verdict array through their device mapping -- when those are
+  // pinned; the last, largest chunk's scatter was the exposed tail of the call.
   uint8_t* dst_status = nullptr;
   uint64_t* dst_verdict = nullptr;
-  bool out_pinned = !dev && pinned(b->status) && (!b->verdict || pinned(b->verdict));
-  if (out_pinned && hipHostGetDevicePointer(reinterpret_cast<void**>(&dst_status), b->status, 0) != hipSuccess)
-    out_pinned = false;
-  if (out_pinned && b->verdict &&
-      hipHostGetDevicePointer(reinterpret_cast<void**>(&dst_verdict), b->verdict, 0) != hipSuccess)
-    out_pinned = false;
-  (void)hipGetLastError();
+  if (!dev) {
+    dst_status = static_cast<uint8_t*>(host_mapped(b->status));
+    dst_verdict = b->verdict ? static_cast<uint64_t*>(host_mapped(b->verdict)) : nullptr;
+  }
+  const bool out_pinned = dst_status && (!b->verdict || dst_verdict);
   auto finish = [&](BatchStage& st) -> hipError_t {  // wait for the stage's chunk, scatter its statuses
     if (!st.pending) return hipSuccess;
     st.pending = false;
