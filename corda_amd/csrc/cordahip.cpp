@@ -490,7 +490,7 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   // (2^17 lanes: 2 waves x 1,024 SIMDs x 64), each waiting on device for the
   // slice that holds its last transaction. Slice-aligned chunks of ~156K C4
   // signatures ran 1.19 ladder rounds each, the second at 19% occupancy:
-  // 12.8 ns per signature against ~10 for whole rounds (profiles/r04_i trace).
+  // 12.8 ns per signature against ~10 for whole rounds (profiles/r04_f kernel trace, r04_i host trace).
   // The first chunk is half a round (the GPU starts after the leaf bytes of
   // 2^16 signatures' transactions, ~0.5 ms of PCIe), the rest one round, the
   // two Ed25519 streams overlapping one chunk's end-of-grid tail with the
