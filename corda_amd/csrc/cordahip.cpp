@@ -497,7 +497,10 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   // next chunk (r04_o: 73.6 M/s against 71.4 for 2^17 / 2^18 chunks).
   uint64_t chunk = 1u << 16;
   if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
-  for (uint64_t x = s0; x < s1; x += (x == s0 ? chunk : 2 * chunk)) di.chunk_bound.push_back(x);
+  // chunks double from `chunk` up to CORDAHIP_TX_SIG_CHUNK_MAX (default 2 x chunk)
+  uint64_t chunk_max = 2 * chunk;
+  if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK_MAX")) chunk_max = std::max<uint64_t>(chunk, strtoull(v, nullptr, 10));
+  for (uint64_t x = s0, c = chunk; x < s1; x += c, c = std::min(chunk_max, 2 * c)) di.chunk_bound.push_back(x);
   di.chunk_bound.push_back(s1);
   if (slices == 0 && s1 > s0) {
     // default: the id slices follow the chunks -- slice k ends with chunk k's
@@ -555,7 +558,7 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
     // so PCIe carries leaf bytes while the GPU verifies the chunk
     di.advance = [&](uint64_t sig_end, bool after) {
       // after: the slices of the next `lookahead` chunks' signatures
-      const uint64_t e = after ? std::min(s1, sig_end + lookahead * 2 * chunk) : sig_end;
+      const uint64_t e = after ? std::min(s1, sig_end + lookahead * chunk_max) : sig_end;
       const uint64_t tx = tx_of[e - 1];
       const size_t j = (size_t)(std::upper_bound(di.tx_bound.begin(), di.tx_bound.end(), tx) - di.tx_bound.begin()) - 1;
       return issue_through(j);
