@@ -478,7 +478,7 @@ void reduce_txs(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b, uint64_t t
 // host. (r03 waited for each slice's ids on the host and copied them back as
 // messages: the GPU sat idle ~5 ms per C4 step until the first signatures were
 // packed.)
-int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b, const uint64_t* tx_of,
+int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b, uint64_t* tx_of,
                      uint64_t lo, uint64_t hi, uint64_t slices) {
   std::lock_guard<std::mutex> g(d.tx_mu);  // d.tx (the ids) stays ours until every gather has run
   int r = tx_acquire_host(d);
@@ -488,13 +488,15 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   const uint64_t s0 = b->tx_sig_off[lo], s1 = b->tx_sig_off[hi];
   // signature chunks of whole full-occupancy rounds of the Ed25519 ladder
   // (2^17 lanes: 2 waves x 1,024 SIMDs x 64), each waiting on device for the
-  // slice that holds its last transaction. Slice-aligned chunks of ~156K C4
-  // signatures ran 1.19 ladder rounds each, the second at 19% occupancy:
-  // 12.8 ns per signature against ~10 for whole rounds (profiles/r04_f kernel trace, r04_i host trace).
-  // The first chunk is half a round (the GPU starts after the leaf bytes of
-  // 2^16 signatures' transactions, ~0.5 ms of PCIe), the rest one round, the
-  // two Ed25519 streams overlapping one chunk's end-of-grid tail with the
-  // next chunk (r04_o: 73.6 M/s against 71.4 for 2^17 / 2^18 chunks).
+  // slice that holds its last transaction. Uniform slices with slice-aligned
+  // chunks of ~156K C4 signatures ran 1.19 ladder rounds each, the second at
+  // 19% occupancy: 12.8 ns per signature against ~10 for whole rounds
+  // (profiles/r04_f kernel trace, r04_i host trace). The first chunk is half a
+  // round (the GPU starts after the leaf bytes of 2^16 signatures'
+  // transactions, ~0.5 ms of PCIe), the rest one round, the two Ed25519
+  // streams overlapping one chunk's end-of-grid tail with the next chunk
+  // (r04_o: 73.6 M/s against 71.4 for 2^17 / 2^18 chunks, both before the
+  // chunk-aligned slices that took it to 80.9, r04_p).
   uint64_t chunk = 1u << 16;
   if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
   // chunks double from `chunk` up to CORDAHIP_TX_SIG_CHUNK_MAX (default 2 x chunk)
@@ -510,7 +512,10 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
     // PCIe before the first kernel)
     di.tx_bound.push_back(lo);
     for (size_t c = 1; c + 1 < di.chunk_bound.size(); c++) {
-      const uint64_t t = tx_of[di.chunk_bound[c] - 1] + 1;
+      // one past the transaction holding the chunk's last signature (tx_of is
+      // not filled yet: it is built while slice 0 crosses PCIe)
+      const uint64_t t = (uint64_t)(std::upper_bound(b->tx_sig_off + lo, b->tx_sig_off + hi + 1,
+                                                     di.chunk_bound[c] - 1) - b->tx_sig_off);
       if (t > di.tx_bound.back() && t < hi) di.tx_bound.push_back(t);
     }
     di.tx_bound.push_back(hi);
@@ -550,6 +555,15 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   };
   if (r == CORDAHIP_SUCCESS && tx_ids_prepare(d, &b->tx, di.tx_bound) != hipSuccess) r = CORDAHIP_ERR_OUT_OF_MEMORY;
   if (r == CORDAHIP_SUCCESS && issue_through(0) != hipSuccess) r = CORDAHIP_ERR_HIP;
+  // each signature signs its transaction's id (SignedTransaction.kt:98): the
+  // pipeline finds it through tx_of, this shard's part built now, while the
+  // first slice's leaf bytes cross PCIe (~0.45 ms of host time for C4 that
+  // preceded every copy in r04_p)
+  if (r == CORDAHIP_SUCCESS)
+    ctx->host->parallel_for(hi - lo, 4096, [&](uint64_t x, uint64_t y) {
+      for (uint64_t t = lo + x; t < lo + y; t++)
+        for (uint64_t q = b->tx_sig_off[t]; q < b->tx_sig_off[t + 1]; q++) tx_of[q] = t;
+    });
   std::vector<std::pair<uint64_t, uint64_t>> reduced;  // tx ranges the chunks reduced
   if (r == CORDAHIP_SUCCESS && s1 > s0) {
     di.txid = d.tx.txid.as<uint8_t>();
@@ -624,10 +638,9 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   const uint64_t nsig = b->tx_sig_off[ntx];
   if (nsig && (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off)) return CORDAHIP_ERR_INVALID_ARG;
   const double t0 = tracing() ? now_ms() : 0;
-  // each signature signs its transaction's id (SignedTransaction.kt:98): the
-  // pipeline finds it through tx_of -- a per-thread buffer kept across calls
-  // (a fresh 20 MB vector per C4 call page-faulted for ~0.8 ms, 3.9 ms on the
-  // first calls)
+  // signature -> transaction (tx_of): a per-thread buffer kept across calls (a
+  // fresh 20 MB vector per C4 call page-faulted for ~0.8 ms, 3.9 ms on the first
+  // calls), each device filling its shard's part (signed_tx_device)
   thread_local std::unique_ptr<uint64_t[]> tl_tx_of;
   thread_local uint64_t tl_tx_of_cap = 0;
   if (nsig > tl_tx_of_cap) {
@@ -636,10 +649,6 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
     tl_tx_of_cap = nsig;
   }
   uint64_t* tx_of = tl_tx_of.get();
-  ctx->host->parallel_for(ntx, 4096, [&](uint64_t x, uint64_t y) {
-    for (uint64_t t = x; t < y; t++)
-      for (uint64_t s = b->tx_sig_off[t]; s < b->tx_sig_off[t + 1]; s++) tx_of[s] = t;
-  });
   const double t_of = tracing() ? now_ms() : 0;
   // per device: its contiguous tx shard in slices (CORDAHIP_TX_SLICES; default:
   // one slice per signature chunk) and, chunk by
