@@ -13,7 +13,7 @@ run() {  # name, env, workload
 }
 for spec in ${RUNS:-"c4h|X=1|c4h" "c4h_32k|CORDAHIP_TX_SIG_CHUNK=32768|c4h" "c4|X=1|c4" "c2h|X=1|c2h" "c2|X=1|c2"}; do
   IFS='|' read -r n e w <<< "$spec"
-  run $n "$e" $w || exit 1
+  run $n "$(echo "$e" | tr "+" " ")" $w || exit 1
 done
 if [ -z "$NOTRACE" ]; then
 CORDAHIP_TRACE=1 timeout -k 10 300 python -u bench.py --workload c4h --steps 3 --warmup 1 --no-cpu-baseline --no-clock > $O/c4h_traced.json 2> $O/c4h_traced.err || { echo "traced failed"; exit 1; }
