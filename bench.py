@@ -744,9 +744,10 @@ class C4H(C4):
         tb = _lib.TxidBatch(ntx, p[0], p[1], p[2], self.h_txid.data_ptr(), self.h_txst.data_ptr())
         self.b = _lib.SignedTxBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], self.h_sst.data_ptr(),
                                     self.h_fb.data_ptr())
+        leaves = ("native Kryo leaves, %.0f B per tx" % (self.leaf_bytes.numel() / ntx) if self.native
+                  else "5 leaves of %s B" % list(C4_LEAF_LENS))
         self.workload = ("C4 via the JVM boundary: cordahip_tx_submit over %d synthetic cash-issue txs per GPU in pinned "
-                         "host CSR memory (5 leaves of %s B, 1-3 Ed25519 signers; PCIe included)"
-                         % (ntx, list(C4_LEAF_LENS)))
+                         "host CSR memory (%s, 1-3 Ed25519 signers; PCIe included)" % (ntx, leaves))
         self.config = dict(self.config, boundary="cordahip_tx_submit + cordahip_wait", host_memory="pinned CSR")
 
     def step(self):
