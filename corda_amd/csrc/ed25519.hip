@@ -472,7 +472,10 @@ CDEV void store_table8(uint32_t* __restrict__ rec, const ge_p3& base) {
 // next starts: decode A -> table [k](-A) | strict decode R -> table [k](-R) |
 // SHA-512, h, S_eff, lattice reduction, e = c1 S_eff mod L. Lanes whose
 // status is already decided run the phases on the identity / zero scalars.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) ed25519_prep_half_kernel(
+#ifndef ED_PREP_WAVES
+#define ED_PREP_WAVES 2
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_PREP_WAVES))) ed25519_prep_half_kernel(
     const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
     uint32_t msg_len, uint64_t base, uint64_t m, const uint8_t* __restrict__ pre_status,
     uint8_t* __restrict__ status, uint32_t* __restrict__ ws, uint32_t empty_is_error) {
