@@ -372,7 +372,8 @@ class C4:
         g = torch.Generator(device=device)
         g.manual_seed(0xC0DA0004 + rank)
         nl = len(C4_LEAF_LENS)
-        self.native = bool(getattr(args, "native_leaves", False))
+        self.native = bool(getattr(args, "native_leaves", False)) or bool(getattr(args, "device_encode", False))
+        self.device_encode = bool(getattr(args, "device_encode", False))
         nsig = torch.randint(1, 4, (ntx,), dtype=torch.int64, device=device, generator=g)
         self.tx_sig_off = torch.zeros(ntx + 1, dtype=torch.int64, device=device)
         self.tx_sig_off[1:] = torch.cumsum(nsig, 0)
@@ -382,7 +383,7 @@ class C4:
             # real-shaped leaves: the five cash-issue components written by
             # cordahip_kryo_encode; the issuer / command signer / mustSign key is the
             # transaction's first signer, whose public key comes from a signing pass
-            from corda_amd.corpus import make_cash_issue_leaves
+            from corda_amd.corpus import cash_issue_items, make_cash_issue_leaves
             first = self.tx_sig_off[:-1]
             pubs0 = torch.empty((ntx, 32), dtype=torch.uint8, device=device)
             scratch = torch.empty((ntx, 64), dtype=torch.uint8, device=device)
@@ -390,14 +391,31 @@ class C4:
                                     pubs0, scratch, stream=stream)
             torch.cuda.synchronize(device)
             rng = np.random.default_rng(0xC0DA0004 + rank)
-            blob, off = make_cash_issue_leaves(pubs0.cpu().numpy(), rng.integers(0, 256, (ntx, 32), dtype=np.uint8),
-                                               rng.integers(0, 256, 32, dtype=np.uint8).tobytes(),
-                                               rng.integers(1, 10**9, ntx), rng.integers(-2**63, 2**63 - 1, ntx),
-                                               threads=min(16, _cores()))
+            comp = (pubs0.cpu().numpy(), rng.integers(0, 256, (ntx, 32), dtype=np.uint8),
+                    rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), rng.integers(1, 10**9, ntx),
+                    rng.integers(-2**63, 2**63 - 1, ntx))
             del pubs0, scratch
-            self.leaf_bytes = torch.from_numpy(blob).to(device)
-            self.leaf_off = torch.from_numpy(off.astype(np.int64)).to(device)
-            del blob, off
+            if self.device_encode:
+                # the components' payloads stay in HBM; every step encodes the leaves
+                # on the GPU (cordahip_kryo_encode_device) before hashing them
+                blob, items, self.layout = cash_issue_items(*comp)
+                self.host_blob, self.host_items = blob, items
+                self.d_blob = torch.from_numpy(blob).to(device)
+                it = items.reshape(-1).copy()
+                it["data"] += np.uint64(self.d_blob.data_ptr())
+                self.d_items = torch.from_numpy(it.view(np.uint8)).to(device)
+                self.n_items = it.size
+                self.leaf_off = torch.zeros(self.n_items + 1, dtype=torch.int64, device=device)
+                self.kstatus = torch.zeros(self.n_items, dtype=torch.uint8, device=device)
+                eng.kryo_encode_device(self.d_items, self.n_items, None, self.leaf_off, self.kstatus, group=nl,
+                                       stream=stream)  # sizes only
+                torch.cuda.synchronize(device)
+                self.leaf_bytes = torch.empty(int(self.leaf_off[-1]), dtype=torch.uint8, device=device)
+            else:
+                blob, off = make_cash_issue_leaves(*comp, threads=min(16, _cores()))
+                self.leaf_bytes = torch.from_numpy(blob).to(device)
+                self.leaf_off = torch.from_numpy(off.astype(np.int64)).to(device)
+                del blob, off
         else:
             per_tx = sum(C4_LEAF_LENS)
             self.leaf_bytes = torch.randint(0, 256, (ntx * per_tx,), dtype=torch.uint8, device=device, generator=g)
@@ -429,16 +447,23 @@ class C4:
         self.exp_status[t_bad] = 1
         self.exp_bad.scatter_reduce_(0, t_bad, idx_in_tx, reduce="amin", include_self=False)
         bad_tx = torch.randperm(ntx, device=device, generator=g)[:max(1, ntx // 200)]
-        pos = self.leaf_off[bad_tx * nl] + torch.randint(0, C4_LEAF_LENS[0], (bad_tx.numel(),), device=device,
-                                                         generator=g)  # inside the output leaf (>= 450 B either way)
-        self.leaf_bytes[pos] ^= 1
+        if self.device_encode:  # a flipped owner-key byte in the component: the re-encoded leaf differs
+            pos = (self.layout["owner_key"] + bad_tx * self.layout["cash_stride"]
+                   + torch.randint(0, 32, (bad_tx.numel(),), device=device, generator=g))
+            self.d_blob[pos] ^= 1
+        else:
+            pos = self.leaf_off[bad_tx * nl] + torch.randint(0, C4_LEAF_LENS[0], (bad_tx.numel(),), device=device,
+                                                             generator=g)  # inside the output leaf (>= 450 B either way)
+            self.leaf_bytes[pos] ^= 1
         self.exp_status[bad_tx] = 1
         self.exp_bad[bad_tx] = 0
         self.ntx, self.ns = ntx, ns
         self.units = ns
         self.macs = LIMB_MACS["ed25519"]
-        leaves = ("native Kryo leaves (cordahip_kryo_encode: TransactionState<Cash.State>, issue Command, notary "
-                  "Party, mustSign key, TransactionType; %.0f B per tx)" % (self.leaf_bytes.numel() / ntx)
+        leaves = ("native Kryo leaves (cordahip_kryo_encode%s: TransactionState<Cash.State>, issue Command, notary "
+                  "Party, mustSign key, TransactionType; %.0f B per tx)"
+                  % ("_device every step, from the components in HBM" if self.device_encode else "",
+                     self.leaf_bytes.numel() / ntx)
                   if self.native else "5 leaves of %s B" % list(C4_LEAF_LENS))
         self.workload = ("C4: SignedTransaction.verifySignatures on %d synthetic cash-issue txs per GPU "
                          "(%s, 1-3 Ed25519 signers; leaf SHA-256 + Merkle id + sigs + per-tx reduce)" % (ntx, leaves))
@@ -447,19 +472,41 @@ class C4:
                       "synthetic: seeded random leaf bytes of the SURVEY §8(d) C4 lengths") +
                      ", signatures made on the GPU over the GPU-computed ids; 0.5% sigs and 0.5% txs corrupted")
         self.config = {"txs_per_gpu": ntx, "sigs_per_gpu": ns,
-                       "leaf_bytes_per_tx": round(self.leaf_bytes.numel() / ntx, 1), "native_leaves": self.native}
+                       "leaf_bytes_per_tx": round(self.leaf_bytes.numel() / ntx, 1), "native_leaves": self.native,
+                       "device_encode": self.device_encode}
+        if self.device_encode:
+            self.kernel = "kryo_size + scan + kryo_write + " + C4.kernel
+            self.config["component_bytes_per_tx"] = round(self.d_blob.numel() / ntx, 1)
         if not self.native:
             self.config["leaf_lens"] = list(C4_LEAF_LENS)
 
     def step(self):
+        if self.device_encode:
+            self.eng.kryo_encode_device(self.d_items, self.n_items, self.leaf_bytes, self.leaf_off, self.kstatus,
+                                        group=len(C4_LEAF_LENS), device=0, stream=self.stream)
         self.eng.signed_tx_verify_ed25519_device(self.leaf_bytes, self.leaf_off, self.tx_leaf_off, self.tx_sig_off,
                                                  self.keys, self.sigs, self.txid, self.tx_status, self.first_bad,
                                                  self.sig_status, device=0, stream=self.stream)
 
     def check(self):
-        return {"mismatches_vs_construction": int((self.tx_status != self.exp_status).sum())
-                + int((self.first_bad != self.exp_bad).sum()),
-                "accepted_txs": int((self.tx_status == 0).sum()), "txs": self.ntx, "sigs": self.ns}
+        out = {"mismatches_vs_construction": int((self.tx_status != self.exp_status).sum())
+               + int((self.first_bad != self.exp_bad).sum()),
+               "accepted_txs": int((self.tx_status == 0).sum()), "txs": self.ntx, "sigs": self.ns}
+        if getattr(self, "device_encode", False):
+            # the GPU's leaves of the first 20,000 transactions against the host encoder
+            # (cordahip_kryo_encode) over the same (corrupted) components
+            from corda_amd import _lib
+            k = min(self.ntx, 20000) * len(C4_LEAF_LENS)
+            blob = self.d_blob.cpu().numpy()
+            it = self.host_items.reshape(-1)[:k].copy()
+            it["data"] += np.uint64(blob.ctypes.data)
+            hb, ho = _lib.kryo_encode_array(it)
+            lo = self.leaf_off[:k + 1].cpu().numpy().astype(np.uint64)
+            out["kryo_item_errors"] = int((self.kstatus != 0).sum())
+            out["leaf_mismatches_vs_host_encoder"] = int(not (np.array_equal(lo, ho) and np.array_equal(
+                self.leaf_bytes[:int(lo[-1])].cpu().numpy(), hb)))
+            out["leaves_checked_vs_host_encoder"] = k
+        return out
 
     def cpu_baseline(self, sample):
         import ctypes
@@ -728,6 +775,8 @@ class C4H(C4):
 
     def __init__(self, eng, device, stream, rank, args):
         from corda_amd import _lib
+        if getattr(args, "device_encode", False):
+            raise SystemExit("--device-encode is a c4 option: c4h hands the library leaf bytes in host memory")
         super().__init__(eng, device, stream, rank, args)
         ntx, ns = self.ntx, self.ns
         ar = np.arange(ns + 1, dtype=np.uint64)
@@ -905,6 +954,9 @@ def main():
     ap.add_argument("--c4-txs", type=int, default=10_000_000 // 8)
     ap.add_argument("--native-leaves", action="store_true",
                     help="c4 / c4h: real-shaped cash-issue leaves from the native Kryo encoder (SURVEY 8f-4)")
+    ap.add_argument("--device-encode", action="store_true",
+                    help="c4: native leaves encoded on the GPU every step from the components in HBM "
+                         "(cordahip_kryo_encode_device; implies --native-leaves)")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock sampling step")

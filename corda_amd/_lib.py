@@ -34,7 +34,7 @@ EXPORTS = [
     "cordahip_tx_ids", "cordahip_signed_tx_verify", "cordahip_signed_tx_verify_ed25519_device",
     "cordahip_ecdsa_verify_device", "cordahip_stream_verify", "cordahip_filtered_tx_verify",
     "cordahip_tx_submit", "cordahip_txid_submit", "cordahip_filtered_tx_submit", "cordahip_shard_range",
-    "cordahip_kryo_encode",
+    "cordahip_kryo_encode", "cordahip_kryo_encode_device",
 ]
 ERR_BUFFER_TOO_SMALL = -8
 # cordahip_kryo_item kinds (CORDAHIP_KRYO_*)
@@ -167,6 +167,7 @@ def lib() -> ctypes.CDLL:
         "cordahip_filtered_tx_submit": (i32, [vp, ctypes.POINTER(FilteredTxBatch), ctypes.POINTER(u64)]),
         "cordahip_shard_range": (None, [u64, u32, u32, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "cordahip_kryo_encode": (i32, [ctypes.POINTER(KryoItem), u64, vp, u64, vp]),
+        "cordahip_kryo_encode_device": (i32, [vp, i32, vp, u64, u32, vp, u64, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(l, name)
@@ -195,12 +196,12 @@ def kryo_encode_array(items):
     assert items.dtype == KRYO_ITEM_DTYPE and KRYO_ITEM_DTYPE.itemsize == ctypes.sizeof(KryoItem)
     off = np.zeros(n + 1, np.uint64)
     cap = int(items["len"].sum()) * 3 + 256 * n + 64
-    out = np.zeros(cap, np.uint8)
+    out = np.empty(cap, np.uint8)
     rc = lib().cordahip_kryo_encode(ctypes.cast(items.ctypes.data, ctypes.POINTER(KryoItem)), n, out.ctypes.data, cap,
                                     off.ctypes.data)
     if rc == ERR_BUFFER_TOO_SMALL:
         cap = int(off[n])
-        out = np.zeros(cap, np.uint8)
+        out = np.empty(cap, np.uint8)
         rc = lib().cordahip_kryo_encode(ctypes.cast(items.ctypes.data, ctypes.POINTER(KryoItem)), n, out.ctypes.data, cap,
                                     off.ctypes.data)
     check(rc, "cordahip_kryo_encode")
@@ -227,57 +228,62 @@ def pack_cash_state(d):
             + (0 if enc is None else int(enc)).to_bytes(4, "little", signed=True))
 
 
-def kryo_encode(items):
-    """Leaf preimages of transaction components (cordahip_kryo_encode; host only, no
-    device). items: (kind, value, class_id) with kind a KRYO_KINDS key; value: bytes
-    for raw / keys, str for String / kotlin_object (and char), int otherwise
-    (float / double: their IEEE bits). Returns the list of leaves (bytes)."""
-    import numpy as np
+def kryo_pack(items):
+    """(kind, value, class_id) tuples -> (payload blob uint8, KRYO_ITEM_DTYPE[n] whose `data` are
+    OFFSETS into the blob, bool[n]: the item has a payload). kind: a KRYO_KINDS key; value: bytes
+    for raw / keys, str for String / kotlin_object (and char), int otherwise (float / double: their
+    IEEE bits). Rebase `data` onto the blob's host or device address before encoding."""
     n = len(items)
-    arr = (KryoItem * max(n, 1))()
-    keep = []
+    arr = np.zeros(n, KRYO_ITEM_DTYPE)
+    has = np.zeros(n, bool)
+    parts = []
+    pos = 0
     for i, (kind, value, class_id) in enumerate(items):
-        it = arr[i]
-        it.kind, it.class_id = KRYO_KINDS[kind], class_id
+        arr[i]["kind"], arr[i]["class_id"] = KRYO_KINDS[kind], class_id
+        b = None
         if kind in ("String", "kotlin_object"):
             b = value.encode("utf-16-le")
-            it.len = len(b) // 2
+            arr[i]["len"] = len(b) // 2
         elif kind in ("raw", "ed25519_key", "public_key"):
             b = bytes(value)
-            it.len = len(b)
+            arr[i]["len"] = len(b)
         elif kind == "party":  # value = (X.500 name DER, key bytes, key class id); class_id = X500Name's id
             name_der, key, key_class = value
             b = bytes(name_der) + bytes(key)
-            it.len = len(b)
-            it.value = key_class
+            arr[i]["len"] = len(b)
+            arr[i]["value"] = key_class
         elif kind == "issue_command":  # value = (class name, nonce, [(key class id, key bytes)]); class_id = Arrays$ArrayList's
             cls, nonce, keys = value
             nm = cls.encode("ascii")
             b = bytes([len(nm)]) + nm + bytes([len(keys)]) + b"".join(
                 int(kc).to_bytes(2, "little") + len(k).to_bytes(2, "little") + bytes(k) for kc, k in keys)
-            it.len = len(b)
-            it.value = nonce
+            arr[i]["len"] = len(b)
+            arr[i]["value"] = nonce
         elif kind == "cash_state":  # value = a dict (pack_cash_state); class_id = X500Name's id
             b = pack_cash_state(value)
-            it.len = len(b)
-            it.value = int(value["quantity"])
+            arr[i]["len"] = len(b)
+            arr[i]["value"] = int(value["quantity"])
         else:
-            b = None
-            it.value = ord(value) if (kind == "char" and isinstance(value, str)) else int(value)
+            arr[i]["value"] = ord(value) if (kind == "char" and isinstance(value, str)) else int(value)
         if b is not None:
-            buf = ctypes.create_string_buffer(b, max(len(b), 1))
-            keep.append(buf)
-            it.data = ctypes.addressof(buf)
-    off = np.zeros(n + 1, np.uint64)
-    cap = 0
-    rc = lib().cordahip_kryo_encode(arr, n, None, 0, off.ctypes.data)
-    if rc == ERR_BUFFER_TOO_SMALL:
-        cap = int(off[n])
-        out = np.zeros(cap, np.uint8)
-        rc = lib().cordahip_kryo_encode(arr, n, out.ctypes.data, cap, off.ctypes.data)
-    else:
-        out = np.zeros(1, np.uint8)
-    check(rc, "cordahip_kryo_encode")
+            has[i] = True
+            arr[i]["data"] = pos
+            parts.append(b)
+            pos += len(b)
+    blob = np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy()
+    return blob, arr, has
+
+
+def kryo_encode(items):
+    """Leaf preimages of transaction components (cordahip_kryo_encode; host only, no
+    device). items as kryo_pack takes them. Returns the list of leaves (bytes)."""
+    n = len(items)
+    blob, arr, has = kryo_pack(items)
+    arr["data"] = np.where(has, arr["data"] + np.uint64(blob.ctypes.data), 0)
+    if n == 0:
+        return []
+    out, off = kryo_encode_array(arr)
+    del blob
     return [out[int(off[i]):int(off[i + 1])].tobytes() for i in range(n)]
 
 

@@ -300,16 +300,16 @@ def x500_name(org: str, locality: str, country: str) -> bytes:
     return _der(0x30, out)
 
 
-def make_cash_issue_leaves(issuer_keys: np.ndarray, owner_keys: np.ndarray, notary_key: bytes,
-                           quantities: np.ndarray, nonces: np.ndarray, threads: int = 8):
-    """CSR leaf bytes of ntx cash-issue transactions: issuer_keys[t] (Ed25519 A) issues
-    quantities[t] USD cents (issue reference 01) to the anonymised owner_keys[t]
-    (an AnonymousParty, as CashIssueFlow's default confidential recipient), notary
-    "Notary Service, Zurich, CH"; the command signer and mustSign key = the issuer key.
-    Returns (leaf_bytes uint8, leaf_off uint64[5 * ntx + 1])."""
-    import ctypes
-    from concurrent.futures import ThreadPoolExecutor
-
+def cash_issue_items(issuer_keys: np.ndarray, owner_keys: np.ndarray, notary_key: bytes, quantities: np.ndarray,
+                     nonces: np.ndarray):
+    """The five cordahip_kryo_items of each of ntx cash-issue transactions (TransactionState<Cash.State>,
+    the issue Command, the notary Party, the mustSign key, TransactionType.General) with their payloads
+    in ONE byte blob: returns (blob uint8, items KRYO_ITEM_DTYPE[ntx, 5]) whose `data` fields are
+    OFFSETS into the blob (add the blob's address -- host or device -- before encoding), and the
+    blob layout of the owner keys ({"owner_key": tx 0's offset, "cash_stride": bytes per tx}).
+    issuer_keys[t] (Ed25519 A) issues quantities[t] USD cents (issue reference 01) to the anonymised
+    owner_keys[t] (an AnonymousParty, as CashIssueFlow's default confidential recipient), notary
+    "Notary Service, Zurich, CH"; the command signer and mustSign key = the issuer key."""
     from corda_amd import _lib
     ntx = len(issuer_keys)
     ik = np.ascontiguousarray(issuer_keys, np.uint8).reshape(ntx, 32)
@@ -333,8 +333,11 @@ def make_cash_issue_leaves(issuer_keys: np.ndarray, owner_keys: np.ndarray, nota
     cash[:, oo:oo + 32] = ok
     cmd = np.tile(cmd_t, (ntx, 1))
     cmd[:, oc:oc + 32] = ik
-    party = np.frombuffer(notary + bytes(notary_key), np.uint8).copy()
-    gen = np.frombuffer(TRANSACTION_TYPE_GENERAL.encode("utf-16-le"), np.uint8).copy()
+    party = np.frombuffer(notary + bytes(notary_key), np.uint8)
+    gen = np.frombuffer(TRANSACTION_TYPE_GENERAL.encode("utf-16-le"), np.uint8)
+    parts = [cash.reshape(-1), cmd.reshape(-1), ik.reshape(-1), party, gen]
+    base = np.cumsum([0] + [p.size for p in parts])
+    blob = np.concatenate(parts)
     items = np.zeros((ntx, 5), _lib.KRYO_ITEM_DTYPE)
     kinds = [_lib.KRYO_KINDS[k] for k in ("cash_state", "issue_command", "party", "ed25519_key", "kotlin_object")]
     items["kind"] = kinds
@@ -343,26 +346,42 @@ def make_cash_issue_leaves(issuer_keys: np.ndarray, owner_keys: np.ndarray, nota
     items["value"][:, 1] = nonces
     items["value"][:, 2] = ed  # the notary key's class
     t = np.arange(ntx, dtype=np.uint64)
-    items["data"][:, 0] = cash.ctypes.data + t * cash.shape[1]
+    items["data"][:, 0] = base[0] + t * cash.shape[1]
     items["len"][:, 0] = cash.shape[1]
-    items["data"][:, 1] = cmd.ctypes.data + t * cmd.shape[1]
+    items["data"][:, 1] = base[1] + t * cmd.shape[1]
     items["len"][:, 1] = cmd.shape[1]
-    items["data"][:, 2] = party.ctypes.data
+    items["data"][:, 2] = base[3]
     items["len"][:, 2] = party.size
-    items["data"][:, 3] = ik.ctypes.data + t * 32
+    items["data"][:, 3] = base[2] + t * 32
     items["len"][:, 3] = 32
-    items["data"][:, 4] = gen.ctypes.data
+    items["data"][:, 4] = base[4]
     items["len"][:, 4] = gen.size // 2
+    # where transaction t's owner key sits in the blob (bench corruption: a flipped
+    # key byte changes the output leaf and so the id, as a flipped leaf byte does)
+    layout = {"owner_key": base[0] + oo, "cash_stride": cash.shape[1]}
+    return blob, items, layout
+
+
+def make_cash_issue_leaves(issuer_keys: np.ndarray, owner_keys: np.ndarray, notary_key: bytes,
+                           quantities: np.ndarray, nonces: np.ndarray, threads: int = 8):
+    """CSR leaf bytes of the ntx cash-issue transactions of cash_issue_items, encoded on the host
+    (cordahip_kryo_encode, `threads` at a time). Returns (leaf_bytes uint8, leaf_off uint64[5 * ntx + 1])."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from corda_amd import _lib
+    ntx = len(issuer_keys)
+    blob, items, _ = cash_issue_items(issuer_keys, owner_keys, notary_key, quantities, nonces)
+    items["data"] += np.uint64(blob.ctypes.data)
     flat = items.reshape(-1)
     per = max(1, -(-ntx // (threads * 4)))
     parts = [(a * 5, min(ntx, a + per) * 5) for a in range(0, ntx, per)]
     with ThreadPoolExecutor(threads) as ex:
         outs = list(ex.map(lambda r: _lib.kryo_encode_array(flat[r[0]:r[1]]), parts))
-    blob = np.concatenate([b for b, _ in outs]) if outs else np.zeros(0, np.uint8)
+    out = np.concatenate([b for b, _ in outs]) if outs else np.zeros(0, np.uint8)
     off = np.zeros(5 * ntx + 1, np.uint64)
     base = 0
     for (a, b), (bb, oo_) in zip(parts, outs):
         off[a + 1:b + 1] = oo_[1:] + base
         base += len(bb)
-    del cash, cmd, party, gen  # the encoder copied everything
-    return blob, off
+    del blob  # the encoder copied everything
+    return out, off

@@ -22,6 +22,7 @@
 #include <cstring>
 
 #include "der.hpp"
+#include "kryo_core.hpp"
 #include "runtime.hpp"
 #include "status.hpp"
 
@@ -879,9 +880,9 @@ void free_device(Device& d) {
                     &d.tx.tx_sig_off, &d.tx.msgs, &d.tx.tok, &d.tx.tok_hash, &d.tx.tx_tok_off, &d.tx.root,
                     &d.tx.stack})
     b->release();
-  for (DevBuf* b : {&d.ec.counters, &d.ec.perm, &d.ec.ws}) b->release();
+  for (DevBuf* b : {&d.ec.counters, &d.ec.perm, &d.ec.ws, &d.kryo_sizes, &d.kryo_temp, &d.kryo_ws}) b->release();
   for (auto& w : d.ed_ws) w.release();
-  for (hipEvent_t ev : {d.ec.ev, d.ed_ev[0], d.ed_ev[1], d.tx_ev})
+  for (hipEvent_t ev : {d.ec.ev, d.ed_ev[0], d.ed_ev[1], d.tx_ev, d.kryo_ev})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& tc : d.ring)
     for (hipEvent_t ev : {tc.a, tc.b})
@@ -1250,6 +1251,45 @@ int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, cons
                                ntx, static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);
   e = e ? e : hipEventRecord(tc->b, s);
   return hip_err(e);
+}
+
+int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_items, uint64_t n, uint32_t group,
+                                void* d_out, uint64_t cap, void* d_off, void* d_status, void* hip_stream) {
+  Device* d = dev_at(ctx, device);
+  if (!d || !d_off || (n && (!d_items || !d_status))) return CORDAHIP_ERR_INVALID_ARG;
+  return guarded([&]() -> int {
+    std::lock_guard<std::mutex> g(d->kryo_mu);
+    if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (!d->kryo_ev && hipEventCreateWithFlags(&d->kryo_ev, hipEventDisableTiming) != hipSuccess)
+      return CORDAHIP_ERR_HIP;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    // writers: one per leaf up to 2^18 (kLevelBytes each: 2 GB of level buffers)
+    const uint64_t ws_threads = std::max<uint64_t>(256, (std::min<uint64_t>(n, 1u << 18) + 255) / 256 * 256);
+    size_t temp_bytes = 0;
+    if (kryo_scan(nullptr, temp_bytes, nullptr, nullptr, n + 1, s) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (d->kryo_sizes.cap < (n + 1) * 8 || d->kryo_temp.cap < temp_bytes ||
+        d->kryo_ws.cap < ws_threads * cordahip::kryo::kLevelBytes) {
+      // growing frees the old buffers: the previous user's kernels must be done
+      if (hipEventSynchronize(d->kryo_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
+      if (d->kryo_sizes.ensure((n + 1) * 8) || d->kryo_temp.ensure(std::max<size_t>(temp_bytes, 16)) ||
+          d->kryo_ws.ensure(ws_threads * cordahip::kryo::kLevelBytes))
+        return CORDAHIP_ERR_OUT_OF_MEMORY;
+    }
+    TimedCall* tc = timed_begin(*d, s);
+    if (!tc) return CORDAHIP_ERR_HIP;
+    const auto* items = static_cast<const cordahip_kryo_item*>(d_items);
+    uint64_t* sizes = d->kryo_sizes.as<uint64_t>();
+    uint8_t* status = static_cast<uint8_t*>(d_status);
+    hipError_t e = hipStreamWaitEvent(s, d->kryo_ev, 0);  // the previous user of the scratch is done
+    e = e ? e : launch_kryo_size(items, n, group, sizes, status, s);
+    size_t tb = d->kryo_temp.cap;
+    e = e ? e : kryo_scan(d->kryo_temp.p, tb, sizes, static_cast<uint64_t*>(d_off), n + 1, s);
+    e = e ? e : launch_kryo_write(items, n, group, static_cast<const uint64_t*>(d_off), static_cast<uint8_t*>(d_out),
+                                  d_out ? cap : 0, status, d->kryo_ws.as<uint8_t>(), ws_threads, s);
+    e = e ? e : hipEventRecord(d->kryo_ev, s);
+    e = e ? e : hipEventRecord(tc->b, s);
+    return hip_err(e);
+  });
 }
 
 }  // extern "C"

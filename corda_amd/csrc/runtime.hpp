@@ -39,6 +39,14 @@ hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uin
 hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
                               hipStream_t s);
 hipError_t launch_store_to_host(const void* src, void* dst, uint64_t n, hipStream_t s);
+// kryo_device.hip: the GPU Kryo leaf encoder (sizes, scan, writes)
+hipError_t launch_kryo_size(const cordahip_kryo_item* items, uint64_t n, uint32_t group, uint64_t* sizes,
+                            uint8_t* status, hipStream_t s);
+hipError_t kryo_scan(void* temp, size_t& temp_bytes, const uint64_t* sizes, uint64_t* off, uint64_t n1,
+                     hipStream_t s);
+hipError_t launch_kryo_write(const cordahip_kryo_item* items, uint64_t n, uint32_t group, const uint64_t* off,
+                             uint8_t* out, uint64_t cap, uint8_t* status, uint8_t* ws, uint64_t ws_threads,
+                             hipStream_t s);
 hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s);
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
                             uint8_t* tx_status, hipStream_t s);
@@ -212,6 +220,12 @@ struct Device {
   std::mutex ped_mu, pb_mu;
   PackStage ped[kPackStages];   // dense Ed25519 rows (cordahip_ed25519_verify_host)
   BatchStage pb[kPackStages];   // generic CSR batches (cordahip_sig_verify / _submit)
+  // GPU Kryo encoder scratch (cordahip_kryo_encode_device): leaf sizes, the
+  // scan's temporary storage, the writers' OutputChunked level buffers;
+  // kryo_mu orders the enqueues, kryo_ev fences reuse
+  std::mutex kryo_mu;
+  DevBuf kryo_sizes, kryo_temp, kryo_ws;
+  hipEvent_t kryo_ev = nullptr;
 };
 
 // Fork-join pool for host-side packing and scattering. parallel_for splits

@@ -168,6 +168,40 @@ class Engine:
             sigs.data_ptr(), keys.shape[0], txid.data_ptr(), tx_status.data_ptr(), first_bad.data_ptr(),
             sig_status.data_ptr(), s), "cordahip_signed_tx_verify_ed25519_device")
 
+    def kryo_encode_device(self, items, n: int, out, off, status, group: int = 1, device: int = 0, stream=None):
+        """cordahip_kryo_encode_device: leaf preimages of n components on the GPU. items: a
+        device tensor holding n cordahip_kryo_item records (_lib.KRYO_ITEM_DTYPE) whose data
+        pointers are device addresses; out: uint8 device tensor (its size is the cap); off:
+        n + 1 int64; status: n uint8 (0 written, 1 invalid item, 2 beyond cap)."""
+        s = stream.cuda_stream if stream is not None else 0
+        check(lib().cordahip_kryo_encode_device(self._ctx, device, items.data_ptr(), n, group,
+                                                out.data_ptr() if out is not None else None,
+                                                out.numel() if out is not None else 0, off.data_ptr(),
+                                                status.data_ptr(), s), "cordahip_kryo_encode_device")
+
+    def kryo_encode_packed_device(self, blob, items, has, group: int = 1, cap=None, device: int = 0, stream=None):
+        """_lib.kryo_pack output (payload blob, items with blob offsets, has-payload mask) encoded on
+        the GPU: the blob and the rebased items go to the device, then cordahip_kryo_encode_device.
+        cap None: sized by a first pass. Synchronous (returns host-visible results): (leaves uint8
+        device tensor, off int64 device tensor [n + 1], status uint8 device tensor [n])."""
+        import torch
+        dev = torch.device("cuda", device)
+        d_blob = torch.from_numpy(np.ascontiguousarray(blob)).to(dev)
+        a = np.array(items, copy=True)
+        a["data"] = np.where(has, a["data"] + np.uint64(d_blob.data_ptr()), 0)
+        d_items = torch.from_numpy(a.view(np.uint8)).to(dev)
+        n = len(a)
+        off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        status = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
+        if cap is None:
+            self.kryo_encode_device(d_items, n, None, off, status, group, device, stream)
+            torch.cuda.synchronize(dev)
+            cap = int(off[n])
+        out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+        self.kryo_encode_device(d_items, n, out, off, status, group, device, stream)
+        torch.cuda.synchronize(dev)
+        return out[:cap], off, status[:n]
+
     def ecdsa_verify_device(self, scheme, keys, key_len, sigs, sig_len, msgs, status, verdict=None, device: int = 0,
                             stream=None):
         """Dense mixed secp256k1/P-256 batch in HBM: keys [n,65] + key_len, DER sigs [n,72] + sig_len."""

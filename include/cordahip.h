@@ -376,6 +376,20 @@ typedef struct {
 } cordahip_kryo_item;
 int cordahip_kryo_encode(const cordahip_kryo_item* items, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* off);
 
+/* The same leaf preimages computed on the GPU, for components whose payloads
+ * are already in device memory (a transaction batch's ids then need neither
+ * host serialisation nor leaf bytes over PCIe). d_items: n items in device
+ * memory whose `data` are device pointers; group: the items come as records of
+ * `group` components (e.g. the 5 of a cash-issue transaction) -- a thread
+ * mapping hint, 1 = none. Writes d_off[0..n] (uint64, the CSR offsets; d_off[n]
+ * = the bytes of all leaves) and d_status[i] (uint8): 0 written, 1 invalid item
+ * (as cordahip_kryo_encode would reject it; size 0), 2 not written because it
+ * ends beyond cap. Enqueued on hip_stream, asynchronous; the caller reads
+ * d_off[n] / d_status when it needs them. Same encoder as cordahip_kryo_encode
+ * (corda_amd/csrc/kryo_core.hpp): bit-identical leaves. */
+int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_items, uint64_t n, uint32_t group,
+                                void* d_out, uint64_t cap, void* d_off, void* d_status, void* hip_stream);
+
 /* Device time (ms) of the calling thread's most recent *_device call on
  * `device`, from HIP events recorded around its launches on the stream it ran
  * on (waits for them); -1 if the thread made no such call. Each call gets its

@@ -1,0 +1,125 @@
+"""The GPU Kryo leaf encoder (cordahip_kryo_encode_device) against the host one
+(cordahip_kryo_encode, itself checked against the Python restatement of Kryo
+4.0.0 in tests/test_kryo.py) and the restatement directly: both sides run the
+same encoder core (kryo_core.hpp), so every leaf must be bit-identical -- every
+component kind, cash states whose X.500 names cross the 1,024-byte chunk
+buffers, invalid items (status 1, size 0), leaves beyond the output's capacity
+(status 2, not written), the record-major thread mapping (group 5), and the
+leaves feeding the transaction ids of the device signed-tx path. Parity beyond
+the key bytes stays UNPINNED (no Kryo here), as for the host encoder."""
+import random
+import struct
+
+import numpy as np
+import pytest
+
+import kryo_leaves as K
+import test_kryo as TK
+from corda_amd import _lib
+from corda_amd.corpus import cash_issue_items, make_cash_issue_leaves
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(k, v):  # the library takes float / double as their IEEE bits
+    if k == "float":
+        return struct.unpack(">i", struct.pack(">f", v))[0]
+    if k == "double":
+        return struct.unpack(">q", struct.pack(">d", v))[0]
+    return v
+
+
+def _mixed_items(rng):
+    """(items as the restatement takes them, the same items as the library takes them)"""
+    ref_keys = [bytes.fromhex(v["A"]) for v in TK._key_vectors()]
+    items = TK._random_items(rng)
+    for i in range(60):
+        items.append(("cash_state", TK._cash_state(rng, ref_keys, big=i % 7 == 0), rng.randrange(20, 300)))
+        items.append(("party", TK._party(rng, ref_keys, big=i % 11 == 0), 50))
+        items.append(("issue_command", ("net.corda.contracts.asset.Cash$Commands$Issue", rng.randrange(-2**63, 2**63),
+                                        [(45, rng.choice(ref_keys)) for _ in range(rng.randrange(1, 4))]), 10))
+    rng.shuffle(items)
+    return items, [(k, _bits(k, v), c) for k, v, c in items]
+
+
+def _leaves(out, off, n):
+    o = off.cpu().numpy()
+    b = out.cpu().numpy()
+    return [b[int(o[i]):int(o[i + 1])].tobytes() for i in range(n)]
+
+
+def test_every_kind_matches_the_host_encoder(engine):
+    rng = random.Random(77)
+    spec, items = _mixed_items(rng)
+    host = _lib.kryo_encode(items)
+    blob, arr, has = _lib.kryo_pack(items)
+    out, off, status = engine.kryo_encode_packed_device(blob, arr, has)
+    assert int(status.sum()) == 0
+    got = _leaves(out, off, len(items))
+    assert got == host
+    # and the restatement itself, kind by kind
+    for (k, v, c), g in zip(spec, got):
+        assert g == K.leaf(k, v, c), (k, g.hex())
+    assert any(len(g) > 2100 for g in got)  # names crossing the chunk buffers
+
+
+def test_invalid_items_and_capacity(engine):
+    rng = random.Random(5)
+    ref_keys = [bytes.fromhex(v["A"]) for v in TK._key_vectors()]
+    good = [("cash_state", TK._cash_state(rng, ref_keys), 52) for _ in range(20)]
+    d = TK._cash_state(rng, ref_keys)
+    bad = [("cash_state", dict(d, reference=b""), 52),                   # empty issue reference
+           ("ed25519_key", b"k" * 31, 47),                               # not 32 bytes
+           ("issue_command", ("net.corda.X$Issue", 1, []), 10)]          # no signers
+    items = good[:10] + bad + good[10:]
+    blob, arr, has = _lib.kryo_pack(items)
+    out, off, status = engine.kryo_encode_packed_device(blob, arr, has)
+    st = status.cpu().numpy()
+    assert list(st[10:13]) == [1, 1, 1] and (np.delete(st, [10, 11, 12]) == 0).all()
+    o = off.cpu().numpy()
+    assert (o[11:14] == o[10]).all()  # invalid items take no bytes
+    host = _lib.kryo_encode(good)
+    got = _leaves(out, off, len(items))
+    assert got[:10] + got[13:] == host
+    # a buffer that holds only the first 7 leaves: the rest are not written (status 2)
+    cap = int(o[7])
+    out2, off2, status2 = engine.kryo_encode_packed_device(blob, arr, has, cap=cap)
+    st2 = status2.cpu().numpy()
+    assert (st2[:7] == 0).all() and (st2[7:10] == 2).all() and list(st2[10:13]) == [1, 1, 1] and (st2[13:] == 2).all()
+    assert _leaves(out2, off2, 7) == host[:7]
+    assert int(off2[-1]) == int(o[-1])  # off[n] is the full size either way
+
+
+def test_cash_issue_records_feed_tx_ids(engine):
+    """The bench's native C4 corpus (5 components per transaction, group 5: the
+    threads of a wave take one kind): device leaves = host leaves, and the ids the
+    device signed-tx path computes from them = the ids of the host leaves."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(3)
+    ntx = 3000
+    ik = rng.integers(0, 256, (ntx, 32), dtype=np.uint8)
+    ok = rng.integers(0, 256, (ntx, 32), dtype=np.uint8)
+    q = rng.integers(0, 2**62, ntx).astype(np.int64)
+    nz = rng.integers(-2**62, 2**62, ntx).astype(np.int64)
+    notary = bytes(range(32))
+    blob, items, _ = cash_issue_items(ik, ok, notary, q, nz)
+    has = np.ones(items.size, bool)
+    out, off, status = engine.kryo_encode_packed_device(blob, items.reshape(-1), has, group=5)
+    assert int(status.sum()) == 0
+    hb, ho = make_cash_issue_leaves(ik, ok, notary, q, nz, threads=4)
+    assert np.array_equal(off.cpu().numpy().astype(np.uint64), ho)
+    assert np.array_equal(out.cpu().numpy(), hb)
+    ids_host, st = engine.tx_ids([[hb[int(ho[5 * t + j]):int(ho[5 * t + j + 1])].tobytes() for j in range(5)]
+                                  for t in range(50)])
+    dev = torch.device("cuda", 0)
+    tlo = torch.arange(0, 5 * ntx + 1, 5, dtype=torch.int64, device=dev)
+    tso = torch.arange(ntx + 1, dtype=torch.int64, device=dev)  # one (dummy) signature each: the ids are compared
+    txid = torch.empty((ntx, 32), dtype=torch.uint8, device=dev)
+    tst = torch.empty(ntx, dtype=torch.uint8, device=dev)
+    fb = torch.empty(ntx, dtype=torch.int64, device=dev)
+    keys = torch.zeros((ntx, 32), dtype=torch.uint8, device=dev)
+    sigs = torch.zeros((ntx, 64), dtype=torch.uint8, device=dev)
+    sst = torch.empty(ntx, dtype=torch.uint8, device=dev)
+    engine.signed_tx_verify_ed25519_device(out, off, tlo, tso, keys, sigs, txid, tst, fb, sst)
+    torch.cuda.synchronize()
+    assert np.array_equal(txid[:50].cpu().numpy(), ids_host)
