@@ -1257,6 +1257,7 @@ int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_ite
                                 void* d_out, uint64_t cap, void* d_off, void* d_status, void* hip_stream) {
   Device* d = dev_at(ctx, device);
   if (!d || !d_off || (n && (!d_items || !d_status))) return CORDAHIP_ERR_INVALID_ARG;
+  if (n >= (1ull << 31) - 1) return CORDAHIP_ERR_INVALID_ARG;  // the scan counts items in an int
   return guarded([&]() -> int {
     std::lock_guard<std::mutex> g(d->kryo_mu);
     if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;

@@ -386,7 +386,9 @@ int cordahip_kryo_encode(const cordahip_kryo_item* items, uint64_t n, uint8_t* o
  * (as cordahip_kryo_encode would reject it; size 0), 2 not written because it
  * ends beyond cap. Enqueued on hip_stream, asynchronous; the caller reads
  * d_off[n] / d_status when it needs them. Same encoder as cordahip_kryo_encode
- * (corda_amd/csrc/kryo_core.hpp): bit-identical leaves. */
+ * (corda_amd/csrc/kryo_core.hpp): bit-identical leaves. n < 2^31 - 1 per call.
+ * Device scratch (grow-only, per device): 8 B per item + 8 KB per writer thread
+ * (at most 2^18 writers: 2 GB). */
 int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_items, uint64_t n, uint32_t group,
                                 void* d_out, uint64_t cap, void* d_off, void* d_status, void* hip_stream);
 
