@@ -65,6 +65,7 @@ constexpr uint32_t kLevelBytes = kMaxDepth * kChunk;  // per-encoder level buffe
 
 KRYO_HD inline uint32_t kmin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
+
 // a byte string view that works on both sides (names are ASCII literals or
 // caller bytes)
 struct Sv {
@@ -80,6 +81,9 @@ struct Sv {
 };
 KRYO_HD inline bool operator==(const Sv& a, const Sv& b) {
   if (a.n != b.n) return false;
+  if (a.p == b.p) return true;  // the same literal (class names are compared often)
+  // class names share long prefixes ("net.corda.core.contracts."): test the end first
+  if (a.n && a.p[a.n - 1] != b.p[a.n - 1]) return false;
   for (uint32_t i = 0; i < a.n; i++)
     if (a.p[i] != b.p[i]) return false;
   return true;
@@ -332,7 +336,15 @@ struct Kout {
     prim(k, t, m);
   }
   KRYO_HD void ascii(uint32_t k, const Sv& s) {
-    string(k, [&](uint64_t i) { return (uint32_t)(uint8_t)s.p[i]; }, s.n);
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(s.p);
+    bool fast = s.n > 1 && s.n < 64;  // writeString's ASCII path, straight from the name's bytes
+    for (uint32_t i = 0; fast && i < s.n; i++) fast = p[i] <= 127;
+    if (fast) {
+      bytes(k, p, s.n);
+      mark_last(k);
+      return;
+    }
+    string(k, [&](uint64_t i) { return (uint32_t)p[i]; }, s.n);
   }
   KRYO_HD void utf16le(uint32_t k, const uint8_t* p, uint64_t n) {  // Java String from UTF-16LE units
     string(k, [&](uint64_t i) { return (uint32_t)(p[2 * i] | (p[2 * i + 1] << 8)); }, n);
@@ -343,7 +355,7 @@ struct Kout {
 // DefaultClassResolver's class-name ids and CompatibleFieldSerializer's
 // "header written" marks.
 struct Graph {
-  static constexpr uint32_t kMaxNames = 24;
+  static constexpr uint32_t kMaxNames = 16;  // a cash-state graph names 11 classes
   Sv names[kMaxNames] = {};
   uint32_t nnames = 0;
   Sv headers[kMaxNames] = {};
