@@ -720,10 +720,20 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
       return CORDAHIP_ERR_OUT_OF_MEMORY;
   }
   const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
-  hipStream_t cs = d.s_copy, es = d.s_ed, xs = d.s_ec;
+  hipStream_t cs = d.s_copy, xs = d.s_ec;
+  // statuses reach pinned caller arrays by kernel stores (a D2H copy queued
+  // behind busy compute streams can hold the enqueuing thread for milliseconds,
+  // delaying the next chunks' H2D: profiles/r04_q); pageable ones by copies
+  uint8_t* map_ed = static_cast<uint8_t*>(host_mapped(b->ed_status));
+  uint8_t* map_ec = static_cast<uint8_t*>(host_mapped(b->ec_status));
   hipError_t e = hipSuccess;
   for (uint64_t k = 0; k < nchunks && e == hipSuccess; k++) {
     StreamStage& st = d.sstage[k % kStreamStages];
+    // consecutive chunks alternate between s_ed / s_ed2 and the two Ed25519
+    // workspace slots: chunk k + 1's prep fills the CUs chunk k's ladder tail
+    // leaves idle
+    const int slot = (int)(k & 1);
+    hipStream_t es = slot ? d.s_ed2 : d.s_ed;
     const uint64_t a = e0 + cut(ne, k), ma = cut(ne, k + 1) - cut(ne, k);
     const uint64_t c = c0 + cut(nc, k), mc = cut(nc, k + 1) - cut(nc, k);
     if (k >= (uint64_t)kStreamStages) {  // the stage's buffers: chunk k-3 must be done with them
@@ -749,8 +759,9 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
     if (ma)
       e = e ? e
             : ed_verify_enqueue(d, st.ed_keys.as<uint8_t>(), st.ed_sigs.as<uint8_t>(), st.ed_msgs.as<uint8_t>(),
-                                (uint32_t)eml, ma, nullptr, st.ed_status.as<uint8_t>(), nullptr, 0u, es);
-    if (ma) e = e ? e : hipMemcpyAsync(b->ed_status + a, st.ed_status.p, ma, d2h, es);
+                                (uint32_t)eml, ma, nullptr, st.ed_status.as<uint8_t>(), nullptr, 0u, es, slot);
+    if (ma && map_ed) e = e ? e : launch_store_to_host(st.ed_status.p, map_ed + a, ma, es);
+    else if (ma) e = e ? e : hipMemcpyAsync(b->ed_status + a, st.ed_status.p, ma, d2h, es);
     e = e ? e : hipEventRecord(st.ed_done, es);
     e = e ? e : hipStreamWaitEvent(xs, st.ec_copied, 0);
     if (mc && e == hipSuccess) {
@@ -759,12 +770,15 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
                             st.ec_sigs.as<uint8_t>(), st.ec_sig_len.as<uint8_t>(), st.ec_msgs.as<uint8_t>(), nullptr,
                             (uint32_t)cml, mc, nullptr, st.ec_status.as<uint8_t>(), nullptr, 0u, xs);
     }
-    if (mc) e = e ? e : hipMemcpyAsync(b->ec_status + c, st.ec_status.p, mc, d2h, xs);
+    if (mc && map_ec) e = e ? e : launch_store_to_host(st.ec_status.p, map_ec + c, mc, xs);
+    else if (mc) e = e ? e : hipMemcpyAsync(b->ec_status + c, st.ec_status.p, mc, d2h, xs);
     e = e ? e : hipEventRecord(st.ec_done, xs);
   }
-  // drain all three streams even after an error, so no queued work outlives the call
-  const hipError_t e1s = hipStreamSynchronize(cs), e2s = hipStreamSynchronize(es), e3s = hipStreamSynchronize(xs);
-  if (e != hipSuccess || e1s != hipSuccess || e2s != hipSuccess || e3s != hipSuccess) return CORDAHIP_ERR_HIP;
+  // drain all four streams even after an error, so no queued work outlives the call
+  const hipError_t e1s = hipStreamSynchronize(cs), e2s = hipStreamSynchronize(d.s_ed),
+                   e2b = hipStreamSynchronize(d.s_ed2), e3s = hipStreamSynchronize(xs);
+  if (e != hipSuccess || e1s != hipSuccess || e2s != hipSuccess || e2b != hipSuccess || e3s != hipSuccess)
+    return CORDAHIP_ERR_HIP;
   return CORDAHIP_SUCCESS;
 }
 
