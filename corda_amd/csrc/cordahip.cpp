@@ -492,12 +492,10 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   // slice that holds its last transaction. Uniform slices with slice-aligned
   // chunks of ~156K C4 signatures ran 1.19 ladder rounds each, the second at
   // 19% occupancy: 12.8 ns per signature against ~10 for whole rounds
-  // (profiles/r04_f kernel trace, r04_i host trace). The first chunk is half a
-  // round (the GPU starts after the leaf bytes of 2^16 signatures'
-  // transactions, ~0.5 ms of PCIe), the rest one round, the two Ed25519
-  // streams overlapping one chunk's end-of-grid tail with the next chunk
-  // (r04_o: 73.6 M/s against 71.4 for 2^17 / 2^18 chunks, both before the
-  // chunk-aligned slices that took it to 80.9, r04_p).
+  // (profiles/r04_f kernel trace, r04_i host trace). Chunks are half a round
+  // (the GPU starts after the leaf bytes of 2^16 signatures' transactions,
+  // ~0.5 ms of PCIe), the two Ed25519 streams keeping two chunks in flight so
+  // one chunk's end-of-grid tail overlaps the next chunk.
   uint64_t chunk = 1u << 16;
   if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
   // chunks double from `chunk` up to CORDAHIP_TX_SIG_CHUNK_MAX (default: chunk,
