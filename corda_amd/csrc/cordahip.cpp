@@ -640,17 +640,36 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   const uint64_t nsig = b->tx_sig_off[ntx];
   if (nsig && (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off)) return CORDAHIP_ERR_INVALID_ARG;
   const double t0 = tracing() ? now_ms() : 0;
-  // signature -> transaction (tx_of): a per-thread buffer kept across calls (a
-  // fresh 20 MB vector per C4 call page-faulted for ~0.8 ms, 3.9 ms on the first
-  // calls), each device filling its shard's part (signed_tx_device)
-  thread_local std::unique_ptr<uint64_t[]> tl_tx_of;
-  thread_local uint64_t tl_tx_of_cap = 0;
-  if (nsig > tl_tx_of_cap) {
-    tl_tx_of.reset();
-    tl_tx_of.reset(new uint64_t[nsig]);
-    tl_tx_of_cap = nsig;
+  // signature -> transaction (tx_of), each device filling its shard's part
+  // (signed_tx_device); the buffer comes from the context's cache and goes
+  // back to it on every exit
+  struct TxOf {
+    cordahip_ctx* ctx;
+    std::unique_ptr<uint64_t[]> p;
+    uint64_t cap = 0;
+    TxOf(cordahip_ctx* c, uint64_t n) : ctx(c) {
+      std::lock_guard<std::mutex> g(ctx->txof_mu);
+      auto& f = ctx->txof_free;
+      for (size_t i = 0; i < f.size(); i++)
+        if (f[i].second >= n) {
+          p = std::move(f[i].first);
+          cap = f[i].second;
+          f.erase(f.begin() + (long)i);
+          return;
+        }
+    }
+    ~TxOf() {
+      if (!p) return;
+      std::lock_guard<std::mutex> g(ctx->txof_mu);
+      auto& f = ctx->txof_free;
+      if (f.size() < cordahip_ctx::kTxOfCache) f.emplace_back(std::move(p), cap);
+    }
+  } buf(ctx, nsig);
+  if (!buf.p && nsig) {
+    buf.p.reset(new uint64_t[nsig]);
+    buf.cap = nsig;
   }
-  uint64_t* tx_of = tl_tx_of.get();
+  uint64_t* tx_of = buf.p.get();
   const double t_of = tracing() ? now_ms() : 0;
   // per device: its contiguous tx shard in slices (CORDAHIP_TX_SLICES; default:
   // one slice per signature chunk) and, chunk by

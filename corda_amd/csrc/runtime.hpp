@@ -358,6 +358,12 @@ struct cordahip_ctx {
   std::unordered_map<uint64_t, std::shared_ptr<cordahip::rt::JobState>> jobs;
   std::unique_ptr<cordahip::rt::WorkerPool> pool;
   std::unique_ptr<cordahip::rt::HostPool> host;  // packing / scattering threads
+  // signed-tx batches' signature -> transaction maps, kept for reuse across
+  // calls (a fresh 20 MB map per C4 call page-faulted for 0.8-3.9 ms): taken
+  // by a call, returned after it; at most kTxOfCache kept
+  static constexpr size_t kTxOfCache = 4;
+  std::mutex txof_mu;
+  std::vector<std::pair<std::unique_ptr<uint64_t[]>, uint64_t>> txof_free;
 };
 
 namespace cordahip {
