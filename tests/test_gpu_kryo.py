@@ -123,3 +123,24 @@ def test_cash_issue_records_feed_tx_ids(engine):
     engine.signed_tx_verify_ed25519_device(out, off, tlo, tso, keys, sigs, txid, tst, fb, sst)
     torch.cuda.synchronize()
     assert np.array_equal(txid[:50].cpu().numpy(), ids_host)
+
+
+def test_edge_batches(engine):
+    """Empty and one-item batches, zero-length RAW leaves, and a 200 KB RAW leaf
+    (many times the encoder's 1,024-byte level buffers) beside short items."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    # n = 0: off[0] = 0, nothing else touched
+    blob, arr, has = _lib.kryo_pack([])
+    out, off, status = engine.kryo_encode_packed_device(blob, arr, has)
+    assert off.numel() == 1 and int(off[0]) == 0
+    rng = random.Random(9)
+    big = bytes(rng.getrandbits(8) for _ in range(200_000))
+    for items in ([("raw", b"", 0)], [("char", "z", 0)], [("raw", b"", 0), ("raw", big, 0), ("int", -5, 0), ("raw", b"", 0)],
+                  [("String", "x" * 70_000, 0), ("ed25519_key", bytes(32), 47)]):
+        host = _lib.kryo_encode(items)
+        blob, arr, has = _lib.kryo_pack(items)
+        out, off, status = engine.kryo_encode_packed_device(blob, arr, has)
+        assert int(status.sum()) == 0
+        assert _leaves(out, off, len(items)) == host
+    torch.cuda.synchronize(dev)
