@@ -236,9 +236,10 @@ def main():
     out = {"lanes": lanes, "mismatches": sum(t["mismatches"] for t in tot.values()),
            "per_scheme": tot, "gpu_verify_s": gpu_s, "wall_s": time.time() - t0,
            "batch": n, "oracle_sample_per_batch": smp,
-           "note": "every lane's status vs the corpus construction where it fixes the status; every open lane "
-                   "(slide()-dependent S, any-rejection ECDSA corruptions) plus a 2^%d-lane sample per batch vs "
-                   "the C oracle" % args.sample_log2}
+           "note": ("every lane's status vs the corpus construction where it fixes the status; " +
+                    ("every lane vs the C oracle (--oracle-all)" if args.oracle_all else
+                     "every open lane (slide()-dependent S, any-rejection ECDSA corruptions) plus a 2^%d-lane "
+                     "sample per batch vs the C oracle" % args.sample_log2))}
     print(json.dumps(out), flush=True)
     if args.out:
         with open(args.out, "w") as f:
