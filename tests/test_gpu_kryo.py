@@ -88,6 +88,11 @@ def test_invalid_items_and_capacity(engine):
     assert (st2[:7] == 0).all() and (st2[7:10] == 2).all() and list(st2[10:13]) == [1, 1, 1] and (st2[13:] == 2).all()
     assert _leaves(out2, off2, 7) == host[:7]
     assert int(off2[-1]) == int(o[-1])  # off[n] is the full size either way
+    # no room at all: every valid leaf status 2, the sizes still complete
+    _, off3, status3 = engine.kryo_encode_packed_device(blob, arr, has, cap=0)
+    st3 = status3.cpu().numpy()
+    assert list(st3[10:13]) == [1, 1, 1] and (np.delete(st3, [10, 11, 12]) == 2).all()
+    assert np.array_equal(off3.cpu().numpy(), o)
 
 
 def test_cash_issue_records_feed_tx_ids(engine):
