@@ -476,6 +476,8 @@ class C4:
                        "device_encode": self.device_encode}
         if self.device_encode:
             self.kernel = "kryo_size + scan + kryo_write + " + C4.kernel
+            # the encoder's L2-to-fabric bytes per tx (tools/gpu_pmc_kryo2.sh -> pmc_kryo_traffic.py)
+            self.extra_pmc = ("r04_pmc_kryo_traffic.json", ntx)
             self.config["component_bytes_per_tx"] = round(self.d_blob.numel() / ntx, 1)
         if not self.native:
             self.config["leaf_lens"] = list(C4_LEAF_LENS)
@@ -1102,6 +1104,15 @@ def main():
                                 "calibrated model of tools/mall_sim.cpp (traffic_l2_fabric: the counters as read)")
             else:
                 traffic_kind = "L2-to-fabric bytes (FETCH_SIZE/WRITE_SIZE): Infinity-Cache hits included, an upper bound"
+            extra = getattr(wl, "extra_pmc", None)
+            extra_file = os.path.join(ROOT, "profiles", extra[0]) if extra else None
+            if traffic is not None and extra_file and os.path.exists(extra_file):
+                with open(extra_file) as f:
+                    xb = json.load(f)["l2_fabric_bytes_per_tx"] * extra[1]
+                traffic += xb
+                traffic_fabric = traffic_fabric + xb if traffic_fabric is not None else None
+                traffic_src += " + profiles/%s (the Kryo encoder kernels' L2-to-fabric bytes per tx x txs)" % extra[0]
+                traffic_kind += "; the encoder's bytes added as read (no MALL split, an upper bound for its share)"
         out = {
             "metric": METRIC,
             "value": value,
