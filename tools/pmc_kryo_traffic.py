@@ -13,12 +13,12 @@ import json
 import sys
 from collections import defaultdict
 
-KINDS = {"kryo_size_kernel": "kryo_size", "kryo_write_kernel": "kryo_write", "DeviceScan": "scan"}
+KINDS = {"kryo_size_kernel": "kryo_size", "kryo_write_kernel": "kryo_write", "scan": "scan"}  # hipcub/rocprim scan kernels
 
 
 def kind(name):
     for k, v in KINDS.items():
-        if k in name:
+        if k in name.lower():
             return v
     return None
 
