@@ -363,7 +363,7 @@ class C3:
 # ---- C4: SignedTransaction.verifySignatures on cash-issue transactions --------
 class C4:
     kernel = "sha256_leaves + merkle_root + ed25519 prep/ladder + tx_reduce"
-    pmc = "r04_pmc_c4.json"  # tools/gpu_r4_pmc2.sh -> pmc_compose.py -> pmc_hbm_split.py (ladder MALL split)
+    pmc = "r04_pmc_c4.json"  # tools/leases/gpu_r4_pmc2.sh -> pmc_compose.py -> pmc_hbm_split.py (ladder MALL split)
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -541,7 +541,7 @@ class C4:
 # ---- C5: verifier-module queue drain, mixed schemes, pinned host memory -------
 class C5:
     kernel = "ed25519 prep/ladder + ecdsa prep/inv/ladder, 3-stage H2D/kernel/D2H pipeline"
-    pmc = "r04_pmc_c5.json"  # tools/gpu_r4_pmc2.sh -> pmc_compose.py -> pmc_hbm_split.py (device side, per lane)
+    pmc = "r04_pmc_c5.json"  # tools/leases/gpu_r4_pmc2.sh -> pmc_compose.py -> pmc_hbm_split.py (device side, per lane)
     host_timed = True  # the drain is synchronous and owns its streams: wall time, PCIe included
 
     def __init__(self, eng, device, stream, rank, args):
