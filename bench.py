@@ -46,6 +46,10 @@ LIMB_MACS = {"ed25519": 198_000, "p256": 211_000, "secp256k1": 192_000}
 # Integer-ALU peak: 256 CUs x 64 v_mad_u64_u32 lane-ops per CU-cycle x 2.4 GHz
 # (per-CU rate measured: profiles/r01_int_rates.jsonl, 59-62 lane-ops/CU-cycle).
 INT_MAC_PEAK_T = 256 * 64 * 2.4e9 / 1e12
+# the MEASURED v_mad_u64_u32 throughput, 59.43 lane-ops per
+# CU-cycle (profiles/r01_int_rates.jsonl, 8 independent chains, 2048 blocks),
+# taken at the shader clock this run holds (clock_ghz; 2.4 GHz without a reading)
+MAD_U64_LANE_OPS_PER_CU_CYCLE = 59.43
 C4_LEAF_LENS = (450, 150, 140, 43, 55)  # SURVEY §8(d) C4 synthetic cash-issue component lengths
 
 
@@ -1091,19 +1095,31 @@ def main():
         # HBM bytes per step from the committed PMC passes (tools/gpu_pmc.sh:
         # FETCH_SIZE and WRITE_SIZE in separate passes), scaled to this step
         traffic, traffic_src, traffic_fabric, traffic_kind = None, None, None, None
+        traffic_hbm_modeled, valu_busy = None, None
         pmc_file = os.path.join(ROOT, "profiles", wl.pmc) if wl.pmc else None
         if pmc_file and os.path.exists(pmc_file):
             with open(pmc_file) as f:
                 pmc = json.load(f)
+            dv = pmc.get("total", {}).get("derived", {})
+            if "valu_busy_est_4cyc" in dv:
+                # VALU busy from the same PMC file: SQ_INSTS_VALU x the measured ~4 SIMD-cycles per
+                # (VOP3-dominated) wave instruction / SIMD-cycles (SQ_ACTIVE_INST_VALU
+                # counts issues on gfx950, so the issue fraction alone is the _issue figure)
+                valu_busy = {"valu_busy": dv["valu_busy_est_4cyc"], "valu_issue_frac": dv.get("valu_busy_direct"),
+                             "valu_insts_per_unit": dv.get("valu_lane_insts_per_lane"),
+                             "source": "profiles/%s total.derived (the verification kernels of one step)" % wl.pmc}
             per_unit = pmc.get("hbm_bytes_per_unit")
             traffic = per_unit * wl.units if per_unit else None
             traffic_src = "profiles/%s (bytes per unit x units per step)" % wl.pmc
+            traffic_kind = ("measured: FETCH_SIZE/WRITE_SIZE counters (separate passes, FETCH_SIZE x2 per the gfx950 "
+                            "correction), L2-to-fabric bytes = HBM + Infinity-Cache hits, an upper bound on HBM")
             if pmc.get("l2_fabric_bytes_per_unit"):
-                traffic_fabric = pmc["l2_fabric_bytes_per_unit"] * wl.units
-                traffic_kind = ("HBM: FETCH_SIZE/WRITE_SIZE with the ladder's Infinity-Cache hits removed by the "
-                                "calibrated model of tools/mall_sim.cpp (traffic_l2_fabric: the counters as read)")
-            else:
-                traffic_kind = "L2-to-fabric bytes (FETCH_SIZE/WRITE_SIZE): Infinity-Cache hits included, an upper bound"
+                # the counters stay primary; the HBM share is a model (tools/mall_sim.cpp, calibrated
+                # on the same counters) and is reported under its own, explicit key
+                traffic_hbm_modeled = traffic
+                traffic = traffic_fabric = pmc["l2_fabric_bytes_per_unit"] * wl.units
+                traffic_kind += ("; traffic_hbm_modeled: the ladder's Infinity-Cache hits removed by the calibrated "
+                                 "model of tools/mall_sim.cpp (not a counter)")
             extra = getattr(wl, "extra_pmc", None)
             extra_file = os.path.join(ROOT, "profiles", extra[0]) if extra else None
             if traffic is not None and extra_file and os.path.exists(extra_file):
@@ -1111,6 +1127,7 @@ def main():
                     xb = json.load(f)["l2_fabric_bytes_per_tx"] * extra[1]
                 traffic += xb
                 traffic_fabric = traffic_fabric + xb if traffic_fabric is not None else None
+                traffic_hbm_modeled = traffic_hbm_modeled + xb if traffic_hbm_modeled is not None else None
                 traffic_src += " + profiles/%s (the Kryo encoder kernels' L2-to-fabric bytes per tx x txs)" % extra[0]
                 traffic_kind += "; the encoder's bytes added as read (no MALL split, an upper bound for its share)"
         out = {
@@ -1137,13 +1154,23 @@ def main():
             "roofline": {"bound": "valu", "achieved": achieved, "peak": INT_MAC_PEAK_T,
                          "unit": "Tlimb-MAC/s", "frac": achieved / INT_MAC_PEAK_T, "traffic": traffic,
                          "traffic_source": traffic_src, "traffic_kind": traffic_kind,
-                         "traffic_l2_fabric": traffic_fabric,
+                         "traffic_l2_fabric": traffic_fabric, "traffic_hbm_modeled": traffic_hbm_modeled,
                          "kernel": wl.kernel, "kernel_ms": kernel_ms,
                          "work_per_unit": "%d limb-MACs per verification (SURVEY §8d)" % wl.macs},
             "int_alu_peak_frac": achieved / INT_MAC_PEAK_T,
+            "valu_busy": valu_busy,
             "verdict_check": chk,
             "corpus_gen_s": t_gen,
         }
+        ghz = clock.get("clock_ghz") if clock else None
+        mpeak = 256 * MAD_U64_LANE_OPS_PER_CU_CYCLE * (ghz or 2.4) * 1e9 / 1e12
+        out["roofline"]["peak_measured"] = mpeak
+        out["roofline"]["peak_measured_basis"] = ("256 CU x %.2f v_mad_u64_u32 lane-ops/CU-cycle "
+                                                  "(profiles/r01_int_rates.jsonl) x %s GHz" %
+                                                  (MAD_U64_LANE_OPS_PER_CU_CYCLE, ("%.3f (clock_ghz)" % ghz) if ghz
+                                                   else "2.4 (spec: no clock reading)"))
+        out["roofline"]["frac_measured_peak"] = achieved / mpeak
+        out["frac_measured_peak"] = achieved / mpeak
         if clock is not None:
             out["clock"] = clock
             if clock.get("clock_ghz"):

@@ -34,16 +34,16 @@ EXPORTS = [
     "cordahip_tx_ids", "cordahip_signed_tx_verify", "cordahip_signed_tx_verify_ed25519_device",
     "cordahip_ecdsa_verify_device", "cordahip_stream_verify", "cordahip_filtered_tx_verify",
     "cordahip_tx_submit", "cordahip_txid_submit", "cordahip_filtered_tx_submit", "cordahip_shard_range",
-    "cordahip_kryo_encode", "cordahip_kryo_encode_device",
+    "cordahip_kryo_encode", "cordahip_kryo_encode_device", "cordahip_signed_txcomp_verify", "cordahip_txcomp_submit",
 ]
 ERR_BUFFER_TOO_SMALL = -8
 # cordahip_kryo_item kinds (CORDAHIP_KRYO_*)
 KRYO_KINDS = {"raw": 0, "char": 1, "short": 2, "int": 3, "long": 4, "byte": 5, "boolean": 6, "float": 7,
               "double": 8, "String": 9, "ed25519_key": 10, "public_key": 11, "kotlin_object": 12, "party": 13,
               "issue_command": 14, "cash_state": 15}
-ABI_VERSION = 2
+ABI_VERSION = 3
 FLAG_IS_VALID = 1  # CORDAHIP_FLAG_IS_VALID: Crypto.isValid semantics (no emptiness checks)
-TX_NO_LEAVES, TX_NO_SIGNATURES, TX_BAD_TREE = 6, 7, 8
+TX_NO_LEAVES, TX_NO_SIGNATURES, TX_BAD_TREE, TX_BAD_COMPONENT = 6, 7, 8, 9
 
 
 class EngineUnavailable(RuntimeError):
@@ -87,6 +87,26 @@ class TxidBatch(ctypes.Structure):
 class SignedTxBatch(ctypes.Structure):
     _fields_ = [
         ("tx", TxidBatch),
+        ("tx_sig_off", ctypes.c_void_p),
+        ("scheme", ctypes.c_void_p),
+        ("key", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
+        ("sig", ctypes.c_void_p), ("sig_off", ctypes.c_void_p),
+        ("sig_status", ctypes.c_void_p), ("first_bad_sig", ctypes.c_void_p),
+    ]
+
+
+class TxcompBatch(ctypes.Structure):
+    _fields_ = [
+        ("ntx", ctypes.c_uint64),
+        ("items", ctypes.c_void_p), ("tx_item_off", ctypes.c_void_p),
+        ("payload", ctypes.c_void_p), ("payload_len", ctypes.c_uint64),
+        ("txid", ctypes.c_void_p), ("tx_status", ctypes.c_void_p),
+    ]
+
+
+class SignedTxcompBatch(ctypes.Structure):
+    _fields_ = [
+        ("tx", TxcompBatch),
         ("tx_sig_off", ctypes.c_void_p),
         ("scheme", ctypes.c_void_p),
         ("key", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
@@ -168,6 +188,8 @@ def lib() -> ctypes.CDLL:
         "cordahip_shard_range": (None, [u64, u32, u32, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "cordahip_kryo_encode": (i32, [ctypes.POINTER(KryoItem), u64, vp, u64, vp]),
         "cordahip_kryo_encode_device": (i32, [vp, i32, vp, u64, u32, vp, u64, vp, vp, vp]),
+        "cordahip_signed_txcomp_verify": (i32, [vp, ctypes.POINTER(SignedTxcompBatch)]),
+        "cordahip_txcomp_submit": (i32, [vp, ctypes.POINTER(SignedTxcompBatch), ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(l, name)

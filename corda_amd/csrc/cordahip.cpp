@@ -248,12 +248,28 @@ hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs
   DevBuf& ws = d.ed_ws[slot];
   hipEvent_t& ev = d.ed_ev[slot];
   static const uint64_t ws_lanes = env_lanes("CORDAHIP_ED25519_WS_LANES", kEdWsLanes);
-  const uint64_t lanes = std::min<uint64_t>(ws_lanes, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
-  if (ws.cap < lanes * ed25519_ws_lane_bytes()) {
+  // Slot 1 only serves the alternating chunks of the pipelines (host batches,
+  // streams, signed-tx chunks): it is capped at half of slot 0, so the two
+  // together stay within 1.5 x CORDAHIP_ED25519_WS_LANES x 3,200 B (81 GB at
+  // the default). The launch loops over whatever the
+  // workspace holds, so a smaller one only costs extra launch pairs.
+  const uint64_t cap_lanes = slot ? std::max<uint64_t>(64, ws_lanes / 2 / 64 * 64) : ws_lanes;
+  const uint64_t lanes = std::min<uint64_t>(cap_lanes, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
+  const uint64_t lane_bytes = ed25519_ws_lane_bytes();
+  if (ws.cap < lanes * lane_bytes) {
     // a smaller buffer may still be in use by an earlier stream
     hipError_t e = ev ? hipEventSynchronize(ev) : hipSuccess;
     if (e != hipSuccess) return e;
-    e = ws.ensure(std::max<uint64_t>(lanes, std::min<uint64_t>(ws_lanes, kWsMinLanes)) * ed25519_ws_lane_bytes());
+    uint64_t want = std::max<uint64_t>(lanes, std::min<uint64_t>(cap_lanes, kWsMinLanes));
+    const uint64_t had = ws.cap / lane_bytes / 64 * 64;  // ensure() frees it before allocating
+    e = ws.ensure(want * lane_bytes);
+    // HBM shared with other work: halve the request until it fits (at least
+    // what the slot held before, or one wave's lanes) instead of failing the call
+    while (e == hipErrorOutOfMemory && want > std::max<uint64_t>(64, had)) {
+      (void)hipGetLastError();
+      want = std::max<uint64_t>(std::max<uint64_t>(64, had), want / 2 / 64 * 64);
+      e = ws.ensure(want * lane_bytes);
+    }
     if (e != hipSuccess) return e;
   }
   if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return hipErrorUnknown;
@@ -374,12 +390,93 @@ int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
 // enqueues slices [j0, j1) (the signed-tx path releases them a few at a time,
 // interleaved with the signature chunks' copies, because H2D copies of all
 // streams leave through the DMA engine in submission order).
-hipError_t tx_ids_prepare(Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound) {
+// Leaf bytes one component may need (kryo_core.hpp): the kind's constant text
+// (class and field names, framing; < 2 KB for a cash state) plus at most 4
+// bytes per payload byte (a cash state writes the owner's key and name up to 3
+// times; a string 3 bytes per UTF-16 unit). A leaf beyond its slice's bound
+// would be reported, not written (CORDAHIP_TX_BAD_COMPONENT);
+// tests/test_kryo_template.py checks the bound on every test item.
+uint64_t comp_leaf_bound(uint64_t payload_bytes) { return 4096 + 4 * payload_bytes; }
+uint64_t comp_payload_bytes(const cordahip_kryo_item& it) {
+  return (it.kind == CORDAHIP_KRYO_STRING || it.kind == CORDAHIP_KRYO_KOTLIN_OBJECT) ? 2 * it.len : it.len;
+}
+
+// Component-level batches (cordahip_txcomp_batch): per id slice, how far the
+// payload prefix must reach, the leaf buffer it needs, and its items per tx.
+struct CompPlan {
+  const cordahip_txcomp_batch* c = nullptr;
+  std::vector<uint64_t> pay_end;  // payload bytes slices 0..j reference (running max)
+  std::vector<uint32_t> group;    // items per transaction when uniform in the slice (the encoder's hint), else 1
+  uint64_t slice_cap = 16;        // leaf bytes of the largest slice's bound (two slice buffers alternate)
+  uint64_t max_items = 0;
+  uint64_t copied = 0;            // payload prefix enqueued so far
+  static constexpr uint64_t kDirectWriters = 1u << 15;
+};
+
+hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound,
+                          CompPlan* cp) {
   const uint64_t t0 = bound.front(), t1 = bound.back(), ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
-  const uint64_t b0 = b->leaf_off[l0], b1 = b->leaf_off[l1];
   TxWork& w = d.tx;
-  if (w.leaf_bytes.ensure(std::max<uint64_t>(b1 - b0, 16)) || w.leaf_off.ensure((nleaves + 1) * 8) ||
+  uint64_t leaf_buf = 0;
+  if (cp) {
+    const cordahip_txcomp_batch* c = cp->c;
+    const size_t ns = bound.size() - 1;
+    cp->pay_end.assign(ns, 0);
+    cp->group.assign(ns, 1);
+    std::vector<uint64_t> cap(ns, 0);
+    ctx->host->parallel_for(ns, 1, [&](uint64_t x, uint64_t y) {
+      for (uint64_t j = x; j < y; j++) {
+        const uint64_t ts0 = bound[j], ts1 = bound[j + 1];
+        const uint64_t g = ts1 > ts0 ? c->tx_item_off[ts0 + 1] - c->tx_item_off[ts0] : 1;
+        bool uniform = g > 0;
+        uint64_t end = 0, bd = 0;
+        for (uint64_t t = ts0; t < ts1; t++) {
+          uniform = uniform && c->tx_item_off[t + 1] - c->tx_item_off[t] == g;
+          for (uint64_t i = c->tx_item_off[t]; i < c->tx_item_off[t + 1]; i++) {
+            const cordahip_kryo_item& it = c->items[i];
+            const uint64_t off = (uint64_t)(uintptr_t)it.data, nb = comp_payload_bytes(it);
+            if (it.kind != CORDAHIP_KRYO_RAW && nb == 0) {
+              bd += comp_leaf_bound(0);
+              continue;
+            }
+            const bool fits = off <= c->payload_len && nb <= c->payload_len - off;
+            if (fits) end = std::max(end, off + nb);
+            bd += comp_leaf_bound(fits ? nb : 0);
+          }
+        }
+        cp->pay_end[j] = end;
+        cp->group[j] = uniform && g <= 64 ? (uint32_t)g : 1;
+        cap[j] = bd;
+      }
+    });
+    for (size_t j = 0; j < ns; j++) {
+      if (j) cp->pay_end[j] = std::max(cp->pay_end[j], cp->pay_end[j - 1]);
+      cp->slice_cap = std::max(cp->slice_cap, cap[j]);
+      cp->max_items = std::max(cp->max_items, b->tx_leaf_off[bound[j + 1]] - b->tx_leaf_off[bound[j]]);
+    }
+    cp->copied = 0;
+    leaf_buf = 2 * cp->slice_cap;
+    if (w.comp_items.ensure(std::max<uint64_t>(nleaves, 1) * sizeof(cordahip_kryo_item)) ||
+        w.payload.ensure(std::max<uint64_t>(ns ? cp->pay_end.back() : 0, 16)) ||
+        w.comp_status.ensure(std::max<uint64_t>(nleaves, 1)))
+      return hipErrorOutOfMemory;
+    // the encoder's scratch (d.kryo_*, kryo_mu held by the caller) for the largest slice
+    const uint64_t n = cp->max_items;
+    size_t temp_bytes = 0;
+    if (hipError_t e = kryo_scan_bytes(temp_bytes, n + 1, d.stream)) return e;
+    if (d.kryo_sizes.cap < (n + 1) * 8 || d.kryo_temp.cap < temp_bytes || d.kryo_items.cap < n * 8 + 8 ||
+        d.kryo_ws.cap < kryo_direct_ws_bytes(CompPlan::kDirectWriters) || d.kryo_fixed.cap < kryo_fixed_scratch_bytes()) {
+      if (d.kryo_ev && hipEventSynchronize(d.kryo_ev) != hipSuccess) return hipErrorUnknown;
+      if (d.kryo_sizes.ensure((n + 1) * 8) || d.kryo_temp.ensure(std::max<size_t>(temp_bytes, 16)) ||
+          d.kryo_items.ensure(n * 8 + 8) || d.kryo_ws.ensure(kryo_direct_ws_bytes(CompPlan::kDirectWriters)) ||
+          d.kryo_fixed.ensure(kryo_fixed_scratch_bytes()))
+        return hipErrorOutOfMemory;
+    }
+  } else {
+    leaf_buf = b->leaf_off[l1] - b->leaf_off[l0];
+  }
+  if (w.leaf_bytes.ensure(std::max<uint64_t>(leaf_buf, 16)) || w.leaf_off.ensure((nleaves + 1) * 8) ||
       w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
       w.txid.ensure(std::max<uint64_t>(ntx, 1) * 32) || w.tx_status.ensure(std::max<uint64_t>(ntx, 1)))
     return hipErrorOutOfMemory;
@@ -388,9 +485,9 @@ hipError_t tx_ids_prepare(Device& d, const cordahip_txid_batch* b, const std::ve
 
 hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound, size_t j0,
                           size_t j1, std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& cev,
-                          std::vector<hipEvent_t>& kev, uint8_t* map_txid, uint8_t* map_status) {
+                          std::vector<hipEvent_t>& kev, uint8_t* map_txid, uint8_t* map_status, CompPlan* cp) {
   const uint64_t t0 = bound.front();
-  const uint64_t l0 = b->tx_leaf_off[t0], b0 = b->leaf_off[l0];
+  const uint64_t l0 = b->tx_leaf_off[t0], b0 = cp ? 0 : b->leaf_off[l0];
   TxWork& w = d.tx;
   hipStream_t s = d.stream, sc = d.s_idcopy ? d.s_idcopy : d.stream;
   const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
@@ -400,21 +497,57 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
   for (size_t j = j0; j < j1 && e == hipSuccess; j++) {
     const uint64_t ts0 = bound[j], ts1 = bound[j + 1];
     const uint64_t ls0 = b->tx_leaf_off[ts0], ls1 = b->tx_leaf_off[ts1];
-    const uint64_t bs0 = b->leaf_off[ls0], bs1 = b->leaf_off[ls1];
-    if (bs1 > bs0)
-      e = blocked("leaf-bytes H2D", [&] {
-        return hipMemcpyAsync(w.leaf_bytes.as<uint8_t>() + (bs0 - b0), b->leaf_bytes + bs0, bs1 - bs0, h2d, sc);
-      });
-    e = e ? e : hipMemcpyAsync(w.leaf_off.as<uint64_t>() + (ls0 - l0), b->leaf_off + ls0, (ls1 - ls0 + 1) * 8, h2d, sc);
+    if (!cp) {
+      const uint64_t bs0 = b->leaf_off[ls0], bs1 = b->leaf_off[ls1];
+      if (bs1 > bs0)
+        e = blocked("leaf-bytes H2D", [&] {
+          return hipMemcpyAsync(w.leaf_bytes.as<uint8_t>() + (bs0 - b0), b->leaf_bytes + bs0, bs1 - bs0, h2d, sc);
+        });
+      e = e ? e : hipMemcpyAsync(w.leaf_off.as<uint64_t>() + (ls0 - l0), b->leaf_off + ls0, (ls1 - ls0 + 1) * 8, h2d, sc);
+    } else {
+      // the slice's components, and the payload prefix they reach
+      const cordahip_txcomp_batch* c = cp->c;
+      if (ls1 > ls0)
+        e = hipMemcpyAsync(w.comp_items.as<cordahip_kryo_item>() + (ls0 - l0), c->items + ls0,
+                           (ls1 - ls0) * sizeof(cordahip_kryo_item), h2d, sc);
+      if (e == hipSuccess && cp->pay_end[j] > cp->copied) {
+        e = blocked("payload H2D", [&] {
+          return hipMemcpyAsync(w.payload.as<uint8_t>() + cp->copied, c->payload + cp->copied,
+                                cp->pay_end[j] - cp->copied, h2d, sc);
+        });
+        cp->copied = cp->pay_end[j];
+      }
+    }
     e = e ? e : hipMemcpyAsync(w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), b->tx_leaf_off + ts0, (ts1 - ts0 + 1) * 8, h2d, sc);
     e = e ? e : hipEventRecord(cev[j], sc);
     e = e ? e : hipStreamWaitEvent(s, cev[j], 0);
-    e = e ? e : blocked("sha256_leaves launch", [&] {
-      return launch_sha256_leaves(bytes_base, w.leaf_off.as<uint64_t>() + (ls0 - l0), ls1 - ls0,
-                                  w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
-    });
+    if (cp) {
+      // the slice's leaves on the GPU (the template encoder) into one of two
+      // alternating slice buffers, offsets relative to that buffer
+      uint8_t* sb = w.leaf_bytes.as<uint8_t>() + (j % 2) * cp->slice_cap;
+      uint32_t* slots = d.kryo_items.as<uint32_t>();
+      const uint64_t n = ls1 - ls0;
+      e = e ? e : launch_kryo_encode(w.comp_items.as<cordahip_kryo_item>() + (ls0 - l0), w.payload.as<uint8_t>(),
+                                     cp->c->payload_len, n, cp->group[j], d.kryo_fixed.as<uint8_t>(), slots, slots + n,
+                                     d.kryo_sizes.as<uint64_t>(), w.leaf_off.as<uint64_t>() + (ls0 - l0), sb,
+                                     cp->slice_cap, w.comp_status.as<uint8_t>() + (ls0 - l0), d.kryo_ws.as<uint8_t>(),
+                                     CompPlan::kDirectWriters, d.kryo_temp.p, d.kryo_temp.cap, s);
+      e = e ? e : launch_sha256_leaves(sb, w.leaf_off.as<uint64_t>() + (ls0 - l0), n,
+                                       w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
+    } else {
+      e = e ? e : blocked("sha256_leaves launch", [&] {
+        return launch_sha256_leaves(bytes_base, w.leaf_off.as<uint64_t>() + (ls0 - l0), ls1 - ls0,
+                                    w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
+      });
+    }
     e = e ? e : launch_merkle_root(hash_base, w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), ts1 - ts0,
                                    w.txid.as<uint8_t>() + (ts0 - t0) * 32, w.tx_status.as<uint8_t>() + (ts0 - t0), s);
+    if (cp) {  // a component the encoder rejected: no id for its transaction
+      const uint8_t* st_base =
+          reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(w.comp_status.p) - l0);
+      e = e ? e : launch_comp_check(st_base, w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), ts1 - ts0,
+                                    w.tx_status.as<uint8_t>() + (ts0 - t0), s);
+    }
     e = e ? e : hipEventRecord(kev[j], s);  // the slice's ids are in HBM: its signatures may gather them
     if (ts1 > ts0 && map_txid && map_status) {  // pinned caller arrays: stored by a kernel
       e = e ? e : launch_store_to_host(w.txid.as<uint8_t>() + (ts0 - t0) * 32, map_txid + ts0 * 32, (ts1 - ts0) * 32, s);
@@ -429,7 +562,13 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
     }
     e = e ? e : hipEventRecord(ev[j], s);
   }
-  if (e == hipSuccess && j1 + 1 == bound.size()) e = hipEventRecord(d.tx_ev, s);  // the last slice: fence d.tx
+  if (e == hipSuccess && j1 + 1 == bound.size()) {
+    e = hipEventRecord(d.tx_ev, s);  // the last slice: fence d.tx
+    if (cp && e == hipSuccess) {     // and the encoder's scratch (d.kryo_*)
+      if (!d.kryo_ev) e = hipEventCreateWithFlags(&d.kryo_ev, hipEventDisableTiming);
+      e = e ? e : hipEventRecord(d.kryo_ev, s);
+    }
+  }
   return e;
 }
 
@@ -480,10 +619,20 @@ void reduce_txs(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b, uint64_t t
 // messages: the GPU sat idle ~5 ms per C4 step until the first signatures were
 // packed.)
 int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b, uint64_t* tx_of,
-                     uint64_t lo, uint64_t hi, uint64_t slices) {
+                     uint64_t lo, uint64_t hi, uint64_t slices, const cordahip_txcomp_batch* comps) {
   std::lock_guard<std::mutex> g(d.tx_mu);  // d.tx (the ids) stays ours until every gather has run
+  // component batches also use the GPU encoder's scratch (d.kryo_*) for the whole call
+  std::unique_lock<std::mutex> gk(d.kryo_mu, std::defer_lock);
+  CompPlan plan, *cp = nullptr;
+  if (comps) {
+    gk.lock();
+    plan.c = comps;
+    cp = &plan;
+  }
   int r = tx_acquire_host(d);
   if (r == CORDAHIP_SUCCESS && ensure_streams(d) != hipSuccess) r = CORDAHIP_ERR_HIP;
+  if (r == CORDAHIP_SUCCESS && cp && d.kryo_ev && hipStreamWaitEvent(d.stream, d.kryo_ev, 0) != hipSuccess)
+    r = CORDAHIP_ERR_HIP;  // an earlier cordahip_kryo_encode_device still using the scratch
   if (r != CORDAHIP_SUCCESS) return r;
   DeviceIds di;
   const uint64_t s0 = b->tx_sig_off[lo], s1 = b->tx_sig_off[hi];
@@ -551,11 +700,13 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   auto issue_through = [&](size_t j) -> hipError_t {  // enqueue slices [issued, j]
     const size_t j1 = std::min<size_t>(slices, j + 1);
     hipError_t e = hipSuccess;
-    if (j1 > issued) e = tx_ids_enqueue(d, &b->tx, di.tx_bound, issued, j1, ev, cev, di.ready, map_txid, map_status);
+    if (j1 > issued)
+      e = tx_ids_enqueue(d, &b->tx, di.tx_bound, issued, j1, ev, cev, di.ready, map_txid, map_status, cp);
     issued = std::max(issued, j1);
     return e;
   };
-  if (r == CORDAHIP_SUCCESS && tx_ids_prepare(d, &b->tx, di.tx_bound) != hipSuccess) r = CORDAHIP_ERR_OUT_OF_MEMORY;
+  if (r == CORDAHIP_SUCCESS && tx_ids_prepare(ctx, d, &b->tx, di.tx_bound, cp) != hipSuccess)
+    r = CORDAHIP_ERR_OUT_OF_MEMORY;
   if (r == CORDAHIP_SUCCESS && issue_through(0) != hipSuccess) r = CORDAHIP_ERR_HIP;
   // each signature signs its transaction's id (SignedTransaction.kt:98): the
   // pipeline finds it through tx_of, this shard's part built now, while the
@@ -631,12 +782,17 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   return r;
 }
 
-int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
+int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b, const cordahip_txcomp_batch* comps = nullptr) {
   const uint64_t ntx = b->tx.ntx;
   if (ntx == 0) return CORDAHIP_SUCCESS;
   if (!b->tx_sig_off || !b->first_bad_sig || !b->sig_status) return CORDAHIP_ERR_INVALID_ARG;
-  if (!b->tx.leaf_off || !b->tx.tx_leaf_off || !b->tx.txid || !b->tx.tx_status || !b->tx.leaf_bytes)
+  if (comps) {  // components instead of leaves (b->tx.tx_leaf_off = comps->tx_item_off)
+    if (!comps->tx_item_off || !comps->txid || !comps->tx_status || (comps->tx_item_off[ntx] && !comps->items) ||
+        (comps->payload_len && !comps->payload))
+      return CORDAHIP_ERR_INVALID_ARG;
+  } else if (!b->tx.leaf_off || !b->tx.tx_leaf_off || !b->tx.txid || !b->tx.tx_status || !b->tx.leaf_bytes) {
     return CORDAHIP_ERR_INVALID_ARG;
+  }
   const uint64_t nsig = b->tx_sig_off[ntx];
   if (nsig && (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off)) return CORDAHIP_ERR_INVALID_ARG;
   const double t0 = tracing() ? now_ms() : 0;
@@ -677,7 +833,7 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
   uint64_t slices = 0;
   if (const char* v = getenv("CORDAHIP_TX_SLICES")) slices = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
   const int rc = for_shards(ctx->devs, ntx, 1, [&](Device& d, uint64_t lo, uint64_t hi) {
-    return signed_tx_device(ctx, d, b, tx_of, lo, hi, slices);
+    return signed_tx_device(ctx, d, b, tx_of, lo, hi, slices, comps);
   });
   const double t_ids = tracing() ? now_ms() : 0;
   if (rc != CORDAHIP_SUCCESS) return rc;
@@ -686,6 +842,25 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b) {
             "ids, signatures and reduce done at %.2f ms\n", (unsigned long long)ntx, (unsigned long long)nsig,
             (unsigned long long)slices, t_of - t0, t_ids - t0);  // slices 0: the per-device default
   return CORDAHIP_SUCCESS;
+}
+
+// cordahip_signed_txcomp_batch as the leaf-batch descriptor the pipeline reads
+// (no leaf bytes: the slices encode them on the device), plus the components
+int signed_txcomp_impl(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* cb) {
+  cordahip_signed_tx_batch b{};
+  b.tx.ntx = cb->tx.ntx;
+  b.tx.tx_leaf_off = cb->tx.tx_item_off;  // one leaf per component
+  b.tx.txid = cb->tx.txid;
+  b.tx.tx_status = cb->tx.tx_status;
+  b.tx_sig_off = cb->tx_sig_off;
+  b.scheme = cb->scheme;
+  b.key = cb->key;
+  b.key_off = cb->key_off;
+  b.sig = cb->sig;
+  b.sig_off = cb->sig_off;
+  b.sig_status = cb->sig_status;
+  b.first_bad_sig = cb->first_bad_sig;
+  return signed_tx_impl(ctx, &b, &cb->tx);
 }
 
 // C5: one device's contiguous shard of both sections, [e0, e1) Ed25519 and
@@ -914,7 +1089,9 @@ void free_device(Device& d) {
                     &d.tx.tx_sig_off, &d.tx.msgs, &d.tx.tok, &d.tx.tok_hash, &d.tx.tx_tok_off, &d.tx.root,
                     &d.tx.stack})
     b->release();
-  for (DevBuf* b : {&d.ec.counters, &d.ec.perm, &d.ec.ws, &d.kryo_sizes, &d.kryo_temp, &d.kryo_ws}) b->release();
+  for (DevBuf* b : {&d.ec.counters, &d.ec.perm, &d.ec.ws, &d.kryo_sizes, &d.kryo_temp, &d.kryo_ws, &d.kryo_fixed,
+                    &d.kryo_items})
+    b->release();
   for (auto& w : d.ed_ws) w.release();
   for (hipEvent_t ev : {d.ec.ev, d.ed_ev[0], d.ed_ev[1], d.tx_ev, d.kryo_ev})
     if (ev) (void)hipEventDestroy(ev);
@@ -1082,6 +1259,20 @@ int cordahip_tx_submit(cordahip_ctx* ctx, const cordahip_signed_tx_batch* batch,
     *ticket = submit_job(ctx, [ctx, copy] { return signed_tx_impl(ctx, &copy); });
     return CORDAHIP_SUCCESS;
   });
+}
+
+int cordahip_txcomp_submit(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* batch, uint64_t* ticket) {
+  if (!ctx || !batch || !ticket) return CORDAHIP_ERR_INVALID_ARG;
+  const cordahip_signed_txcomp_batch copy = *batch;
+  return guarded([&] {
+    *ticket = submit_job(ctx, [ctx, copy] { return signed_txcomp_impl(ctx, &copy); });
+    return CORDAHIP_SUCCESS;
+  });
+}
+
+int cordahip_signed_txcomp_verify(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* batch) {
+  if (!ctx || !batch) return CORDAHIP_ERR_INVALID_ARG;
+  return guarded([&] { return signed_txcomp_impl(ctx, batch); });
 }
 
 int cordahip_txid_submit(cordahip_ctx* ctx, const cordahip_txid_batch* batch, uint64_t* ticket) {
@@ -1298,29 +1489,30 @@ int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_ite
     if (!d->kryo_ev && hipEventCreateWithFlags(&d->kryo_ev, hipEventDisableTiming) != hipSuccess)
       return CORDAHIP_ERR_HIP;
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    // writers: one per leaf up to 2^18 (kLevelBytes each: 2 GB of level buffers)
-    const uint64_t ws_threads = std::max<uint64_t>(256, (std::min<uint64_t>(n, 1u << 18) + 255) / 256 * 256);
+    // the direct encoder's writers (items without a template): 2^15 threads,
+    // 7 KB of level buffers each (224 MB)
+    const uint64_t dwriters = 1u << 15;
     size_t temp_bytes = 0;
-    if (kryo_scan(nullptr, temp_bytes, nullptr, nullptr, n + 1, s) != hipSuccess) return CORDAHIP_ERR_HIP;
-    if (d->kryo_sizes.cap < (n + 1) * 8 || d->kryo_temp.cap < temp_bytes ||
-        d->kryo_ws.cap < ws_threads * cordahip::kryo::kLevelBytes) {
+    if (kryo_scan_bytes(temp_bytes, n + 1, s) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (d->kryo_sizes.cap < (n + 1) * 8 || d->kryo_temp.cap < temp_bytes || d->kryo_items.cap < n * 8 + 8 ||
+        d->kryo_ws.cap < kryo_direct_ws_bytes(dwriters) || d->kryo_fixed.cap < kryo_fixed_scratch_bytes()) {
       // growing frees the old buffers: the previous user's kernels must be done
       if (hipEventSynchronize(d->kryo_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
       if (d->kryo_sizes.ensure((n + 1) * 8) || d->kryo_temp.ensure(std::max<size_t>(temp_bytes, 16)) ||
-          d->kryo_ws.ensure(ws_threads * cordahip::kryo::kLevelBytes))
+          d->kryo_items.ensure(n * 8 + 8) || d->kryo_ws.ensure(kryo_direct_ws_bytes(dwriters)) ||
+          d->kryo_fixed.ensure(kryo_fixed_scratch_bytes()))
         return CORDAHIP_ERR_OUT_OF_MEMORY;
     }
     TimedCall* tc = timed_begin(*d, s);
     if (!tc) return CORDAHIP_ERR_HIP;
-    const auto* items = static_cast<const cordahip_kryo_item*>(d_items);
-    uint64_t* sizes = d->kryo_sizes.as<uint64_t>();
-    uint8_t* status = static_cast<uint8_t*>(d_status);
+    uint32_t* slots = d->kryo_items.as<uint32_t>();
     hipError_t e = hipStreamWaitEvent(s, d->kryo_ev, 0);  // the previous user of the scratch is done
-    e = e ? e : launch_kryo_size(items, n, group, sizes, status, s);
-    size_t tb = d->kryo_temp.cap;
-    e = e ? e : kryo_scan(d->kryo_temp.p, tb, sizes, static_cast<uint64_t*>(d_off), n + 1, s);
-    e = e ? e : launch_kryo_write(items, n, group, static_cast<const uint64_t*>(d_off), static_cast<uint8_t*>(d_out),
-                                  d_out ? cap : 0, status, d->kryo_ws.as<uint8_t>(), ws_threads, s);
+    e = e ? e
+          : launch_kryo_encode(static_cast<const cordahip_kryo_item*>(d_items), nullptr, 0, n, group,
+                               d->kryo_fixed.as<uint8_t>(),
+                               slots, slots + n, d->kryo_sizes.as<uint64_t>(), static_cast<uint64_t*>(d_off),
+                               static_cast<uint8_t*>(d_out), d_out ? cap : 0, static_cast<uint8_t*>(d_status),
+                               d->kryo_ws.as<uint8_t>(), dwriters, d->kryo_temp.p, d->kryo_temp.cap, s);
     e = e ? e : hipEventRecord(d->kryo_ev, s);
     e = e ? e : hipEventRecord(tc->b, s);
     return hip_err(e);

@@ -75,13 +75,16 @@ struct Chunk {
 };
 std::vector<Chunk> make_chunks(const std::vector<Unit>& units, uint64_t chunk) {
   std::vector<Chunk> out;
+  // chunk/16, chunk/4, then chunk lanes: `chunk` (CORDAHIP_HOST_CHUNK) is the
+  // largest chunk, which sizes the pinned stages and the workspace slots
+  const uint64_t top = std::max<uint64_t>(64, chunk / 64 * 64);
   uint64_t sz = std::max<uint64_t>(64, chunk / 16 / 64 * 64);  // multiples of 64: chunks start word-aligned
   for (uint32_t u = 0; u < units.size(); u++)
     for (uint64_t a = units[u].lo; a < units[u].hi;) {
       const uint64_t b = std::min(units[u].hi, a + sz);
       out.push_back({u, a, b});
       a = b;
-      sz = std::min<uint64_t>(std::max<uint64_t>(64, 4 * chunk), 4 * sz);
+      sz = std::min<uint64_t>(top, 4 * sz);
     }
   return out;
 }

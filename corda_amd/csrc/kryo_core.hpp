@@ -18,6 +18,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/cordahip.h"
 
 #if defined(__HIPCC__)
@@ -61,7 +63,7 @@ constexpr uint32_t kName = static_cast<uint32_t>(-1);  // DefaultClassResolver.N
 // ByteArrayOutputStream) flushes in order, so level 0 is kept unbounded.
 constexpr uint32_t kChunk = 1024;
 constexpr uint32_t kMaxDepth = 8;                   // levels 0..7 (a cash-state leaf uses 0..6)
-constexpr uint32_t kLevelBytes = kMaxDepth * kChunk;  // per-encoder level buffers (level 0 unused)
+constexpr uint32_t kLevelBytes = (kMaxDepth - 1) * kChunk;  // per-encoder level buffers: levels 1..7
 
 KRYO_HD inline uint32_t kmin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
@@ -95,20 +97,59 @@ KRYO_HD inline bool operator<(const Sv& a, const Sv& b) {  // std::string order 
   return a.n < b.n;
 }
 
-struct Kout {
-  uint8_t* out;      // level 0 (the leaf); nullptr: counting
+// ---- trace symbols (KoutT<true>) -------------------------------------------
+// The GPU encoder builds one template per leaf *shape* (kryo_template.hpp): it
+// encodes a representative item once with every byte as a 32-bit symbol that
+// says where the byte comes from -- a constant of the shape, byte `off` of the
+// item's payload (optionally with bit 7 set: the last byte of an ASCII string),
+// or byte j of the item's `value` as Kryo writes it (zig-zag varlong, or
+// big-endian fixed width) -- and every item of that shape is then written from
+// the symbols (sym_byte) without running the encoder.
+constexpr uint32_t kSymConst = 0u << 30, kSymPayload = 1u << 30, kSymValZz = 2u << 30, kSymValBe = 3u << 30;
+constexpr uint32_t kSymTypeMask = 3u << 30;
+constexpr uint32_t kSymOr80 = 1u << 29;
+constexpr uint32_t kMaxPayloadOff = 1u << 21;  // payload offsets a symbol can name (bits 8..28)
+
+template <bool Trace>
+struct KoutT {
+  using Sym = typename std::conditional<Trace, uint32_t, uint8_t>::type;
+  Sym* out;          // level 0 (the leaf); nullptr: counting
   uint64_t pos = 0;  // level-0 bytes so far (also past cap)
   uint64_t cap;      // writes at or beyond cap are dropped (pos still counts them)
-  uint8_t* buf;      // kMaxDepth x kChunk level buffers; nullptr: counting
-  uint32_t stride;   // byte i of level k at buf[(k * kChunk + i) * stride] (GPU: 64, a wave's lanes interleaved)
+  Sym* buf;          // levels 1..kMaxDepth-1, kChunk each (kLevelBytes symbols); nullptr: counting
   uint32_t len[kMaxDepth];
   uint32_t depth = 0;   // the deepest level in use
   bool failed = false;  // nesting or a graph beyond the fixed tables, a bad payload
-  KRYO_HD Kout(uint8_t* o, uint64_t c, uint8_t* levels, uint32_t lane_stride = 1)
-      : out(o), cap(c), buf(levels), stride(lane_stride) {
-    len[0] = 0;
+  // trace only: the item's payload (bytes copied from it become PAYLOAD symbols)
+  // and the value tag of the bytes being written (VAL_* | byte index << 8)
+  const uint8_t* src = nullptr;
+  uint64_t src_len = 0;
+  uint32_t vtag = 0;
+  KRYO_HD KoutT(Sym* o, uint64_t c, Sym* levels) : out(o), cap(c), buf(levels) { len[0] = 0; }
+  KRYO_HD Sym& at(uint32_t k, uint32_t i) { return buf[(size_t)(k - 1) * kChunk + i]; }  // k >= 1
+  KRYO_HD void set_vtag(uint32_t t) {
+    if constexpr (Trace) vtag = t;
+    else (void)t;
   }
-  KRYO_HD uint8_t& at(uint32_t k, uint32_t i) { return buf[((size_t)k * kChunk + i) * stride]; }
+  // the symbol of byte p[j] (the byte itself when not tracing)
+  KRYO_HD Sym sym(const uint8_t* p, uint32_t j) {
+    if constexpr (Trace) {
+      const uint8_t b = p[j];
+      const uintptr_t a = (uintptr_t)(p + j), lo = (uintptr_t)src;
+      if (src && a >= lo && a - lo < src_len) {
+        if (a - lo >= kMaxPayloadOff) failed = true;
+        return kSymPayload | ((uint32_t)(a - lo) << 8) | b;
+      }
+      return vtag ? ((vtag + (j << 8)) | b) : (uint32_t)b;
+    } else {
+      return p[j];
+    }
+  }
+  KRYO_HD static void mark(Sym& x) {
+    x |= 0x80;
+    if constexpr (Trace)
+      if ((x & kSymTypeMask) == kSymPayload) x |= kSymOr80;
+  }
   KRYO_HD uint32_t push_level() {
     if (depth + 1 >= kMaxDepth) {
       failed = true;
@@ -134,32 +175,47 @@ struct Kout {
   }
   KRYO_HD void mark_last(uint32_t k) {  // the last byte written carries the end mark (ASCII strings)
     if (k == 0) {
-      if (out && pos - 1 < cap) out[pos - 1] |= 0x80;
+      if (out && pos - 1 < cap) mark(out[pos - 1]);
     } else if (buf) {
-      at(k, len[k] - 1) |= 0x80;
+      mark(at(k, len[k] - 1));
     }
   }
   KRYO_HD void copy(uint32_t k, const uint8_t* p, uint32_t n) {  // n bytes that fit
     if (k == 0) {
       if (out) {
-        if (pos + n <= cap) {
-          __builtin_memcpy(out + pos, p, n);
-        } else {
-          for (uint32_t i = 0; i < n; i++)
-            if (pos + i < cap) out[pos + i] = p[i];
+        bool done = false;
+        if constexpr (!Trace) {
+          if (pos + n <= cap) {
+            __builtin_memcpy(out + pos, p, n);
+            done = true;
+          }
         }
+        if (!done)
+          for (uint32_t i = 0; i < n; i++)
+            if (pos + i < cap) out[pos + i] = sym(p, i);
       }
       pos += n;
     } else {
       if (buf) {
-        if (stride == 1) {
+        if constexpr (!Trace) {
           __builtin_memcpy(&at(k, len[k]), p, n);
         } else {
-          for (uint32_t i = 0; i < n; i++) at(k, len[k] + i) = p[i];
+          for (uint32_t i = 0; i < n; i++) at(k, len[k] + i) = sym(p, i);
         }
       }
       len[k] += n;
     }
+  }
+  KRYO_HD void put_syms0(const Sym* p, uint32_t n) {  // a flushed level-1 chunk into the leaf
+    if (out) {
+      if (pos + n <= cap) {
+        __builtin_memcpy(out + pos, p, (size_t)n * sizeof(Sym));
+      } else {
+        for (uint32_t i = 0; i < n; i++)
+          if (pos + i < cap) out[pos + i] = p[i];
+      }
+    }
+    pos += n;
   }
   // Output.require(n) at level k. A flush writes into the level below, which may
   // itself need a flush there, and so on: D counts that nesting, so the call
@@ -245,29 +301,18 @@ struct Kout {
       chunk_bytes<D + 1>(k - 1, k, n);
     }
   }
-  // writeBytes of level src's flushed chunk (its first n bytes) into level k = src - 1
+  // writeBytes of level `from`'s flushed chunk (its first n bytes) into level k = from - 1
   template <uint32_t D>
-  KRYO_HD void chunk_bytes(uint32_t k, uint32_t src, uint32_t n) {
+  KRYO_HD void chunk_bytes(uint32_t k, uint32_t from, uint32_t n) {
     uint32_t s = 0;  // next source byte
     if (k == 0) {
-      if (!buf) {
-        pos += n;
-      } else if (stride == 1) {
-        copy(0, &at(src, 0), n);
-      } else {
-        for (; s < n; s++) put0(at(src, s));
-      }
+      if (!buf) pos += n;
+      else put_syms0(&at(from, 0), n);
       return;
     }
     uint32_t c = kmin(kChunk - len[k], n);
     for (;;) {
-      if (buf) {
-        if (stride == 1) {
-          __builtin_memcpy(&at(k, len[k]), &at(src, s), c);
-        } else {
-          for (uint32_t i = 0; i < c; i++) at(k, len[k] + i) = at(src, s + i);
-        }
-      }
+      if (buf) __builtin_memcpy(&at(k, len[k]), &at(from, s), (size_t)c * sizeof(Sym));
       len[k] += c;
       s += c;
       n -= c;
@@ -350,6 +395,7 @@ struct Kout {
     string(k, [&](uint64_t i) { return (uint32_t)(p[2 * i] | (p[2 * i + 1] << 8)); }, n);
   }
 };
+using Kout = KoutT<false>;
 
 // One object graph (Kryo.writeClassAndObject resets both at the top level):
 // DefaultClassResolver's class-name ids and CompatibleFieldSerializer's
@@ -362,10 +408,12 @@ struct Graph {
   uint32_t nheaders = 0;
   KRYO_HD Graph() {}
   // DefaultClassResolver.writeClass for a registered class: varint(id + 2)
-  KRYO_HD static void class_id(Kout& o, uint32_t k, uint32_t id) { o.varint(k, id + 2); }
+  template <class O>
+  KRYO_HD static void class_id(O& o, uint32_t k, uint32_t id) { o.varint(k, id + 2); }
   // DefaultClassResolver.writeName: NAME + 2, the graph's name id, and the class
   // name the first time the class occurs in the graph
-  KRYO_HD void class_name(Kout& o, uint32_t k, const Sv& name) {
+  template <class O>
+  KRYO_HD void class_name(O& o, uint32_t k, const Sv& name) {
     o.varint(k, kName + 2);
     for (uint32_t i = 0; i < nnames; i++)
       if (names[i] == name) {
@@ -384,8 +432,8 @@ struct Graph {
   // header (once per graph), then each field through the OutputChunked at level
   // k + 1. The fields come in sorted EXTENDED-name order (checked: an unsorted
   // list fails the leaf rather than mis-frame it).
-  template <uint32_t N, class... F>
-  KRYO_HD void cfs(Kout& o, uint32_t k, const Sv& cls, const Sv (&fields)[N], F&&... write) {
+  template <class O, uint32_t N, class... F>
+  KRYO_HD void cfs(O& o, uint32_t k, const Sv& cls, const Sv (&fields)[N], F&&... write) {
     static_assert(N == sizeof...(F), "one writer per field");
     for (uint32_t i = 1; i < N; i++)
       if (!(fields[i - 1] < fields[i])) o.failed = true;
@@ -410,7 +458,8 @@ struct Graph {
 // (registered: Ed25519PublicKeySerializer or PublicKeySerializer, Kryo.kt:383-393,
 // :441-451), then writeBytesWithLength (Kryo.kt:305-308: writeInt(size, true) +
 // writeBytes) -- the same bytes for both serializers
-KRYO_HD inline void key_value(Kout& o, uint32_t k, uint32_t key_class, const uint8_t* key, uint64_t n) {
+template <class O>
+KRYO_HD inline void key_value(O& o, uint32_t k, uint32_t key_class, const uint8_t* key, uint64_t n) {
   Graph::class_id(o, k, key_class);
   o.varint(k, (uint32_t)n);
   o.bytes(k, key, n);
@@ -471,7 +520,8 @@ struct Reader {
 // written) by implicit NAME registration (CordaClassResolver.registerImplicit), then
 // CompatibleFieldSerializer over AbstractParty.owningKey and Party.name; the name
 // through X500NameSerializer (Kryo.kt:615-624: writeBytes(encoded), no length).
-KRYO_HD inline void party_body(Kout& o, Graph& g, uint32_t k, const PartyRef& p, uint32_t x500_class) {
+template <class O>
+KRYO_HD inline void party_body(O& o, Graph& g, uint32_t k, const PartyRef& p, uint32_t x500_class) {
   auto key = [&](uint32_t c) { key_value(o, c, p.key_class, p.key, p.key_len); };
   if (p.name_len)
     g.cfs(o, k, "net.corda.core.identity.Party", {"AbstractParty.owningKey", "Party.name"}, key, [&](uint32_t c) {
@@ -481,7 +531,8 @@ KRYO_HD inline void party_body(Kout& o, Graph& g, uint32_t k, const PartyRef& p,
   else
     g.cfs(o, k, "net.corda.core.identity.AnonymousParty", {"AbstractParty.owningKey"}, key);
 }
-KRYO_HD inline void party_class_and_object(Kout& o, Graph& g, uint32_t k, const PartyRef& p, uint32_t x500_class) {
+template <class O>
+KRYO_HD inline void party_class_and_object(O& o, Graph& g, uint32_t k, const PartyRef& p, uint32_t x500_class) {
   g.class_name(o, k, p.name_len ? "net.corda.core.identity.Party" : "net.corda.core.identity.AnonymousParty");
   party_body(o, g, k, p, x500_class);
 }
@@ -490,7 +541,8 @@ KRYO_HD inline void party_class_and_object(Kout& o, Graph& g, uint32_t k, const 
 // crypto/SecureHash.kt:13-15): one field OpaqueBytes.bytes, a byte[] (a final
 // class: no class written; ByteArraySerializer accepts null, so no null marker):
 // varint(length + 1), the bytes
-KRYO_HD inline void opaque_bytes(Kout& o, Graph& g, uint32_t k, const Sv& cls, const uint8_t* b, uint64_t n) {
+template <class O>
+KRYO_HD inline void opaque_bytes(O& o, Graph& g, uint32_t k, const Sv& cls, const uint8_t* b, uint64_t n) {
   g.class_name(o, k, cls);
   g.cfs(o, k, cls, {"OpaqueBytes.bytes"}, [&](uint32_t c) {
     o.varint(c, (uint32_t)n + 1);
@@ -526,7 +578,8 @@ KRYO_HD inline bool same_key(const PartyRef& a, const PartyRef& b) {
 // Classes without a registration go by implicit NAME registration: each name's
 // string is written at its first occurrence in the graph (DefaultWhitelist.kt
 // whitelists LinkedHashSet, Currency, SingletonList, BigDecimal).
-KRYO_HD inline bool cash_state(Kout& o, const cordahip_kryo_item& it) {
+template <class O>
+KRYO_HD inline bool cash_state(O& o, const cordahip_kryo_item& it) {
   Reader r(it.data, it.data + it.len);
   const PartyRef issuer = r.party();
   const uint32_t ref_len = r.u8();
@@ -563,7 +616,11 @@ KRYO_HD inline bool cash_state(Kout& o, const cordahip_kryo_item& it) {
                           // Currency: ONE.scaleByPowerOfTen(-digits), Amount.kt:70-80
                           o.varint_zigzag(k3, (int32_t)(int8_t)scale);
                         },
-                        [&](uint32_t k3) { o.varlong_zigzag(k3, quantity); },
+                        [&](uint32_t k3) {  // the item's value: VALUE symbols when tracing
+                          o.set_vtag(kSymValZz);
+                          o.varlong_zigzag(k3, quantity);
+                          o.set_vtag(0);
+                        },
                         [&](uint32_t k3) {  // token
                           g.class_name(o, k3, "net.corda.core.contracts.Issued");
                           g.cfs(o, k3, "net.corda.core.contracts.Issued", {"Issued.issuer", "Issued.product"},
@@ -625,7 +682,8 @@ KRYO_HD inline bool cash_state(Kout& o, const cordahip_kryo_item& it) {
 // the command class's binary name, u8 key count, per key u16 LE registration id,
 // u16 LE length, the key bytes; class_id = the Arrays$ArrayList registration
 // (ArraysAsListSerializer); value = the nonce.
-KRYO_HD inline bool issue_command(Kout& o, const cordahip_kryo_item& it) {
+template <class O>
+KRYO_HD inline bool issue_command(O& o, const cordahip_kryo_item& it) {
   if (!it.data || it.len < 2) return false;
   Reader r(it.data, it.data + it.len);
   const uint32_t nlen = r.u8();
@@ -670,14 +728,19 @@ KRYO_HD inline bool issue_command(Kout& o, const cordahip_kryo_item& it) {
           // the command data: implicit NAME, its own CompatibleFieldSerializer (a
           // primitive long nonce: writeVarLong(v, false)) -- a nested OutputChunked
           g.class_name(o, k, name);
-          g.cfs(o, k, name, {simple}, [&](uint32_t c) { o.varlong_zigzag(c, it.value); });
+          g.cfs(o, k, name, {simple}, [&](uint32_t c) {
+            o.set_vtag(kSymValZz);  // the item's value: VALUE symbols when tracing
+            o.varlong_zigzag(c, it.value);
+            o.set_vtag(0);
+          });
         });
   return true;
 }
 
 // One component's leaf preimage through o (RAW: the bytes as given); false for
 // an unknown kind or a missing / malformed payload.
-KRYO_HD inline bool encode_leaf(Kout& o, const cordahip_kryo_item& it) {
+template <class O>
+KRYO_HD inline bool encode_leaf(O& o, const cordahip_kryo_item& it) {
   if (it.kind == CORDAHIP_KRYO_RAW) {
     if (it.len && !it.data) return false;
     o.bytes(0, it.data, it.len);
@@ -686,8 +749,12 @@ KRYO_HD inline bool encode_leaf(Kout& o, const cordahip_kryo_item& it) {
   const uint8_t header[8] = {'c', 'o', 'r', 'd', 'a', 0, 0, 1};  // KryoHeaderV0_1
   o.bytes(0, header, 8);
   const uint64_t v = (uint64_t)it.value;
-  auto be = [&](uint64_t x, int n) {
-    for (int i = n - 1; i >= 0; i--) o.byte(0, (uint32_t)(x >> (8 * i)));
+  auto be = [&](uint64_t x, int n) {  // the item's value, big-endian: VALUE symbols when tracing
+    for (int i = n - 1; i >= 0; i--) {
+      o.set_vtag(kSymValBe | ((uint32_t)i << 8));
+      o.byte(0, (uint32_t)(x >> (8 * i)));
+    }
+    o.set_vtag(0);
   };
   bool ok = true;
   switch (it.kind) {

@@ -39,15 +39,19 @@ hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uin
 hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
                               hipStream_t s);
 hipError_t launch_store_to_host(const void* src, void* dst, uint64_t n, hipStream_t s);
-// kryo_device.hip: the GPU Kryo leaf encoder (sizes, scan, writes)
-hipError_t launch_kryo_size(const cordahip_kryo_item* items, uint64_t n, uint32_t group, uint64_t* sizes,
-                            uint8_t* status, hipStream_t s);
-hipError_t kryo_scan(void* temp, size_t& temp_bytes, const uint64_t* sizes, uint64_t* off, uint64_t n1,
-                     hipStream_t s);
-hipError_t launch_kryo_write(const cordahip_kryo_item* items, uint64_t n, uint32_t group, const uint64_t* off,
-                             uint8_t* out, uint64_t cap, uint8_t* status, uint8_t* ws, uint64_t ws_threads,
-                             hipStream_t s);
+// kryo_device.hip: the GPU Kryo leaf encoder (shapes, templates, sizes, scan, writes)
+size_t kryo_fixed_scratch_bytes();                     // shape table + templates (per call, reused)
+size_t kryo_direct_ws_bytes(uint64_t writers);         // the direct encoder's level buffers
+hipError_t kryo_scan_bytes(size_t& bytes, uint64_t n1, hipStream_t s);
+// data_base != nullptr: items' `data` are offsets into data_len bytes at data_base
+hipError_t launch_kryo_encode(const cordahip_kryo_item* items, const uint8_t* data_base, uint64_t data_len,
+                              uint64_t n, uint32_t group, uint8_t* fixed,
+                              uint32_t* item_slot, uint32_t* direct, uint64_t* sizes, uint64_t* off, uint8_t* out,
+                              uint64_t cap, uint8_t* status, uint8_t* dws, uint64_t dwriters, void* scan_temp,
+                              size_t scan_bytes, hipStream_t s);
 hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s);
+hipError_t launch_comp_check(const uint8_t* item_status, const uint64_t* tx_item_off, uint64_t ntx, uint8_t* tx_status,
+                             hipStream_t s);
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
                             uint8_t* tx_status, hipStream_t s);
 hipError_t launch_pmt_verify(const uint32_t* leaf_hashes, const uint64_t* tx_leaf_off, const uint8_t* tok,
@@ -158,6 +162,7 @@ struct BatchStage {
 
 struct TxWork {  // device buffers of the transaction paths (grow-only)
   DevBuf leaf_bytes, leaf_off, tx_leaf_off, hashes, txid, tx_status, tx_sig_off, msgs;
+  DevBuf comp_items, payload, comp_status;  // component-level batches: items, their payload, encoder statuses
   DevBuf tok, tok_hash, tx_tok_off, root, stack;  // filtered-tx (partial Merkle tree) path
 };
 
@@ -221,10 +226,11 @@ struct Device {
   PackStage ped[kPackStages];   // dense Ed25519 rows (cordahip_ed25519_verify_host)
   BatchStage pb[kPackStages];   // generic CSR batches (cordahip_sig_verify / _submit)
   // GPU Kryo encoder scratch (cordahip_kryo_encode_device): leaf sizes, the
-  // scan's temporary storage, the writers' OutputChunked level buffers;
-  // kryo_mu orders the enqueues, kryo_ev fences reuse
+  // scan's temporary storage, the shape table and templates, per-item shape
+  // slots and the direct-encoder list, the direct writers' OutputChunked level
+  // buffers; kryo_mu orders the enqueues, kryo_ev fences reuse
   std::mutex kryo_mu;
-  DevBuf kryo_sizes, kryo_temp, kryo_ws;
+  DevBuf kryo_sizes, kryo_temp, kryo_ws, kryo_fixed, kryo_items;
   hipEvent_t kryo_ev = nullptr;
 };
 

@@ -221,6 +221,23 @@ __global__ void __launch_bounds__(256) tx_reduce_kernel(const uint8_t* __restric
   tx_status[t] = st;
 }
 
+// Component-level tx batches: a transaction with a component the Kryo encoder
+// rejected (item status != 0: invalid, or beyond the slice's leaf buffer) has
+// no id -- CORDAHIP_TX_BAD_COMPONENT (after merkle_root wrote its status).
+// item_status is indexed by absolute item number (a shifted base pointer).
+static constexpr uint8_t kTxBadComponent = 9;
+__global__ void __launch_bounds__(256) comp_check_kernel(const uint8_t* __restrict__ item_status,
+                                                        const uint64_t* __restrict__ tx_item_off, uint64_t ntx,
+                                                        uint8_t* __restrict__ tx_status) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx) return;
+  for (uint64_t i = tx_item_off[t]; i < tx_item_off[t + 1]; i++)
+    if (item_status[i] != 0) {
+      tx_status[t] = kTxBadComponent;
+      return;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // K6: FilteredTransaction.verify (MerkleTransaction.kt:134-140) ->
 // PartialMerkleTree.verify (PartialMerkleTree.kt:132-158), one lane per
@@ -362,6 +379,13 @@ hipError_t launch_store_to_host(const void* src, void* dst, uint64_t n, hipStrea
 hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(gather_rows32_kernel, dim3((uint32_t)((2 * n + 255) / 256)), dim3(256), 0, s, txid, idx, n, rows);
+  return hipGetLastError();
+}
+hipError_t launch_comp_check(const uint8_t* item_status, const uint64_t* tx_item_off, uint64_t ntx, uint8_t* tx_status,
+                             hipStream_t s) {
+  if (!ntx) return hipSuccess;
+  hipLaunchKernelGGL(comp_check_kernel, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, s, item_status, tx_item_off,
+                     ntx, tx_status);
   return hipGetLastError();
 }
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,

@@ -13,7 +13,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import EngineError, FilteredTxBatch, SigBatch, SignedTxBatch, StreamBatch, TxidBatch, check, lib
+from ._lib import (EngineError, FilteredTxBatch, SigBatch, SignedTxBatch, SignedTxcompBatch, StreamBatch, TxcompBatch,
+                   TxidBatch, check, lib)
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -159,6 +160,51 @@ class Engine:
         check(lib().cordahip_signed_tx_verify(self._ctx, ctypes.byref(sbatch)), "cordahip_signed_tx_verify")
         return res()
 
+    def signed_txcomp_verify(self, txs, sigs, async_: bool = False):
+        """cordahip_signed_txcomp_verify / cordahip_txcomp_submit: txs[t] = the transaction's components
+        as (kind, value, class_id) tuples (_lib.kryo_pack's form, availableComponents order) -- the GPU
+        writes their leaves; sigs as in signed_tx_verify. Returns (ids, tx_status, first_bad, sig_status)."""
+        comps = [c for tx in txs for c in tx]
+        blob, items, has = _lib.kryo_pack(comps)
+        items = items.copy()
+        items["data"] = np.where(has, items["data"], 0)  # offsets into the payload
+        tio = np.zeros(len(txs) + 1, dtype=np.uint64)
+        if txs:
+            tio[1:] = np.cumsum([len(tx) for tx in txs], dtype=np.uint64)
+        return self.signed_txcomp_verify_arrays(np.ascontiguousarray(blob), items, tio, sigs, async_=async_)
+
+    def signed_txcomp_verify_arrays(self, payload, items, tx_item_off, sigs, async_: bool = False):
+        """The array form: payload uint8, items KRYO_ITEM_DTYPE whose `data` are offsets into payload,
+        tx_item_off uint64[ntx + 1]; sigs[t] = [(scheme, key, sig), ...]."""
+        n = len(tx_item_off) - 1
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        items = np.ascontiguousarray(items)
+        tio = np.ascontiguousarray(tx_item_off, dtype=np.uint64)
+        txid = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        st = np.zeros(max(n, 1), dtype=np.uint8)
+        tb = TxcompBatch(n, _ptr(items) if len(items) else None, _ptr(tio), _ptr(payload) if payload.size else None,
+                         payload.size, _ptr(txid), _ptr(st))
+        flat = [x for per in sigs for x in per]
+        so = np.zeros(n + 1, dtype=np.uint64)
+        if n:
+            so[1:] = np.cumsum([len(per) for per in sigs], dtype=np.uint64)
+        sch = np.ascontiguousarray(np.asarray([x[0] for x in flat] or [0], dtype=np.uint8))
+        kb, ko = self._csr([x[1] for x in flat])
+        sb, sgo = self._csr([x[2] for x in flat])
+        sst = np.zeros(max(len(flat), 1), dtype=np.uint8)
+        fb = np.zeros(max(n, 1), dtype=np.int64)
+        sbatch = SignedTxcompBatch(tb, _ptr(so), _ptr(sch), _ptr(kb), _ptr(ko), _ptr(sb), _ptr(sgo), _ptr(sst),
+                                   _ptr(fb))
+        res = lambda: (txid[:n], st[:n], fb[:n], sst[:len(flat)])  # noqa: E731
+        keep = (payload, items, tio, txid, st, so, sch, kb, ko, sb, sgo, sst, fb, tb, sbatch)
+        if async_:
+            t = ctypes.c_uint64()
+            check(lib().cordahip_txcomp_submit(self._ctx, ctypes.byref(sbatch), ctypes.byref(t)),
+                  "cordahip_txcomp_submit")
+            return Ticket(self, t.value, res, keep)
+        check(lib().cordahip_signed_txcomp_verify(self._ctx, ctypes.byref(sbatch)), "cordahip_signed_txcomp_verify")
+        return res()
+
     def signed_tx_verify_ed25519_device(self, leaf_bytes, leaf_off, tx_leaf_off, tx_sig_off, keys, sigs,
                                         txid, tx_status, first_bad, sig_status, device: int = 0, stream=None):
         s = stream.cuda_stream if stream is not None else 0
@@ -184,15 +230,19 @@ class Engine:
         the GPU: the blob and the rebased items go to the device, then cordahip_kryo_encode_device.
         cap None: sized by a first pass. Synchronous (returns host-visible results): (leaves uint8
         device tensor, off int64 device tensor [n + 1], status uint8 device tensor [n])."""
+        import contextlib
+
         import torch
         dev = torch.device("cuda", device)
-        d_blob = torch.from_numpy(np.ascontiguousarray(blob)).to(dev)
-        a = np.array(items, copy=True)
-        a["data"] = np.where(has, a["data"] + np.uint64(d_blob.data_ptr()), 0)
-        d_items = torch.from_numpy(a.view(np.uint8)).to(dev)
-        n = len(a)
-        off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        status = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
+        # the copies and zero fills are ordered before the encoder on `stream`
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            d_blob = torch.from_numpy(np.ascontiguousarray(blob)).to(dev)
+            a = np.array(items, copy=True)
+            a["data"] = np.where(has, a["data"] + np.uint64(d_blob.data_ptr()), 0)
+            d_items = torch.from_numpy(a.view(np.uint8)).to(dev)
+            n = len(a)
+            off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            status = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
         if cap is None:
             self.kryo_encode_device(d_items, n, None, off, status, group, device, stream)
             torch.cuda.synchronize(dev)

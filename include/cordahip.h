@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CORDAHIP_ABI_VERSION 2u
+#define CORDAHIP_ABI_VERSION 3u
 
 /* ---- per-lane statuses (status[i]) ------------------------------------- */
 #define CORDAHIP_STATUS_OK 0            /* isValid -> true;  doVerify -> true                         */
@@ -349,7 +349,9 @@ int cordahip_filtered_tx_submit(cordahip_ctx* ctx, const cordahip_filtered_tx_ba
  * class_id = kryo.getRegistration(cls).id on the node (registration order of
  * DefaultKryoCustomizer.kt is fixed per build; the JVM reads it once).
  * off[0..n] receives the CSR offsets; returns CORDAHIP_ERR_BUFFER_TOO_SMALL with
- * off[n] = the bytes needed when cap is too small. Host-only: no device work. */
+ * off[n] = the bytes needed when cap is too small, and CORDAHIP_ERR_INVALID_ARG
+ * at the first invalid item -- `out` (and off) are then left partly written:
+ * the leaves before that item are in place. Host-only: no device work. */
 #define CORDAHIP_ERR_BUFFER_TOO_SMALL (-8)
 #define CORDAHIP_KRYO_RAW 0
 #define CORDAHIP_KRYO_CHAR 1
@@ -386,11 +388,57 @@ int cordahip_kryo_encode(const cordahip_kryo_item* items, uint64_t n, uint8_t* o
  * (as cordahip_kryo_encode would reject it; size 0), 2 not written because it
  * ends beyond cap. Enqueued on hip_stream, asynchronous; the caller reads
  * d_off[n] / d_status when it needs them. Same encoder as cordahip_kryo_encode
- * (corda_amd/csrc/kryo_core.hpp): bit-identical leaves. n < 2^31 - 1 per call.
- * Device scratch (grow-only, per device): 8 B per item + 8 KB per writer thread
- * (at most 2^18 writers: 2 GB). */
+ * (corda_amd/csrc/kryo_core.hpp): bit-identical leaves; items of one shape
+ * (equal structure, kryo_template.hpp) are written from a template traced once
+ * per shape. d_out NULL: sizes and offsets only (statuses 0 / 1). n < 2^31 - 1
+ * per call. Device scratch (grow-only, per device): 16 B per item, ~18 MB of
+ * shape table and templates, 224 MB of level buffers for the items written
+ * without a template. */
 int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_items, uint64_t n, uint32_t group,
                                 void* d_out, uint64_t cap, void* d_off, void* d_status, void* hip_stream);
+
+/* ---- component-level SignedTransaction batches (SURVEY §8b + §8f rank 4) ---- *
+ * cordahip_signed_tx_verify with each transaction's COMPONENTS instead of their
+ * serialised leaves: the JVM hands over the Kryo items of availableComponents
+ * (MerkleTransaction.kt:51-62) and the GPU writes the leaf preimages
+ * (serializedHash, MerkleTransaction.kt:16-18; the encoder of
+ * cordahip_kryo_encode_device) ahead of K3 / K4, so tx ids need no JVM
+ * re-serialisation and PCIe carries the components (~600 B per cash-issue
+ * transaction) instead of the leaves (1,717 B). Replaces the same reference
+ * calls as cordahip_tx_submit: SignedTransaction.checkSignaturesAreValid
+ * (SignedTransaction.kt:95-100) + the id of verifySignatures (:70-85,
+ * WireTransaction.kt:48).
+ * items[i].data is an OFFSET into `payload` (not a pointer); any number of
+ * items may share a payload (the notary Party, TransactionType). The payload
+ * crosses PCIe as a growing prefix, slice by slice: laid out in transaction
+ * order (shared payloads first) the first slice's copy stays short. An item
+ * whose payload runs past payload_len, or that cordahip_kryo_encode would
+ * reject, makes its transaction CORDAHIP_TX_BAD_COMPONENT (its id is not
+ * computed; serialise that transaction on the JVM and use RAW leaves).
+ * Signature fields, outputs and statuses as in cordahip_signed_tx_batch.     */
+#define CORDAHIP_TX_BAD_COMPONENT 9
+typedef struct {
+  uint64_t ntx;
+  const cordahip_kryo_item* items; /* [nitems] components, tx by tx, availableComponents order */
+  const uint64_t* tx_item_off;     /* [ntx+1] items of tx t: [tx_item_off[t], tx_item_off[t+1]) */
+  const uint8_t* payload;          /* item payloads (data = offsets into it) */
+  uint64_t payload_len;
+  uint8_t* txid;      /* [ntx*32] out */
+  uint8_t* tx_status; /* [ntx] out */
+} cordahip_txcomp_batch;
+typedef struct {
+  cordahip_txcomp_batch tx;
+  const uint64_t* tx_sig_off; /* [ntx+1] */
+  const uint8_t* scheme;      /* [nsig] */
+  const uint8_t* key;
+  const uint64_t* key_off;
+  const uint8_t* sig;
+  const uint64_t* sig_off;
+  uint8_t* sig_status;    /* [nsig] out */
+  int64_t* first_bad_sig; /* [ntx] out */
+} cordahip_signed_txcomp_batch;
+int cordahip_signed_txcomp_verify(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* batch);
+int cordahip_txcomp_submit(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* batch, uint64_t* ticket);
 
 /* Device time (ms) of the calling thread's most recent *_device call on
  * `device`, from HIP events recorded around its launches on the stream it ran

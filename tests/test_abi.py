@@ -42,8 +42,8 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_abi_version_and_errors(lib):
     from corda_amd import _lib
-    assert lib.cordahip_abi_version() == _lib.ABI_VERSION == 2
-    assert "#define CORDAHIP_ABI_VERSION 2u" in open(HEADER).read()
+    assert lib.cordahip_abi_version() == _lib.ABI_VERSION == 3
+    assert "#define CORDAHIP_ABI_VERSION 3u" in open(HEADER).read()
     assert lib.cordahip_strerror(0) == b"success"
     assert lib.cordahip_strerror(-7) == b"not implemented on the GPU path"
     assert lib.cordahip_strerror(12345) == b"unknown error"

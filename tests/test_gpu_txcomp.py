@@ -1,0 +1,190 @@
+"""Component-level SignedTransaction batches (cordahip_signed_txcomp_verify /
+cordahip_txcomp_submit): the JVM hands over each transaction's components as
+Kryo items and the GPU writes their leaves (the template encoder) before K3/K4.
+
+Checked against (a) the C oracle's tx ids over the Python restatement's leaves
+(oracle/kryo_leaves.py), and (b) the leaf-level path (cordahip_signed_tx_verify
+over the host encoder's leaves) output by output: ids, tx statuses,
+first_bad_sig and every signature status -- including signatures corrupted,
+transactions with a component the encoder rejects (CORDAHIP_TX_BAD_COMPONENT),
+with no components (NO_LEAVES) and without signatures (NO_SIGNATURES), payloads
+shared by many items, multi-slice shards and the ticketed form."""
+import ctypes
+import hashlib
+import os
+import random
+
+import numpy as np
+import pytest
+
+import kryo_leaves as K
+import test_kryo as TK
+from corda_amd import _lib
+from corda_amd.corpus import cash_issue_items
+
+pytestmark = pytest.mark.gpu
+ED = 4
+
+
+def _sign(oracle, seed, msg):
+    pub, sig = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+    oracle.oracle_ed25519_sign(seed, msg, len(msg), pub, sig)
+    return pub.raw, sig.raw
+
+
+def _oracle_id(oracle, leaves):
+    out = ctypes.create_string_buffer(32)
+    blob = np.frombuffer(b"".join(leaves) or b"\0", np.uint8).copy()
+    off = np.zeros(len(leaves) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in leaves])
+    rc = oracle.oracle_tx_id(blob.ctypes.data, off.ctypes.data, len(leaves), out)
+    return out.raw if rc == 0 else None
+
+
+def _random_txs(rng, ntx):
+    """(components per tx in the restatement's form, the same in the library's form)"""
+    ref_keys = [bytes.fromhex(v["A"]) for v in TK._key_vectors()]
+    pool = TK._random_items(rng)
+    spec = []
+    for t in range(ntx):
+        comps = []
+        for _ in range(rng.choice([1, 2, 5, 5, 5, 7])):
+            r = rng.random()
+            if r < 0.3:
+                comps.append(("cash_state", TK._cash_state(rng, ref_keys, big=t % 37 == 0), 52))
+            elif r < 0.45:
+                comps.append(("party", TK._party(rng, ref_keys), 52))
+            elif r < 0.6:
+                comps.append(("issue_command", ("net.corda.contracts.asset.Cash$Commands$Issue",
+                                                rng.randrange(-2**63, 2**63),
+                                                [(45, rng.choice(ref_keys)) for _ in range(rng.randrange(1, 4))]), 10))
+            else:
+                comps.append(rng.choice(pool))
+        spec.append(comps)
+    lib_form = [[(k, _bits(k, v), c) for k, v, c in comps] for comps in spec]
+    return spec, lib_form
+
+
+def _bits(k, v):
+    import struct
+    if k == "float":
+        return struct.unpack(">i", struct.pack(">f", v))[0]
+    if k == "double":
+        return struct.unpack(">q", struct.pack(">d", v))[0]
+    return v
+
+
+def _signers(oracle, rng, ids, ntx, corrupt=0.05):
+    sigs = []
+    for t in range(ntx):
+        per = []
+        for q in range(rng.choice([0, 1, 2, 3]) if t % 50 == 7 else rng.choice([1, 2, 3])):
+            pub, sg = _sign(oracle, hashlib.sha256(b"txc%d-%d" % (t, q)).digest(), ids[t] if ids[t] else b"\0" * 32)
+            sg = bytearray(sg)
+            if rng.random() < corrupt:
+                sg[rng.randrange(64)] ^= 1 << rng.randrange(8)
+            per.append((ED, pub, bytes(sg)))
+        sigs.append(per)
+    return sigs
+
+
+def _compare(engine, leaves_per_tx, comp_result, sigs):
+    """the component path's outputs == the leaf path's over the host encoder's leaves"""
+    ids_l, st_l, fb_l, sst_l = engine.signed_tx_verify(leaves_per_tx, sigs)
+    ids_c, st_c, fb_c, sst_c = comp_result
+    assert np.array_equal(st_c, st_l)
+    assert np.array_equal(fb_c, fb_l)
+    assert np.array_equal(sst_c, sst_l)
+    assert np.array_equal(ids_c[st_l == 0], ids_l[st_l == 0])
+
+
+def test_components_vs_oracle_and_leaf_path(engine, oracle):
+    rng = random.Random(51)
+    ntx = 400
+    spec, comps = _random_txs(rng, ntx)
+    comps[3] = []  # no components: MerkleTreeException (NO_LEAVES)
+    spec[3] = []
+    leaves = [[K.leaf(k, v, c) for k, v, c in tx] for tx in spec]
+    ids = [_oracle_id(oracle, lv) if lv else None for lv in leaves]
+    sigs = _signers(oracle, rng, ids, ntx)
+    res = engine.signed_txcomp_verify(comps, sigs)
+    got_ids, st, fb, sst = res
+    for t in range(ntx):
+        if ids[t] is not None and sigs[t]:
+            assert got_ids[t].tobytes() == ids[t], t
+    assert st[3] == _lib.TX_NO_SIGNATURES or st[3] == _lib.TX_NO_LEAVES
+    assert (st == _lib.TX_NO_SIGNATURES).sum() >= 1 and (st == 1).sum() >= 5 and (st == 0).sum() > 200
+    _compare(engine, leaves, res, sigs)
+
+
+def test_bad_components(engine, oracle):
+    """an invalid component (cordahip_kryo_encode rejects it) or one whose payload runs past the
+    payload's end: CORDAHIP_TX_BAD_COMPONENT, its signatures carry that status, first_bad -1"""
+    rng = random.Random(52)
+    ref_keys = [bytes.fromhex(v["A"]) for v in TK._key_vectors()]
+    good = [("cash_state", TK._cash_state(rng, ref_keys), 52), ("ed25519_key", ref_keys[0], 45),
+            ("kotlin_object", K.TRANSACTION_TYPE_GENERAL, 0)]
+    bad = [("ed25519_key", b"k" * 31, 45)]
+    txs = [good, good[:2] + bad, good, [bad[0]], good]
+    leaves_ok = [K.leaf(k, v, c) for k, v, c in good]
+    tid = _oracle_id(oracle, leaves_ok)
+    sigs = [[(ED,) + _sign(oracle, b"\x11" * 32, tid)] for _ in txs]
+    ids, st, fb, sst = engine.signed_txcomp_verify(txs, sigs)
+    assert list(st) == [0, _lib.TX_BAD_COMPONENT, 0, _lib.TX_BAD_COMPONENT, 0]
+    assert list(fb) == [-1] * 5 and list(sst) == [0, 9, 0, 9, 0]
+    assert ids[0].tobytes() == tid and ids[4].tobytes() == tid
+    # a payload offset past the end of the payload
+    blob, items, has = _lib.kryo_pack([c for tx in txs[:1] for c in tx])
+    items = items.copy()
+    items["data"] = np.where(has, items["data"], 0)
+    items2 = np.concatenate([items, items])
+    items2[4]["data"] = len(blob) - 3  # the second tx's key: 32 bytes from 3 before the end
+    tio = np.array([0, 3, 6], np.uint64)
+    ids, st, fb, sst = engine.signed_txcomp_verify_arrays(blob, items2, tio, sigs[:2])
+    assert list(st) == [0, _lib.TX_BAD_COMPONENT] and ids[0].tobytes() == tid
+
+
+@pytest.mark.parametrize("chunk", [None, "4096"])
+def test_cash_issue_corpus_many_slices(engine, oracle, chunk):
+    """the bench's cash-issue components (payloads shared by every transaction: the notary Party
+    and TransactionType) through the component path, in one or many id slices, against the leaf
+    path over the host encoder's leaves and the oracle's ids; plus the ticketed form"""
+    torch = pytest.importorskip("torch")  # noqa: F841
+    rng = np.random.default_rng(53)
+    ntx = 12000
+    ik = rng.integers(0, 256, (ntx, 32), dtype=np.uint8)
+    blob, items, _ = cash_issue_items(ik, rng.integers(0, 256, (ntx, 32), dtype=np.uint8), bytes(range(32)),
+                                      rng.integers(1, 10**9, ntx), rng.integers(-2**63, 2**63 - 1, ntx))
+    it = items.reshape(-1).copy()
+    host_it = it.copy()
+    host_it["data"] += np.uint64(blob.ctypes.data)
+    hb, ho = _lib.kryo_encode_array(host_it)
+    leaves = [[hb[int(ho[5 * t + j]):int(ho[5 * t + j + 1])].tobytes() for j in range(5)] for t in range(ntx)]
+    ids = [_oracle_id(oracle, leaves[t]) for t in range(0, ntx, 997)]
+    # signatures: one per tx over the (leaf-path) id, every 10th corrupted
+    ids_l, _ = engine.tx_ids(leaves)
+    sigs = []
+    for t in range(ntx):
+        pub, sg = _sign(oracle, hashlib.sha256(b"c4c%d" % t).digest(), ids_l[t].tobytes())
+        if t % 10 == 3:
+            sg = sg[:5] + bytes([sg[5] ^ 4]) + sg[6:]
+        sigs.append([(ED, pub, sg)] * (1 + t % 3))
+    tio = np.arange(0, 5 * ntx + 1, 5, dtype=np.uint64)
+    old = os.environ.get("CORDAHIP_TX_SIG_CHUNK")
+    if chunk:
+        os.environ["CORDAHIP_TX_SIG_CHUNK"] = chunk
+    try:
+        res = engine.signed_txcomp_verify_arrays(blob, it, tio, sigs)
+        tk = engine.signed_txcomp_verify_arrays(blob, it, tio, sigs, async_=True)
+        res2 = tk.wait()
+    finally:
+        if chunk:
+            if old is None:
+                del os.environ["CORDAHIP_TX_SIG_CHUNK"]
+            else:
+                os.environ["CORDAHIP_TX_SIG_CHUNK"] = old
+    for a, b in zip(res, res2):
+        assert np.array_equal(a, b)
+    assert [res[0][t].tobytes() for t in range(0, ntx, 997)] == ids
+    assert (res[1] == 0).sum() == ntx - len(range(3, ntx, 10))
+    _compare(engine, leaves, res, sigs)
