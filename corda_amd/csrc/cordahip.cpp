@@ -212,6 +212,39 @@ uint64_t env_lanes(const char* name, uint64_t dflt) {
   return x >= 64 ? x / 64 * 64 : dflt;
 }
 
+// The Kryo encoder's persistent state ready for a call on stream s (kryo_mu
+// held, d.kryo_fixed allocated): zeroed when freshly allocated; cleared when the
+// usage the last call reported passes half the table or nearly fills the
+// template arena (recurring shapes then rebuild once).
+hipError_t kryo_state_ready(Device& d, hipStream_t s) {
+  if (!d.kryo_usage) {
+    void* h = nullptr;
+    void* dp = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped) != hipSuccess) return hipErrorOutOfMemory;
+    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) return hipErrorUnknown;
+    std::memset(h, 0, 64);
+    d.kryo_usage = static_cast<uint32_t*>(h);
+    d.kryo_usage_dev = static_cast<uint32_t*>(dp);
+  }
+  const volatile uint32_t* u = d.kryo_usage;
+  if (d.kryo_fresh || u[0] > kryo_clear_threshold_templates() || u[1] > kryo_clear_threshold_slots()) {
+    d.kryo_fresh = false;
+    d.kryo_usage[0] = d.kryo_usage[1] = 0;
+    return kryo_clear(d.kryo_fixed.as<uint8_t>(), s);
+  }
+  return hipSuccess;
+}
+// after a call's encoder launches: its usage counters to the host-mapped copy
+hipError_t kryo_usage_report(Device& d, hipStream_t s) {
+  return launch_store_to_host(kryo_usage_src(d.kryo_fixed.as<uint8_t>()), d.kryo_usage_dev, 8, s);
+}
+// grows kryo_fixed if needed (once: its size is fixed), marking it fresh
+hipError_t kryo_fixed_ensure(Device& d) {
+  if (d.kryo_fixed.cap >= kryo_fixed_scratch_bytes()) return hipSuccess;
+  d.kryo_fresh = true;
+  return d.kryo_fixed.ensure(kryo_fixed_scratch_bytes());
+}
+
 // Enqueue ECDSA verification of n slot-layout lanes on stream s (device current,
 // d.ec_mu held): the shared work buffers are reused only after their previous
 // user's kernels (on whatever stream) have finished.
@@ -470,9 +503,10 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batc
       if (d.kryo_ev && hipEventSynchronize(d.kryo_ev) != hipSuccess) return hipErrorUnknown;
       if (d.kryo_sizes.ensure((n + 1) * 8) || d.kryo_temp.ensure(std::max<size_t>(temp_bytes, 16)) ||
           d.kryo_items.ensure(n * 8 + 8) || d.kryo_ws.ensure(kryo_direct_ws_bytes(CompPlan::kDirectWriters)) ||
-          d.kryo_fixed.ensure(kryo_fixed_scratch_bytes()))
+          kryo_fixed_ensure(d))
         return hipErrorOutOfMemory;
     }
+    if (hipError_t e = kryo_state_ready(d, d.stream)) return e;
   } else {
     leaf_buf = b->leaf_off[l1] - b->leaf_off[l0];
   }
@@ -565,7 +599,8 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
   if (e == hipSuccess && j1 + 1 == bound.size()) {
     e = hipEventRecord(d.tx_ev, s);  // the last slice: fence d.tx
     if (cp && e == hipSuccess) {     // and the encoder's scratch (d.kryo_*)
-      if (!d.kryo_ev) e = hipEventCreateWithFlags(&d.kryo_ev, hipEventDisableTiming);
+      e = kryo_usage_report(d, s);
+      if (!d.kryo_ev) e = e ? e : hipEventCreateWithFlags(&d.kryo_ev, hipEventDisableTiming);
       e = e ? e : hipEventRecord(d.kryo_ev, s);
     }
   }
@@ -1093,6 +1128,8 @@ void free_device(Device& d) {
                     &d.kryo_items})
     b->release();
   for (auto& w : d.ed_ws) w.release();
+  if (d.kryo_usage) (void)hipHostFree(d.kryo_usage);
+  d.kryo_usage = d.kryo_usage_dev = nullptr;
   for (hipEvent_t ev : {d.ec.ev, d.ed_ev[0], d.ed_ev[1], d.tx_ev, d.kryo_ev})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& tc : d.ring)
@@ -1500,19 +1537,21 @@ int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_ite
       if (hipEventSynchronize(d->kryo_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
       if (d->kryo_sizes.ensure((n + 1) * 8) || d->kryo_temp.ensure(std::max<size_t>(temp_bytes, 16)) ||
           d->kryo_items.ensure(n * 8 + 8) || d->kryo_ws.ensure(kryo_direct_ws_bytes(dwriters)) ||
-          d->kryo_fixed.ensure(kryo_fixed_scratch_bytes()))
+          kryo_fixed_ensure(*d))
         return CORDAHIP_ERR_OUT_OF_MEMORY;
     }
     TimedCall* tc = timed_begin(*d, s);
     if (!tc) return CORDAHIP_ERR_HIP;
     uint32_t* slots = d->kryo_items.as<uint32_t>();
     hipError_t e = hipStreamWaitEvent(s, d->kryo_ev, 0);  // the previous user of the scratch is done
+    e = e ? e : kryo_state_ready(*d, s);
     e = e ? e
           : launch_kryo_encode(static_cast<const cordahip_kryo_item*>(d_items), nullptr, 0, n, group,
                                d->kryo_fixed.as<uint8_t>(),
                                slots, slots + n, d->kryo_sizes.as<uint64_t>(), static_cast<uint64_t*>(d_off),
                                static_cast<uint8_t*>(d_out), d_out ? cap : 0, static_cast<uint8_t*>(d_status),
                                d->kryo_ws.as<uint8_t>(), dwriters, d->kryo_temp.p, d->kryo_temp.cap, s);
+    e = e ? e : kryo_usage_report(*d, s);
     e = e ? e : hipEventRecord(d->kryo_ev, s);
     e = e ? e : hipEventRecord(tc->b, s);
     return hip_err(e);

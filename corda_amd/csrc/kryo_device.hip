@@ -7,26 +7,34 @@
 //
 // Leaves are written from per-shape templates (kryo_template.hpp), not by
 // running the byte-sequential encoder once per item:
-//   1. kryo_shape: every item's shape (the inputs the encoder branches on),
-//      hashed into a 2^16-slot table; the first item of a shape claims a slot
-//      (one 64-bit CAS: hash | item) and becomes its representative; equal
-//      hashes are confirmed with same_shape, so a collision costs a probe,
-//      never a wrong leaf.
-//   2. kryo_build: one wave per shape traces its representative through the
-//      encoder (KoutT<true>, the OutputChunked level buffers in LDS): a
-//      symbol per leaf byte -- a constant, payload byte k, or byte j of the
-//      item's value.
-//   3. kryo_tsize: every item's size from its shape (RAW: its length); items
-//      without a shape, or whose shape has no template, go on a list for the
-//      direct encoder, which sizes them (kryo_dsize, counting mode).
+//   1. kryo_shape: every item's shape hash (a streaming walk of the inputs the
+//      encoder branches on) picks a slot of a 2^16-slot table; an empty slot is
+//      claimed with one 64-bit CAS (hash | item) and the item becomes the
+//      shape's representative.
+//   2. kryo_build: one wave per NEW shape records the representative's shape
+//      (structure words and span bytes, ShapeRec) in the slot and traces it
+//      through the encoder (KoutT<true>, the OutputChunked level buffers in
+//      LDS): a symbol per leaf byte -- a constant, payload byte k, or byte j of
+//      the item's value -- stored in 4 copies shifted by 0..3 bytes, so every
+//      output dword reads its 4 symbols with one aligned 16-byte load.
+//   3. kryo_tsize: every item is compared with its slot's record
+//      (shape_matches: exact; the hash only picked the slot) and sized from
+//      the template (RAW: its length); items without a shape, with a hash
+//      collision, or whose shape has no template go on a list for the direct
+//      encoder, which sizes them (kryo_dsize, counting mode).
 //   4. an exclusive scan of the sizes into the CSR offsets (hipcub).
-//   5. kryo_twrite: a wave per 8 consecutive leaves writes their bytes in
+//   5. kryo_twrite: a wave per 32 consecutive leaves writes their bytes in
 //      output order, one aligned dword per lane (64 lanes = 256 contiguous
-//      bytes per store instruction), each byte from its template symbol; the
-//      dword a leaf ends in carries the next leaves' first bytes.
+//      bytes per store instruction); a dword of constant symbols is 4 selects,
+//      payload and value bytes are fetched per byte; the dword a leaf ends in
+//      carries the next leaves' first bytes.
 //   6. kryo_dwrite: the listed items through the direct encoder (per-thread
 //      level buffers in a workspace), after kryo_twrite: their byte stores
 //      replace what kryo_twrite left in the dwords they share.
+// The table, the records and the templates persist across calls on a device
+// (a template is derived metadata of a shape, never a cached leaf: every call
+// writes every leaf from its own items), so batches of recurring shapes build
+// nothing; the host clears the table when it passes half full.
 // r04 ran the direct encoder for every item: 80.5 KB of L2-fabric traffic per
 // cash-issue transaction (the level buffers' round trips) against 1,717 B of
 // leaves, 5.0 + 17.9 ms per 6.25 M leaves (profiles/r04_pmc_kryo_traffic.json).
@@ -44,13 +52,34 @@ using kryo::kChunk;
 
 constexpr uint32_t kSlots = 1u << 16;      // shape table slots (a power of two)
 constexpr uint32_t kMaxProbe = 64;         // linear probes before an item goes to the direct encoder
-constexpr uint32_t kBuilders = 1024;       // templates per call (more shapes: direct encoder)
-constexpr uint32_t kTmplSyms = 4096;       // symbols per template (longer leaves: direct encoder)
+constexpr uint32_t kBuilders = 512;        // templates the arena holds (more shapes: direct encoder)
+constexpr uint32_t kTmplSyms = 4096;       // leaf bytes a template covers (longer leaves: direct encoder)
+// One template in the arena (byte offsets; kryo_build writes it, kryo_twrite reads it):
+//   syms [kTmplSyms] u32   the traced symbols, one per leaf byte (the byte-by-byte path)
+//   tb   [16][kTB] u8      copy c: leaf byte i at 16 + c + i if it is a constant, 0 where it
+//                          is patched and in the pads -- for a leaf starting at output address
+//                          a, copy (a & 15) lines its bytes up with the 16-byte output blocks
+//   desc [16][kBlk] u64    per copy and 16-byte block: the patched bytes' mask (bits 0..15),
+//                          the block's kind (bits 16..17: 0 constants only, 1 every patched
+//                          byte t is payload byte delta + t, 2 anything else: byte by byte),
+//                          delta (bits 32..63, signed)
+//   work [2][kTmplSyms] u8 the builder's byte scratch
+constexpr uint32_t kTB = kTmplSyms + 48;   // 16 pad + up to 15 shift + the leaf + 16 pad + 1 (a multiple of 16)
+constexpr uint32_t kBlk = kTB / 16;        // blocks per copy
+constexpr size_t kOffTb = (size_t)kTmplSyms * 4, kOffDesc = kOffTb + 16 * (size_t)kTB,
+                 kOffWork = kOffDesc + 16 * (size_t)kBlk * 8,
+                 kTmplBytes = (kOffWork + 2 * (size_t)kTmplSyms + 255) / 256 * 256;
+constexpr size_t kTmplWords = kTmplBytes / 4;
+constexpr uint32_t kDescConst = 0, kDescLinear = 1, kDescBytes = 2;
 constexpr uint32_t kNoSlot = 0xffffffffu;  // item_slot: no shape (direct encoder)
 constexpr uint32_t kRawSlot = 0xfffffffeu; // item_slot: a RAW leaf (copied)
-constexpr int32_t kInvalid = -1, kNoTemplate = -2;
-constexpr uint32_t kLeavesPerWave = 8;
+constexpr int32_t kNoTemplate = -2, kUnbuilt = -3;  // slot_size values besides a size (-1: an invalid shape)
+constexpr uint32_t kDefer = 0x80000000u;  // item_slot: the slot was claimed this call (verified in kryo_tsize)
+constexpr uint32_t kLeavesPerWave = 16;  // a wave writes the output span of this many leaves
 constexpr uint32_t kLevelSyms = kryo::kLevelBytes;  // levels 1..7 (level 0 is the leaf itself)
+// counters: [0] new shapes this call, [1] direct items this call, [2] templates
+// in the arena, [3] table slots in use (the last two persist with the table)
+enum { kCNew = 0, kCDirect = 1, kCArena = 2, kCUsed = 3 };
 
 // Items as the encoder sees them. base == nullptr: `data` are device pointers
 // (cordahip_kryo_encode_device). Otherwise `data` are offsets into a payload of
@@ -81,94 +110,178 @@ __device__ inline uint64_t item_of(uint64_t j, uint64_t n, uint32_t group) {
 }
 
 // ---- 1. shapes ------------------------------------------------------------------
-__global__ void __launch_bounds__(256) kryo_shape_kernel(ItemSrc items, uint64_t n,
-                                                         uint32_t group, unsigned long long* __restrict__ table,
+// An item whose slot holds a shape built by an earlier call is compared with
+// the slot's record and sized here; one whose slot was claimed in this call
+// (slot_size still kUnbuilt) is compared after kryo_build, in kryo_tsize.
+__device__ inline void direct_item(uint32_t* direct, uint32_t* counters, uint64_t i) {
+  direct[atomicAdd(&counters[kCDirect], 1u)] = (uint32_t)i;  // sized by kryo_dsize
+}
+
+// the size and status of an item of slot `slot` (built): false when it goes to the direct encoder
+__device__ inline bool template_item(const cordahip_kryo_item& it, const kryo::ShapeRec& rec, int32_t z,
+                                     uint64_t& size, uint8_t& st) {
+  if (z == kNoTemplate || !kryo::shape_matches(it, rec)) return false;  // exact: a hash collision goes direct
+  size = z >= 0 ? (uint64_t)z : 0;
+  st = z >= 0 ? 0 : 1;  // an invalid shape: the encoder rejects every item of it
+  return true;
+}
+
+__global__ void __launch_bounds__(256) kryo_shape_kernel(ItemSrc items, uint64_t n, uint32_t group,
+                                                         unsigned long long* __restrict__ table,
+                                                         const int32_t* __restrict__ slot_size,
+                                                         const kryo::ShapeRec* __restrict__ rec,
                                                          uint32_t* __restrict__ item_slot, uint32_t* __restrict__ shape_list,
-                                                         uint32_t* __restrict__ counters) {
+                                                         uint64_t* __restrict__ sizes, uint8_t* __restrict__ status,
+                                                         uint32_t* __restrict__ direct, uint32_t* __restrict__ counters) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j == 0) sizes[n] = 0;  // the scan's last element: off[n] = the total
   if (j >= n) return;
   const uint64_t i = item_of(j, n, group);
   const cordahip_kryo_item it = items[i];
+  uint64_t size = 0;
+  uint8_t st = 0;
   if (it.kind == CORDAHIP_KRYO_RAW) {
     item_slot[i] = kRawSlot;
+    if (it.len && !it.data) st = 1;
+    else size = it.len;
+    sizes[i] = size;
+    status[i] = st;
     return;
   }
-  const kryo::Shape s = kryo::shape_of(it);
+  uint64_t h = 0;
   uint32_t slot = kNoSlot;
-  if (s.ok) {
-    const uint64_t h = kryo::shape_hash(s);
-    const unsigned long long mine = ((unsigned long long)(uint32_t)(h >> 32) << 32) | (unsigned long long)(i + 1);
+  bool claimed = false;
+  if (kryo::shape_hash_of(it, h)) {
+    const uint32_t tag = (uint32_t)(h >> 32);
+    const unsigned long long mine = ((unsigned long long)tag << 32) | (unsigned long long)(i + 1);
     uint32_t k = (uint32_t)h & (kSlots - 1);
     for (uint32_t probe = 0; probe < kMaxProbe; probe++, k = (k + 1) & (kSlots - 1)) {
       unsigned long long v = __hip_atomic_load(&table[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (v == 0) {
         v = atomicCAS(&table[k], 0ull, mine);
-        if (v == 0) {  // claimed: this item represents the shape
+        if (v == 0) {  // claimed: this item represents a new shape
           slot = k;
-          const uint32_t idx = atomicAdd(&counters[0], 1u);
-          if (idx < kSlots) shape_list[idx] = k;
+          claimed = true;
+          shape_list[atomicAdd(&counters[kCNew], 1u)] = k;
+          atomicAdd(&counters[kCUsed], 1u);
           break;
         }
       }
-      if ((uint32_t)(v >> 32) == (uint32_t)(h >> 32) &&
-          kryo::same_shape(kryo::shape_of(items[(uint32_t)v - 1]), s)) {
+      if ((uint32_t)(v >> 32) == tag) {
         slot = k;
         break;
       }
     }
   }
+  if (slot != kNoSlot) {
+    const int32_t z = claimed ? kUnbuilt : slot_size[slot];
+    if (z == kUnbuilt) {  // built after this kernel: compared in kryo_tsize
+      item_slot[i] = slot | kDefer;
+      return;
+    }
+    if (!template_item(it, rec[slot], z, size, st)) slot = kNoSlot;
+  }
   item_slot[i] = slot;
+  if (slot == kNoSlot) direct_item(direct, counters, i);
+  sizes[i] = size;
+  status[i] = st;
 }
 
-// ---- 2. templates -----------------------------------------------------------------
-// One wave per shape (lane 0 traces; the level buffers live in LDS).
-__global__ void __launch_bounds__(64) kryo_build_kernel(ItemSrc items,
-                                                        const unsigned long long* __restrict__ table,
+// ---- 2. records and templates ----------------------------------------------------------
+// One wave per new shape: lane 0 records the representative's shape and traces
+// it (the level buffers in LDS) into the template's symbols; then the wave
+// writes the 16 shifted copies of the constant bytes and every block's
+// descriptor.
+__global__ void __launch_bounds__(64) kryo_build_kernel(ItemSrc items, const unsigned long long* __restrict__ table,
                                                         const uint32_t* __restrict__ shape_list,
-                                                        const uint32_t* __restrict__ counters,
+                                                        uint32_t* __restrict__ counters, kryo::ShapeRec* __restrict__ rec,
                                                         int32_t* __restrict__ slot_size, uint32_t* __restrict__ slot_map,
                                                         uint32_t* __restrict__ arena) {
   __shared__ uint32_t levels[kLevelSyms];
-  const uint32_t nshapes = counters[0] < kSlots ? counters[0] : kSlots;
-  for (uint32_t b = blockIdx.x; b < nshapes; b += gridDim.x) {
-    if (threadIdx.x != 0) continue;
+  __shared__ int32_t sh_size;
+  __shared__ uint32_t sh_idx;
+  const uint32_t nnew = counters[kCNew];
+  for (uint32_t b = blockIdx.x; b < nnew; b += gridDim.x) {
     const uint32_t slot = shape_list[b];
-    if (b >= kBuilders) {  // beyond the arena: the shape's items use the direct encoder
-      slot_size[slot] = kNoTemplate;
-      continue;
+    if (threadIdx.x == 0) {
+      const cordahip_kryo_item it = items[(uint32_t)table[slot] - 1];
+      kryo::ShapeRecord rv(rec[slot]);
+      kryo::shape_walk(it, rv);
+      int32_t size = kNoTemplate;
+      uint32_t idx = kBuilders;
+      if (rec[slot].ok) {
+        idx = atomicAdd(&counters[kCArena], 1u);
+        if (idx < kBuilders) size = (int32_t)kryo::trace_leaf(it, arena + idx * kTmplWords, kTmplSyms, levels);
+      }
+      slot_map[slot] = idx;
+      slot_size[slot] = size;  // the size, or -1 (an invalid shape) / kNoTemplate
+      sh_size = size;
+      sh_idx = idx;
     }
-    slot_map[slot] = b;
-    const uint64_t rep = (uint32_t)table[slot] - 1;
-    const cordahip_kryo_item it = items[rep];
-    const int64_t sz = kryo::trace_leaf(it, arena + (size_t)b * kTmplSyms, kTmplSyms, levels);
-    slot_size[slot] = (int32_t)sz;  // the size, or kInvalid / kNoTemplate
+    __syncthreads();
+    if (sh_size > 0) {
+      const uint32_t* syms = arena + sh_idx * kTmplWords;
+      uint8_t* base = reinterpret_cast<uint8_t*>(arena + sh_idx * kTmplWords);
+      const int32_t size = sh_size;
+      // the 16 shifted copies of the constant bytes, a dword at a time
+      for (uint32_t x = threadIdx.x; x < 16 * kTB / 4; x += blockDim.x) {
+        const uint32_t c = x / (kTB / 4), o = (x % (kTB / 4)) * 4;
+        uint32_t tw = 0;
+        for (uint32_t q = 0; q < 4; q++) {
+          const int32_t i = (int32_t)(o + q) - 16 - (int32_t)c;
+          if (i >= 0 && i < size && (syms[i] & kryo::kSymTypeMask) == kryo::kSymConst)
+            tw |= (syms[i] & 0xffu) << (8 * q);
+        }
+        reinterpret_cast<uint32_t*>(base + kOffTb)[x] = tw;
+      }
+      // the descriptors: block k of copy c covers leaf bytes 16 k + t - 16 - c
+      for (uint32_t x = threadIdx.x; x < 16 * kBlk; x += blockDim.x) {
+        const uint32_t c = x / kBlk, k = x % kBlk;
+        uint32_t pm = 0, kind = kDescConst;
+        int64_t delta = 0;
+        for (uint32_t t = 0; t < 16; t++) {
+          const int32_t i = (int32_t)(16 * k + t) - 16 - (int32_t)c;
+          if (i < 0 || i >= size) continue;
+          const uint32_t sym = syms[i];
+          if ((sym & kryo::kSymTypeMask) == kryo::kSymConst) continue;
+          const int64_t o = (int64_t)((sym >> 8) & (kryo::kMaxPayloadOff - 1)) - t;
+          const bool lin = (sym & kryo::kSymTypeMask) == kryo::kSymPayload && !(sym & kryo::kSymOr80);
+          if (!pm) {
+            kind = lin ? kDescLinear : kDescBytes;
+            delta = o;
+          } else if (!lin || o != delta) {
+            kind = kDescBytes;
+          }
+          pm |= 1u << t;
+        }
+        reinterpret_cast<uint64_t*>(base + kOffDesc)[x] =
+            (uint64_t)pm | ((uint64_t)kind << 16) | ((uint64_t)(uint32_t)(int32_t)delta << 32);
+      }
+    }
+    __syncthreads();
   }
 }
 
-// ---- 3. sizes ---------------------------------------------------------------------
+// ---- 3. sizes of the shapes built this call ------------------------------------------
 __global__ void __launch_bounds__(256) kryo_tsize_kernel(ItemSrc items, uint64_t n,
-                                                         const uint32_t* __restrict__ item_slot,
+                                                         uint32_t* __restrict__ item_slot,
                                                          const int32_t* __restrict__ slot_size,
+                                                         const kryo::ShapeRec* __restrict__ rec,
                                                          uint64_t* __restrict__ sizes, uint8_t* __restrict__ status,
                                                          uint32_t* __restrict__ direct, uint32_t* __restrict__ counters) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) sizes[n] = 0;  // the scan's last element: off[n] = the total
   if (i >= n) return;
-  const uint32_t slot = item_slot[i];
+  uint32_t slot = item_slot[i];
+  if (slot == kNoSlot || slot == kRawSlot || !(slot & kDefer)) return;  // resolved by kryo_shape
+  slot &= ~kDefer;
+  const cordahip_kryo_item it = items[i];
   uint64_t size = 0;
   uint8_t st = 0;
-  bool dir = slot == kNoSlot;
-  if (slot == kRawSlot) {
-    const cordahip_kryo_item it = items[i];
-    if (it.len && !it.data) st = 1;
-    else size = it.len;
-  } else if (!dir) {
-    const int32_t z = slot_size[slot];
-    if (z >= 0) size = (uint64_t)z;
-    else if (z == kInvalid) st = 1;
-    else dir = true;
+  if (!template_item(it, rec[slot], slot_size[slot], size, st)) {
+    slot = kNoSlot;
+    direct_item(direct, counters, i);
   }
-  if (dir) direct[atomicAdd(&counters[1], 1u)] = (uint32_t)i;  // sized by kryo_dsize
+  item_slot[i] = slot;
   sizes[i] = size;
   status[i] = st;
 }
@@ -178,7 +291,7 @@ __global__ void __launch_bounds__(256) kryo_dsize_kernel(ItemSrc items,
                                                          const uint32_t* __restrict__ direct,
                                                          const uint32_t* __restrict__ counters,
                                                          uint64_t* __restrict__ sizes, uint8_t* __restrict__ status) {
-  const uint32_t nd = counters[1];
+  const uint32_t nd = counters[kCDirect];
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t i = direct[j];
     kryo::Kout o(nullptr, 0, nullptr);  // counting mode
@@ -190,16 +303,16 @@ __global__ void __launch_bounds__(256) kryo_dsize_kernel(ItemSrc items,
 }
 
 // ---- 5. template writes -------------------------------------------------------------
+// A leaf's source: kind 0 template (its copy 0), 1 RAW, 2 direct (not written here).
 struct LeafSrc {
-  uint32_t kind;  // 0 template, 1 raw, 2 direct (not written here)
+  uint32_t kind;
   const uint32_t* syms;
   const uint8_t* data;
   int64_t value;
 };
 
-__device__ inline LeafSrc leaf_src(const ItemSrc& items, const uint32_t* item_slot,
-                                   const int32_t* slot_size, const uint32_t* slot_map, const uint32_t* arena,
-                                   uint64_t L) {
+__device__ inline LeafSrc leaf_src(const ItemSrc& items, const uint32_t* item_slot, const uint32_t* slot_map,
+                                   const uint32_t* arena, uint64_t L) {
   const cordahip_kryo_item it = items[L];
   const uint32_t slot = item_slot[L];
   LeafSrc s;
@@ -208,100 +321,220 @@ __device__ inline LeafSrc leaf_src(const ItemSrc& items, const uint32_t* item_sl
   s.syms = nullptr;
   if (slot == kRawSlot) {
     s.kind = 1;
-  } else if (slot == kNoSlot || slot_size[slot] < 0) {
+  } else if (slot == kNoSlot) {
     s.kind = 2;
   } else {
     s.kind = 0;
-    s.syms = arena + (size_t)slot_map[slot] * kTmplSyms;
+    s.syms = arena + (size_t)slot_map[slot] * kTmplWords;
   }
   return s;
 }
 
-__device__ inline uint8_t src_byte(const LeafSrc& s, uint64_t p) {
-  return s.kind == 1 ? s.data[p] : kryo::sym_byte(s.syms[p], s.data, s.value);
+__device__ inline uint8_t src_byte(uint32_t kind, const uint32_t* syms, const uint8_t* data, int64_t value,
+                                   uint64_t p) {
+  return kind == 1 ? data[p] : kryo::sym_byte(syms[p], data, value);
 }
 
 // Byte q of the output when it lies in a leaf after `from` (the end of a dword
 // whose first byte is in an earlier leaf): false when that leaf is not written
 // here (direct encoder, or beyond cap).
-__device__ inline bool spill_byte(const ItemSrc& items, uint64_t n, const uint64_t* off,
-                                  const uint32_t* item_slot, const int32_t* slot_size, const uint32_t* slot_map,
-                                  const uint32_t* arena, uint64_t cap, uint64_t from, uint64_t q, uint8_t& byte) {
+__device__ inline bool spill_byte(const ItemSrc& items, uint64_t n, const uint64_t* off, const uint32_t* item_slot,
+                                  const uint32_t* slot_map, const uint32_t* arena, uint64_t cap, uint64_t from,
+                                  uint64_t q, uint8_t& byte) {
   uint64_t L = from;
   while (L < n && off[L + 1] <= q) L++;
   if (L >= n || off[L + 1] > cap) return false;
-  const LeafSrc s = leaf_src(items, item_slot, slot_size, slot_map, arena, L);
+  const LeafSrc s = leaf_src(items, item_slot, slot_map, arena, L);
   if (s.kind == 2) return false;
-  byte = src_byte(s, q - off[L]);
+  byte = src_byte(s.kind, s.syms, s.data, s.value, q - off[L]);
   return true;
+}
+
+// A wave writes the output span of kLeavesPerWave consecutive leaves as 16-byte
+// output blocks, one per lane per pass (1 KB per store instruction). A block
+// that lies inside one template leaf reads that leaf's constant bytes from the
+// copy shifted to its alignment and the block's descriptor: constants only, or
+// every patched byte t = payload byte delta + t (one 16-byte window of the
+// item: at most two aligned 16-byte loads). Every other block -- a leaf
+// boundary, value bytes, a RAW or direct leaf's edge, the buffer's ends -- goes
+// on a per-wave queue in LDS and is written byte by byte afterwards, 16 lanes
+// per block, so the rare paths do not diverge the common one. (r05's first
+// writer walked symbols per byte: ~4,500 VALU instructions per wave of 16
+// leaves, the TA busy for the whole kernel; profiles/r05_pmc_kryo_encoder.json.)
+constexpr uint32_t kQueue = 256;
+
+struct LeafMeta {
+  uint32_t kind;  // 0 template, 1 RAW, 2 not written here (direct encoder, empty, beyond cap)
+  uint32_t sh;    // (output address of the leaf) & 15: the template copy aligned to the blocks
+  uint32_t a, b;  // the leaf's bytes, relative to the span's start
+  const uint32_t* tmpl;  // the template (its syms; tb / desc at fixed offsets)
+  const uint8_t* data;
+  int64_t value;
+};
+
+// the leaf holding span byte x (0 <= x < bound[nl], nl <= 16): the last leaf starting at or
+// before it (empty leaves start where the next one does; the search passes over them)
+__device__ inline uint32_t leaf_at(const uint32_t* bound, uint32_t nl, uint32_t x) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t step = 8; step; step >>= 1) {
+    const uint32_t c = lo + step;
+    if (c < nl && bound[c] <= x) lo = c;
+  }
+  return lo;
+}
+
+__device__ inline uint32_t byte_mask32(uint32_t m4) {  // 4 mask bits -> 4 byte masks
+  return ((m4 * 0x00204081u) & 0x01010101u) * 0xffu;
+}
+
+// bytes q[t0 .. t1] (t0 <= t1 < 16) as a 16-byte window w[t] = q[t]: at most two aligned
+// 16-byte loads, each holding one of the wanted bytes (so both are mapped)
+__device__ inline void load_window(const uint8_t* q, uint32_t t0, uint32_t t1, uint32_t* w) {
+  const uintptr_t qa = (uintptr_t)q, ca = qa & ~(uintptr_t)15;
+  const uint32_t s = (uint32_t)(qa - ca);
+  uint4 u0 = make_uint4(0, 0, 0, 0), u1 = make_uint4(0, 0, 0, 0);
+  if (s + t0 < 16) u0 = *reinterpret_cast<const uint4*>(ca);
+  if (s + t1 >= 16) u1 = *reinterpret_cast<const uint4*>(ca + 16);
+  const uint32_t d[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+  const uint32_t dw = s >> 2, sb = s & 3;
+  uint32_t e[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++)
+    e[i] = dw == 0 ? d[i] : dw == 1 ? d[i + 1] : dw == 2 ? d[i + 2] : (i + 3 < 8 ? d[i + 3] : 0);
+#pragma unroll
+  for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
 }
 
 __global__ void __launch_bounds__(256) kryo_twrite_kernel(ItemSrc items, uint64_t n,
                                                           const uint64_t* __restrict__ off,
                                                           const uint32_t* __restrict__ item_slot,
-                                                          const int32_t* __restrict__ slot_size,
                                                           const uint32_t* __restrict__ slot_map,
                                                           const uint32_t* __restrict__ arena, uint8_t* __restrict__ out,
                                                           uint64_t cap, uint8_t* __restrict__ status) {
-  const uint32_t lane = threadIdx.x & 63;
-  // wave-uniform (readfirstlane: the leaf loop and its loads stay scalar)
-  const uint64_t wave = (uint64_t)__builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  __shared__ LeafMeta meta_s[4][kLeavesPerWave];
+  __shared__ uint32_t bound_s[4][kLeavesPerWave + 1];
+  __shared__ uint32_t queue_s[4][kQueue];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  LeafMeta* meta = meta_s[wv];
+  uint32_t* bound = bound_s[wv];
+  uint32_t* queue = queue_s[wv];
+  const uint64_t wave = (uint64_t)blockIdx.x * 4 + wv;
   const uint64_t L0 = wave * kLeavesPerWave;
   if (L0 >= n) return;
-  const uint64_t L1 = L0 + kLeavesPerWave < n ? L0 + kLeavesPerWave : n;
+  const uint32_t nl = (uint32_t)(L0 + kLeavesPerWave < n ? kLeavesPerWave : n - L0);
   const uint64_t base = (uint64_t)(uintptr_t)out;
-  for (uint64_t L = L0; L < L1; L++) {
-    const uint64_t a = off[L], b = off[L + 1];
-    if (b == a) continue;  // invalid item (or an empty RAW leaf)
-    const LeafSrc s = leaf_src(items, item_slot, slot_size, slot_map, arena, L);
-    if (b > cap) {  // not written (nor are the leaves after it)
-      if (lane == 0 && s.kind != 2) status[L] = 2;
-      continue;
-    }
-    // the dwords whose first output byte is in this leaf (the leaf at output
-    // position 0 also takes the dword that starts before the buffer)
-    const uint64_t lo = a == 0 ? (base & ~3ull) : ((base + a + 3) & ~3ull);
-    const uint64_t hi = (base + b + 3) & ~3ull;
-    // a direct leaf's bytes come later (kryo_dwrite); only its last dword may
-    // carry bytes of the next leaves
-    const uint64_t start = s.kind == 2 ? (hi - 4 > lo ? hi - 4 : lo) : lo;
-    for (uint64_t A = start + 4ull * lane; A < hi; A += 256) {
-      uint32_t w = 0, valid = 0;
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) {
-        if (A + j < base) continue;
-        const uint64_t q = A + j - base;
-        uint8_t byte = 0;
-        if (q < b) {
-          if (s.kind == 2) continue;
-          byte = src_byte(s, q - a);
-        } else if (!spill_byte(items, n, off, item_slot, slot_size, slot_map, arena, cap, L + 1, q, byte)) {
-          continue;
-        }
-        w |= (uint32_t)byte << (8 * j);
-        valid |= 1u << j;
-      }
-      if (valid == 15) {
-        *reinterpret_cast<uint32_t*>(A) = w;
-      } else {
-        for (uint32_t j = 0; j < 4; j++)
-          if (valid >> j & 1) reinterpret_cast<uint8_t*>(A)[j] = (uint8_t)(w >> (8 * j));
-      }
-    }
+  const uint64_t P0 = off[L0], P1 = off[L0 + nl];  // the span (< 2^32 bytes: kLeavesPerWave leaves)
+  if (lane <= nl) bound[lane] = (uint32_t)(off[L0 + lane] - P0);
+  if (lane < nl) {
+    const uint64_t a = off[L0 + lane], b = off[L0 + lane + 1];
+    const LeafSrc s = leaf_src(items, item_slot, slot_map, arena, L0 + lane);
+    LeafMeta m;
+    m.kind = (b == a || b > cap) ? 2 : s.kind;
+    m.sh = (uint32_t)((base + a) & 15);
+    m.a = (uint32_t)(a - P0);
+    m.b = (uint32_t)(b - P0);
+    m.tmpl = s.syms;
+    m.data = s.data;
+    m.value = s.value;
+    meta[lane] = m;
+    if (b > cap && b > a && s.kind != 2) status[L0 + lane] = 2;  // not written (nor the leaves after it)
   }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the wave's LDS stores before its loads
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (P1 == P0) return;
+  // the 16-byte blocks whose first output byte is in the span (the span at
+  // output position 0 also takes the block that starts before the buffer)
+  const uint64_t lo = P0 == 0 ? (base & ~15ull) : ((base + P0 + 15) & ~15ull);
+  const uint64_t hi = (base + P1 + 15) & ~15ull;
+  const uint32_t nblk = (uint32_t)((hi - lo) / 16);
+  const int64_t span = (int64_t)(P1 - P0);
+
+  // the queued blocks, byte by byte: 16 lanes per block
+  auto flush = [&](uint32_t nq) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t j = lane; j < nq * 16; j += 64) {
+      const uint64_t A = lo + 16ull * queue[j >> 4];
+      const uint32_t t = j & 15;
+      if (A + t < base) continue;  // before the buffer
+      const int64_t xt = (int64_t)(A + t - base) - (int64_t)P0;
+      uint8_t byte = 0;
+      if (xt >= span) {  // past the span: the next wave's leaves
+        if (!spill_byte(items, n, off, item_slot, slot_map, arena, cap, L0 + nl, A + t - base, byte)) continue;
+      } else {
+        const LeafMeta& m = meta[leaf_at(bound, nl, (uint32_t)xt)];
+        if (m.kind == 2) continue;
+        const uint32_t p = (uint32_t)xt - m.a;
+        byte = m.kind == 1 ? m.data[p] : kryo::sym_byte(m.tmpl[p], m.data, m.value);
+      }
+      reinterpret_cast<uint8_t*>(A)[t] = byte;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the queue is refilled after this
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  uint32_t nq = 0;  // wave-uniform
+  for (uint32_t b0 = 0; b0 < nblk; b0 += 64) {
+    if (nq + 64 > kQueue) {
+      flush(nq);
+      nq = 0;
+    }
+    const uint32_t bi = b0 + lane;
+    bool fast = false;
+    if (bi < nblk) {
+      const uint64_t A = lo + 16ull * bi;
+      const int64_t x = (int64_t)(A - base) - (int64_t)P0;  // span position of the block's byte 0
+      const LeafMeta& m = meta[leaf_at(bound, nl, x < 0 ? 0u : (uint32_t)x)];
+      if (A >= base && x >= (int64_t)m.a && x + 16 <= (int64_t)m.b && m.kind != 2) {
+        const int64_t pb = x - (int64_t)m.a;  // leaf position of the block's byte 0
+        uint32_t v[4];
+        if (m.kind == 1) {  // RAW: the item's bytes
+          load_window(m.data + pb, 0, 15, v);
+          fast = true;
+        } else {
+          const uint8_t* tp = reinterpret_cast<const uint8_t*>(m.tmpl);
+          const uint32_t idx = (uint32_t)(16 + (int64_t)m.sh + pb);  // a multiple of 16
+          const uint64_t desc = reinterpret_cast<const uint64_t*>(tp + kOffDesc)[m.sh * kBlk + idx / 16];
+          const uint32_t pm = (uint32_t)desc & 0xffff, kind = (uint32_t)(desc >> 16) & 3;
+          if (kind != kDescBytes) {
+            const uint4 tv = *reinterpret_cast<const uint4*>(tp + kOffTb + (size_t)m.sh * kTB + idx);
+            v[0] = tv.x, v[1] = tv.y, v[2] = tv.z, v[3] = tv.w;
+            if (pm) {
+              uint32_t w[4];
+              load_window(m.data + (int32_t)(desc >> 32), __builtin_ctz(pm), 31 - __builtin_clz(pm), w);
+#pragma unroll
+              for (int i = 0; i < 4; i++) {
+                const uint32_t mk = byte_mask32((pm >> (4 * i)) & 15);
+                v[i] = (v[i] & ~mk) | (w[i] & mk);
+              }
+            }
+            fast = true;
+          }
+        }
+        if (fast) *reinterpret_cast<uint4*>(A) = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    // the others to the queue (in block order; positions by ballot prefix)
+    const bool need = bi < nblk && !fast;
+    const uint64_t ball = __ballot(need);
+    if (need) queue[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0))] = bi;
+    nq += (uint32_t)__popcll(ball);
+  }
+  flush(nq);
 }
 
 // ---- 6. direct writes ---------------------------------------------------------------
-__global__ void __launch_bounds__(256) kryo_dwrite_kernel(ItemSrc items,
-                                                          const uint32_t* __restrict__ direct,
+__global__ void __launch_bounds__(256) kryo_dwrite_kernel(ItemSrc items, const uint32_t* __restrict__ direct,
                                                           const uint32_t* __restrict__ counters,
                                                           const uint64_t* __restrict__ off, uint8_t* __restrict__ out,
                                                           uint64_t cap, uint8_t* __restrict__ status,
                                                           uint8_t* __restrict__ ws) {
-  const uint32_t nd = counters[1];
+  const uint32_t nd = counters[kCDirect];
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // levels 1..7 of this thread's OutputChunked buffers (level 0 is the leaf)
-  uint8_t* levels = ws + t * (uint64_t)kLevelSyms;
+  uint8_t* levels = ws + t * (uint64_t)kLevelSyms;  // levels 1..7 of this thread's OutputChunked buffers
   for (uint64_t j = t; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t i = direct[j];
     if (status[i] != 0) continue;
@@ -318,50 +551,62 @@ __global__ void __launch_bounds__(256) kryo_dwrite_kernel(ItemSrc items,
 
 }  // namespace
 
-// Scratch of one encode call (cordahip.cpp sizes it with kryo_scratch_bytes).
-struct KryoScratch {
-  unsigned long long* table;  // [kSlots]
-  uint32_t* shape_list;       // [kSlots]
+// The encoder's persistent per-device state (cordahip.cpp allocates
+// kryo_fixed_scratch_bytes() once, zeroed; kryo_clear() empties it).
+struct KryoState {
+  unsigned long long* table;  // [kSlots] tag | representative + 1
+  kryo::ShapeRec* rec;        // [kSlots]
   int32_t* slot_size;         // [kSlots]
-  uint32_t* slot_map;         // [kSlots] builder index of the slot's template
-  uint32_t* counters;         // [0] shapes, [1] direct items
-  uint32_t* item_slot;        // [n]
-  uint32_t* direct;           // [n]
-  uint32_t* arena;            // [kBuilders * kTmplSyms]
-  uint8_t* dws;               // direct writers' level buffers
+  uint32_t* slot_map;         // [kSlots] the slot's template in the arena
+  uint32_t* shape_list;       // [kSlots] slots claimed this call
+  uint32_t* counters;         // [16] kCNew, kCDirect, kCArena, kCUsed
+  uint32_t* arena;            // [kBuilders * kTmplWords]
+  explicit KryoState(uint8_t* p) {
+    table = reinterpret_cast<unsigned long long*>(p);
+    rec = reinterpret_cast<kryo::ShapeRec*>(table + kSlots);
+    slot_size = reinterpret_cast<int32_t*>(rec + kSlots);
+    slot_map = reinterpret_cast<uint32_t*>(slot_size + kSlots);
+    shape_list = slot_map + kSlots;
+    counters = shape_list + kSlots;
+    arena = counters + 16;
+  }
 };
 
 size_t kryo_fixed_scratch_bytes() {
-  return (size_t)kSlots * (8 + 4 + 4 + 4) + 64 + (size_t)kBuilders * kTmplSyms * 4;
+  return (size_t)kSlots * (8 + sizeof(kryo::ShapeRec) + 4 + 4 + 4) + 64 + (size_t)kBuilders * kTmplBytes;
 }
 size_t kryo_direct_ws_bytes(uint64_t writers) { return (size_t)writers * kLevelSyms; }
+// the table, records and templates emptied (the arena need not be)
+hipError_t kryo_clear(uint8_t* fixed, hipStream_t s) {
+  const KryoState k(fixed);
+  hipError_t e = hipMemsetAsync(k.table, 0, (size_t)kSlots * 8, s);
+  static_assert(kUnbuilt == -3, "kUnbuilt as a byte pattern");
+  e = e ? e : hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(k.slot_size), (int)kUnbuilt, kSlots, s);
+  return e ? e : hipMemsetAsync(k.counters, 0, 64, s);
+}
+// counters[kCArena], counters[kCUsed] (device) -> usage[0..1] (host-mapped), after a call
+const uint32_t* kryo_usage_src(uint8_t* fixed) { return KryoState(fixed).counters + kCArena; }
+uint32_t kryo_clear_threshold_slots() { return kSlots / 2; }
+uint32_t kryo_clear_threshold_templates() { return kBuilders - 64; }
 
 hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
-                              uint64_t n, uint32_t group, uint8_t* fixed,
-                              uint32_t* item_slot, uint32_t* direct, uint64_t* sizes, uint64_t* off, uint8_t* out,
-                              uint64_t cap, uint8_t* status, uint8_t* dws, uint64_t dwriters, void* scan_temp,
-                              size_t scan_bytes, hipStream_t s) {
+                              uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
+                              uint64_t* sizes, uint64_t* off, uint8_t* out, uint64_t cap, uint8_t* status,
+                              uint8_t* dws, uint64_t dwriters, void* scan_temp, size_t scan_bytes, hipStream_t s) {
   const ItemSrc items{d_items, data_base, data_len};
-  KryoScratch k;
-  k.table = reinterpret_cast<unsigned long long*>(fixed);
-  k.shape_list = reinterpret_cast<uint32_t*>(k.table + kSlots);
-  k.slot_size = reinterpret_cast<int32_t*>(k.shape_list + kSlots);
-  k.slot_map = reinterpret_cast<uint32_t*>(k.slot_size + kSlots);
-  k.counters = k.slot_map + kSlots;
-  k.arena = k.counters + 16;
-  hipError_t e = hipMemsetAsync(k.table, 0, (size_t)kSlots * 8, s);
-  e = e ? e : hipMemsetAsync(k.counters, 0, 64, s);
+  const KryoState k(fixed);
+  hipError_t e = hipMemsetAsync(k.counters, 0, 8, s);  // kCNew, kCDirect
   if (e || n == 0) {
     e = e ? e : hipMemsetAsync(off, 0, 8, s);
     return e;
   }
   const uint32_t blocks = (uint32_t)((n + 255) / 256);
-  hipLaunchKernelGGL(kryo_shape_kernel, dim3(blocks), dim3(256), 0, s, items, n, group, k.table, item_slot,
-                     k.shape_list, k.counters);
-  hipLaunchKernelGGL(kryo_build_kernel, dim3(kBuilders), dim3(64), 0, s, items, k.table, k.shape_list, k.counters,
+  hipLaunchKernelGGL(kryo_shape_kernel, dim3(blocks), dim3(256), 0, s, items, n, group, k.table, k.slot_size, k.rec,
+                     item_slot, k.shape_list, sizes, status, direct, k.counters);
+  hipLaunchKernelGGL(kryo_build_kernel, dim3(256), dim3(64), 0, s, items, k.table, k.shape_list, k.counters, k.rec,
                      k.slot_size, k.slot_map, k.arena);
-  hipLaunchKernelGGL(kryo_tsize_kernel, dim3((uint32_t)((n + 1 + 255) / 256)), dim3(256), 0, s, items, n, item_slot,
-                     k.slot_size, sizes, status, direct, k.counters);
+  hipLaunchKernelGGL(kryo_tsize_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, items, n, item_slot,
+                     k.slot_size, k.rec, sizes, status, direct, k.counters);
   hipLaunchKernelGGL(kryo_dsize_kernel, dim3(1024), dim3(256), 0, s, items, direct, k.counters, sizes, status);
   e = hipGetLastError();
   size_t tb = scan_bytes;
@@ -369,7 +614,7 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* 
   if (e || !out) return e;
   const uint64_t waves = (n + kLeavesPerWave - 1) / kLeavesPerWave;
   hipLaunchKernelGGL(kryo_twrite_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, items, n, off, item_slot,
-                     k.slot_size, k.slot_map, k.arena, out, cap, status);
+                     k.slot_map, k.arena, out, cap, status);
   hipLaunchKernelGGL(kryo_dwrite_kernel, dim3((uint32_t)std::max<uint64_t>(1, dwriters / 256)), dim3(256), 0, s, items,
                      direct, k.counters, off, out, cap, status, dws);
   return hipGetLastError();

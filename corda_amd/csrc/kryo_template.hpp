@@ -19,8 +19,9 @@
 // from `value` are content. Content that the encoder inspects is therefore put
 // in the shape whole (the command class name, the currency code, STRING and
 // KOTLIN_OBJECT text) or in part (the DER header of an X.500 name, which the
-// party decode validates). same_shape() compares structure words and those
-// spans byte for byte; the hash only picks the table slot.
+// party decode validates). shape_matches() compares an item's structure words
+// and those spans byte for byte with a recorded shape; the hash only picks the
+// table slot.
 // tests/test_kryo_template.py checks, on the host, every item of randomised
 // batches rebuilt from its shape representative's symbols against the direct
 // encoder.
@@ -30,27 +31,14 @@
 namespace cordahip {
 namespace kryo {
 
-struct Shape {
-  static constexpr uint32_t kWords = 32, kSpans = 4;
-  uint32_t w[kWords];
-  uint32_t nw = 0;
-  const uint8_t* sp[kSpans];
-  uint32_t sl[kSpans];
-  uint32_t ns = 0;
-  bool ok = true;  // false: no template (the item goes through the direct encoder)
-  KRYO_HD void word(uint32_t x) {
-    if (nw < kWords) w[nw++] = x;
-    else ok = false;
-  }
-  KRYO_HD void span(const uint8_t* p, uint32_t n) {
-    if (ns < kSpans && (p || !n)) {
-      sp[ns] = p;
-      sl[ns++] = n;
-    } else {
-      ok = false;
-    }
-  }
-};
+// ---- shapes ---------------------------------------------------------------------
+// shape_walk visits an item's shape -- its structure words and the content
+// spans the encoder inspects -- in a fixed order through a visitor V
+// (V::word(x), V::span(p, n)), so hashing, recording and comparing shapes
+// stream over the payload without arrays. Returns false when the item has no
+// shape (RAW leaves are copied directly; unknown kinds, malformed payloads and
+// outsized content go to the direct encoder, which also decides their
+// validity).
 
 // bytes of Output.writeVarLong(zigzag(v)) (1..9): part of the shape of a VALUE_ZZ kind
 KRYO_HD inline uint32_t varlong_zz_len(int64_t x) {
@@ -65,20 +53,18 @@ KRYO_HD inline uint32_t varlong_zz_len(int64_t x) {
 
 // a party of a CASH_STATE payload: its structure, and the DER header of its
 // name (Reader::party validates the name's TLV)
-KRYO_HD inline void shape_party(Shape& s, const PartyRef& p) {
-  s.word(p.key_class);
-  s.word(p.key_len);
-  s.word(p.name_len);
-  s.span(p.name, p.name_len < 6 ? p.name_len : 6);
+template <class V>
+KRYO_HD inline void shape_party(V& v, const PartyRef& p) {
+  v.word(p.key_class);
+  v.word(p.key_len);
+  v.word(p.name_len);
+  v.span(p.name, p.name_len < 6 ? p.name_len : 6);
 }
 
-// The shape of an item, or ok = false when it has none (RAW leaves are copied
-// directly; unknown kinds, malformed payloads and outsized content go to the
-// direct encoder, which also decides their validity).
-KRYO_HD inline Shape shape_of(const cordahip_kryo_item& it) {
-  Shape s;
-  s.word(it.kind);
-  s.word(it.class_id);
+template <class V>
+KRYO_HD inline bool shape_walk(const cordahip_kryo_item& it, V& v) {
+  v.word(it.kind);
+  v.word(it.class_id);
   switch (it.kind) {
     case CORDAHIP_KRYO_CHAR:
     case CORDAHIP_KRYO_SHORT:
@@ -86,57 +72,46 @@ KRYO_HD inline Shape shape_of(const cordahip_kryo_item& it) {
     case CORDAHIP_KRYO_LONG:
     case CORDAHIP_KRYO_BYTE:
     case CORDAHIP_KRYO_FLOAT:
-    case CORDAHIP_KRYO_DOUBLE: break;  // value bytes only
-    case CORDAHIP_KRYO_BOOLEAN: s.word(it.value != 0); break;
+    case CORDAHIP_KRYO_DOUBLE: return true;  // value bytes only
+    case CORDAHIP_KRYO_BOOLEAN: v.word(it.value != 0); return true;
     case CORDAHIP_KRYO_STRING:
     case CORDAHIP_KRYO_KOTLIN_OBJECT:  // the text is transcoded (UTF-16 -> Kryo string): all of it is shape
-      if (it.len > 512 || (it.len && !it.data)) {
-        s.ok = false;
-        break;
-      }
-      s.word((uint32_t)it.len);
-      s.span(it.data, (uint32_t)(2 * it.len));
-      break;
+      if (it.len > 512 || (it.len && !it.data)) return false;
+      v.word((uint32_t)it.len);
+      v.span(it.data, (uint32_t)(2 * it.len));
+      return true;
     case CORDAHIP_KRYO_ED25519_KEY:
     case CORDAHIP_KRYO_PUBLIC_KEY:
-      if (!it.data || it.len >= kMaxPayloadOff) s.ok = false;
-      s.word((uint32_t)it.len);
-      break;
+      if (!it.data || it.len >= kMaxPayloadOff) return false;
+      v.word((uint32_t)it.len);
+      return true;
     case CORDAHIP_KRYO_PARTY:
-      if (!it.data || it.len >= kMaxPayloadOff) {
-        s.ok = false;
-        break;
-      }
-      s.word((uint32_t)it.value);  // the key class (its varint is written)
-      s.word((uint32_t)it.len);
-      s.span(it.data, it.len < 6 ? (uint32_t)it.len : 6);  // der_tlv_len splits name | key on these
-      break;
+      if (!it.data || it.len >= kMaxPayloadOff) return false;
+      v.word((uint32_t)it.value);  // the key class (its varint is written)
+      v.word((uint32_t)it.len);
+      v.span(it.data, it.len < 6 ? (uint32_t)it.len : 6);  // der_tlv_len splits name | key on these
+      return true;
     case CORDAHIP_KRYO_ISSUE_COMMAND: {
-      if (!it.data || it.len < 2 || it.len >= kMaxPayloadOff) {
-        s.ok = false;
-        break;
-      }
+      if (!it.data || it.len < 2 || it.len >= kMaxPayloadOff) return false;
       Reader r(it.data, it.data + it.len);
       const uint32_t nlen = r.u8();
       const uint8_t* nm = r.span(nlen);
       const uint32_t nkeys = r.u8();
-      s.word(varlong_zz_len(it.value));
-      s.word(nlen);
-      s.span(nm, nlen);  // the class name: written, compared, and cut for the field name
-      s.word(nkeys);
+      if (!r.ok || nkeys > 12) return false;
+      v.word(varlong_zz_len(it.value));
+      v.word(nlen);
+      v.span(nm, nlen);  // the class name: written, compared, and cut for the field name
+      v.word(nkeys);
       for (uint32_t i = 0; i < nkeys && r.ok; i++) {
-        s.word(r.u16());
-        s.word(r.u16());
-        r.span(s.w[s.nw - 1]);
+        v.word(r.u16());
+        const uint32_t kl = r.u16();
+        v.word(kl);
+        r.span(kl);
       }
-      if (!r.ok || r.p != r.end) s.ok = false;
-      break;
+      return r.ok && r.p == r.end;
     }
     case CORDAHIP_KRYO_CASH_STATE: {
-      if (!it.data || it.len >= kMaxPayloadOff) {
-        s.ok = false;
-        break;
-      }
+      if (!it.data || it.len >= kMaxPayloadOff) return false;
       Reader r(it.data, it.data + it.len);
       const PartyRef issuer = r.party();
       const uint32_t ref_len = r.u8();
@@ -149,53 +124,96 @@ KRYO_HD inline Shape shape_of(const cordahip_kryo_item& it) {
       r.span(32);
       const uint32_t flags = r.u8();
       const uint8_t* enc = r.span(4);
-      if (!r.ok || r.p != r.end) {
-        s.ok = false;
-        break;
-      }
-      s.word(varlong_zz_len(it.value));
-      shape_party(s, issuer);
-      s.word(ref_len);
-      shape_party(s, owner);
-      shape_party(s, notary);
-      s.word(code_len);
-      s.span(code, code_len);  // ASCII-checked, written as a string
-      s.word(scale);
-      s.word(flags);
-      s.word((flags & 1u) ? (uint32_t)(enc[0] | (enc[1] << 8) | (enc[2] << 16) | ((uint32_t)enc[3] << 24)) : 0);
-      s.word(same_key(owner, issuer));  // exitKeys has one element or two
-      break;
+      if (!r.ok || r.p != r.end) return false;
+      v.word(varlong_zz_len(it.value));
+      shape_party(v, issuer);
+      v.word(ref_len);
+      shape_party(v, owner);
+      shape_party(v, notary);
+      v.word(code_len);
+      v.span(code, code_len);  // ASCII-checked, written as a string
+      v.word(scale);
+      v.word(flags);
+      v.word((flags & 1u) ? (uint32_t)(enc[0] | (enc[1] << 8) | (enc[2] << 16) | ((uint32_t)enc[3] << 24)) : 0);
+      v.word(same_key(owner, issuer));  // exitKeys has one element or two
+      return true;
     }
-    default: s.ok = false;  // RAW (copied directly) and unknown kinds
+    default: return false;  // RAW (copied directly) and unknown kinds
   }
-  return s;
 }
 
-KRYO_HD inline uint64_t shape_hash(const Shape& s) {
-  uint64_t h = 1469598103934665603ull;  // FNV-1a over the words and the span bytes
-  auto mix = [&](uint32_t x) {
+// FNV-1a over the words and the span bytes
+struct ShapeHash {
+  uint64_t h = 1469598103934665603ull;
+  KRYO_HD void mix(uint32_t x) {
     h ^= x;
     h *= 1099511628211ull;
-  };
-  for (uint32_t i = 0; i < s.nw; i++) mix(s.w[i]);
-  for (uint32_t j = 0; j < s.ns; j++) {
-    mix(0x100 | s.sl[j]);
-    for (uint32_t i = 0; i < s.sl[j]; i++) mix(s.sp[j][i]);
   }
-  return h ^ (h >> 29);
-}
+  KRYO_HD void word(uint32_t x) { mix(x); }
+  KRYO_HD void span(const uint8_t* p, uint32_t n) {
+    mix(0x100 | n);
+    for (uint32_t i = 0; i < n; i++) mix(p[i]);
+  }
+  KRYO_HD uint64_t value() const { return h ^ (h >> 29); }
+};
 
-KRYO_HD inline bool same_shape(const Shape& a, const Shape& b) {
-  if (!a.ok || !b.ok || a.nw != b.nw || a.ns != b.ns) return false;
-  for (uint32_t i = 0; i < a.nw; i++)
-    if (a.w[i] != b.w[i]) return false;
-  for (uint32_t j = 0; j < a.ns; j++) {
-    if (a.sl[j] != b.sl[j]) return false;
-    if (a.sp[j] == b.sp[j]) continue;
-    for (uint32_t i = 0; i < a.sl[j]; i++)
-      if (a.sp[j][i] != b.sp[j][i]) return false;
+// A shape as data: the GPU keeps one per table slot (the words and the span
+// BYTES, so the record outlives the call whose item it came from), and items
+// are compared with it as they are walked (ShapeCmp).
+struct ShapeRec {
+  static constexpr uint32_t kWords = 48, kSpans = 8, kBytes = 192;
+  uint32_t nw, ns, nb, ok;
+  uint32_t w[kWords];
+  uint32_t sl[kSpans];
+  uint8_t bytes[kBytes];
+};
+
+struct ShapeRecord {  // visitor: fills a record (ok = 0 when it does not fit)
+  ShapeRec& r;
+  KRYO_HD explicit ShapeRecord(ShapeRec& x) : r(x) { r.nw = r.ns = r.nb = 0, r.ok = 1; }
+  KRYO_HD void word(uint32_t x) {
+    if (r.nw < ShapeRec::kWords) r.w[r.nw++] = x;
+    else r.ok = 0;
   }
-  return true;
+  KRYO_HD void span(const uint8_t* p, uint32_t n) {
+    if (r.ns >= ShapeRec::kSpans || r.nb + n > ShapeRec::kBytes) {
+      r.ok = 0;
+      return;
+    }
+    r.sl[r.ns++] = n;
+    for (uint32_t i = 0; i < n; i++) r.bytes[r.nb++] = p[i];
+  }
+};
+
+struct ShapeCmp {  // visitor: eq stays true while the walk matches the record
+  const ShapeRec& r;
+  uint32_t iw = 0, is = 0, ib = 0;
+  bool eq = true;
+  KRYO_HD explicit ShapeCmp(const ShapeRec& x) : r(x) {}
+  KRYO_HD void word(uint32_t x) {
+    eq = eq && iw < r.nw && r.w[iw] == x;
+    iw++;
+  }
+  KRYO_HD void span(const uint8_t* p, uint32_t n) {
+    eq = eq && is < r.ns && r.sl[is] == n && ib + n <= r.nb;
+    for (uint32_t i = 0; eq && i < n; i++) eq = r.bytes[ib + i] == p[i];
+    is++;
+    ib += n;
+  }
+  KRYO_HD bool done() const { return eq && iw == r.nw && is == r.ns && ib == r.nb; }
+};
+
+// hash of an item's shape; false: no shape
+KRYO_HD inline bool shape_hash_of(const cordahip_kryo_item& it, uint64_t& h) {
+  ShapeHash v;
+  const bool ok = shape_walk(it, v);
+  h = v.value();
+  return ok;
+}
+// the item has exactly the recorded shape
+KRYO_HD inline bool shape_matches(const cordahip_kryo_item& it, const ShapeRec& rec) {
+  ShapeCmp v(rec);
+  return rec.ok && shape_walk(it, v) && v.done();
 }
 
 // One leaf byte of an item from its shape's symbol.

@@ -40,9 +40,13 @@ hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, u
                               hipStream_t s);
 hipError_t launch_store_to_host(const void* src, void* dst, uint64_t n, hipStream_t s);
 // kryo_device.hip: the GPU Kryo leaf encoder (shapes, templates, sizes, scan, writes)
-size_t kryo_fixed_scratch_bytes();                     // shape table + templates (per call, reused)
+size_t kryo_fixed_scratch_bytes();                     // shape table, records, templates (persistent per device)
 size_t kryo_direct_ws_bytes(uint64_t writers);         // the direct encoder's level buffers
 hipError_t kryo_scan_bytes(size_t& bytes, uint64_t n1, hipStream_t s);
+hipError_t kryo_clear(uint8_t* fixed, hipStream_t s);  // empty the shape table (and the template arena)
+const uint32_t* kryo_usage_src(uint8_t* fixed);        // device: [templates in the arena, table slots in use]
+uint32_t kryo_clear_threshold_slots();
+uint32_t kryo_clear_threshold_templates();
 // data_base != nullptr: items' `data` are offsets into data_len bytes at data_base
 hipError_t launch_kryo_encode(const cordahip_kryo_item* items, const uint8_t* data_base, uint64_t data_len,
                               uint64_t n, uint32_t group, uint8_t* fixed,
@@ -231,6 +235,12 @@ struct Device {
   // buffers; kryo_mu orders the enqueues, kryo_ev fences reuse
   std::mutex kryo_mu;
   DevBuf kryo_sizes, kryo_temp, kryo_ws, kryo_fixed, kryo_items;
+  // the fixed part is persistent (shape table, records, templates): zeroed when
+  // allocated, cleared when a call reports it over half full (kryo_usage: a
+  // host-mapped copy of its usage counters, stored after each call)
+  bool kryo_fresh = false;
+  uint32_t* kryo_usage = nullptr;
+  uint32_t* kryo_usage_dev = nullptr;
   hipEvent_t kryo_ev = nullptr;
 };
 

@@ -149,3 +149,62 @@ def test_edge_batches(engine):
         assert int(status.sum()) == 0
         assert _leaves(out, off, len(items)) == host
     torch.cuda.synchronize(dev)
+
+
+def test_template_cache_across_calls(engine):
+    """The shape table, records and templates persist across calls on a device: a second batch of
+    the same shapes with different content is written from the cached templates; a batch of more
+    distinct shapes than the table keeps (40,000 strings) overflows to the direct encoder and makes
+    the next call clear the table; every leaf still equals the host encoder's."""
+    rng = np.random.default_rng(77)
+    ntx = 2000
+    for seed in (1, 2):
+        r = np.random.default_rng(seed)
+        blob, items, _ = cash_issue_items(r.integers(0, 256, (ntx, 32), dtype=np.uint8),
+                                          r.integers(0, 256, (ntx, 32), dtype=np.uint8), r.integers(0, 256, 32, dtype=np.uint8).tobytes(),
+                                          r.integers(1, 10**9, ntx), r.integers(-2**63, 2**63 - 1, ntx))
+        out, off, status = engine.kryo_encode_packed_device(blob, items.reshape(-1), np.ones(items.size, bool), group=5)
+        host_it = items.reshape(-1).copy()
+        host_it["data"] += np.uint64(blob.ctypes.data)
+        hb, ho = _lib.kryo_encode_array(host_it)
+        assert int(status.sum()) == 0
+        assert np.array_equal(off.cpu().numpy().astype(np.uint64), ho) and np.array_equal(out.cpu().numpy(), hb)
+    many = [("String", "s%06d" % int(x), 0) for x in rng.permutation(40000)] + [("int", 7, 0)] * 10
+    for items in (many, many[:5000]):
+        host = _lib.kryo_encode(items)
+        blob, arr, has = _lib.kryo_pack(items)
+        out, off, status = engine.kryo_encode_packed_device(blob, arr, has)
+        assert int(status.sum()) == 0
+        assert _leaves(out, off, len(items)) == host
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_unaligned_output_buffer(engine, shift):
+    """the writer works in aligned output dwords: a buffer that starts 1..3 bytes past a dword
+    boundary (its first dword partly before the buffer) and tiny leaves (RAW 0..3 bytes, BOOLEAN)
+    whose bytes share dwords with their neighbours"""
+    torch = pytest.importorskip("torch")
+    rng = random.Random(shift)
+    spec, items = _mixed_items(rng)
+    items = [("raw", bytes([1, 2, 3][:shift]), 0), ("boolean", 1, 0)] + items + [("raw", b"\x07", 0)]
+    for k in range(0, len(items), 17):
+        items.insert(k, ("raw", bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 4))), 0))
+    host = _lib.kryo_encode(items)
+    blob, arr, has = _lib.kryo_pack(items)
+    dev = torch.device("cuda", 0)
+    d_blob = torch.from_numpy(np.ascontiguousarray(blob)).to(dev)
+    a = arr.copy()
+    a["data"] = np.where(has, a["data"] + np.uint64(d_blob.data_ptr()), 0)
+    d_items = torch.from_numpy(a.view(np.uint8)).to(dev)
+    n = len(a)
+    total = sum(len(x) for x in host)
+    buf = torch.full((total + 16,), 0xEE, dtype=torch.uint8, device=dev)
+    out = buf[shift:shift + total]
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    engine.kryo_encode_device(d_items, n, out, off, status)
+    torch.cuda.synchronize()
+    assert int(status.sum()) == 0
+    b = buf.cpu().numpy()
+    assert (b[:shift] == 0xEE).all() and (b[shift + total:] == 0xEE).all()  # nothing outside the buffer
+    assert _leaves(out, off, n) == host

@@ -16,3 +16,6 @@ import csv
 r=list(csv.DictReader(open("$O/c4de_kernel_stats.csv")))
 for x in sorted(r,key=lambda x:-float(x['TotalDurationNs']))[:14]: print(x['Name'][:70], x['Calls'], round(float(x['AverageNs'])/1e6,3), x['Percentage'])
 PY
+cd $R
+timeout -k 10 300 python3 tools/microbench/radix32_ab.py 256 $O/r05_radix32_ab.json > $O/radix32.log 2>&1 || { echo "radix32 failed"; tail -20 $O/radix32.log; exit 1; }
+cat $O/radix32.log

@@ -1,6 +1,7 @@
 // Host check of the GPU encoder's template scheme (kryo_template.hpp), built by
 // tests/test_kryo_template.py with g++: groups items by shape exactly as the
-// GPU does (shape_of + same_shape), traces the first item of each shape
+// GPU does (shape_hash_of picks the slot, the first item's ShapeRec is the
+// slot's record, shape_matches confirms the others), traces the first item of each shape
 // (trace_leaf) and rebuilds EVERY item of the shape from those symbols
 // (sym_byte), comparing with the direct encoder (encode_leaf) byte for byte.
 // stats: [0] shapes, [1] items rebuilt from a template, [2] items without a
@@ -18,7 +19,7 @@ namespace {
 
 struct Rep {
   uint64_t hash;
-  Shape shape;
+  ShapeRec rec;
   int64_t size;  // -1 invalid, -2 no template
   std::vector<uint32_t> syms;
 };
@@ -45,29 +46,33 @@ extern "C" int kryo_template_check(const cordahip_kryo_item* items, uint64_t n, 
   for (int i = 0; i < 6; i++) stats[i] = 0;
   for (uint64_t i = 0; i < n; i++) {
     const cordahip_kryo_item& it = items[i];
-    const Shape s = shape_of(it);
+    uint64_t h = 0;
     std::vector<uint8_t> want(1 << 12);
     const bool ok = direct(it, want);
-    if (!s.ok) {
+    if (!shape_hash_of(it, h)) {
       stats[2]++;
       continue;
     }
-    const uint64_t h = shape_hash(s);
     Rep* r = nullptr;
     for (Rep& x : reps)
-      if (x.hash == h && same_shape(x.shape, s)) {
+      if (x.hash == h) {
         r = &x;
         break;
       }
     if (!r) {
       Rep x;
       x.hash = h;
-      x.shape = s;
+      ShapeRecord rv(x.rec);
+      shape_walk(it, rv);
       x.syms.assign(cap_syms, 0);
-      x.size = trace_leaf(it, x.syms.data(), cap_syms, levels.data());
+      x.size = x.rec.ok ? trace_leaf(it, x.syms.data(), cap_syms, levels.data()) : -2;
       reps.push_back(std::move(x));
       r = &reps.back();
       stats[0]++;
+    }
+    if (!shape_matches(it, r->rec)) {  // a hash collision, or a shape too big to record: direct encoder
+      stats[2]++;
+      continue;
     }
     if (r->size == -1) {  // invalid shape: the direct encoder must reject the item too
       stats[3]++;
