@@ -780,36 +780,65 @@ class C4H(C4):
     host_timed = True
 
     def __init__(self, eng, device, stream, rank, args):
+        import argparse
+
         from corda_amd import _lib
         if getattr(args, "device_encode", False):
-            raise SystemExit("--device-encode is a c4 option: c4h hands the library leaf bytes in host memory")
+            raise SystemExit("--device-encode is a c4 option: c4h hands the library leaf bytes in host memory "
+                             "(--components: the components, encoded on the GPU)")
+        self.components = bool(getattr(args, "components", False))
+        if self.components:  # the C4 corpus of cash-issue components (its device path encodes them each step)
+            args = argparse.Namespace(**dict(vars(args), device_encode=True))
         super().__init__(eng, device, stream, rank, args)
         ntx, ns = self.ntx, self.ns
         ar = np.arange(ns + 1, dtype=np.uint64)
-        self.t = [_pinned(x) for x in (
-            self.leaf_bytes.cpu().numpy(), self.leaf_off.cpu().numpy().astype(np.uint64),
-            self.tx_leaf_off.cpu().numpy().astype(np.uint64), self.tx_sig_off.cpu().numpy().astype(np.uint64),
-            np.full(ns, 4, np.uint8), self.keys.cpu().numpy().reshape(-1), ar * 32,
-            self.sigs.cpu().numpy().reshape(-1), ar * 64)]
+        sig_arrays = (np.full(ns, 4, np.uint8), self.keys.cpu().numpy().reshape(-1), ar * 32,
+                      self.sigs.cpu().numpy().reshape(-1), ar * 64)
         self.h_txid = _pinned(np.zeros((ntx, 32), np.uint8))
         self.h_txst = _pinned(np.zeros(ntx, np.uint8))
         self.h_sst = _pinned(np.zeros(ns, np.uint8))
         self.h_fb = _pinned(np.zeros(ntx, np.int64))
-        p = [x.data_ptr() for x in self.t]
-        tb = _lib.TxidBatch(ntx, p[0], p[1], p[2], self.h_txid.data_ptr(), self.h_txst.data_ptr())
-        self.b = _lib.SignedTxBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], self.h_sst.data_ptr(),
-                                    self.h_fb.data_ptr())
-        leaves = ("native Kryo leaves, %.0f B per tx" % (self.leaf_bytes.numel() / ntx) if self.native
-                  else "5 leaves of %s B" % list(C4_LEAF_LENS))
-        self.workload = ("C4 via the JVM boundary: cordahip_tx_submit over %d synthetic cash-issue txs per GPU in pinned "
-                         "host CSR memory (%s, 1-3 Ed25519 signers; PCIe included)" % (ntx, leaves))
-        self.config = dict(self.config, boundary="cordahip_tx_submit + cordahip_wait", host_memory="pinned CSR")
+        if self.components:
+            # what the JVM hands over instead of leaves: the Kryo items (data = offsets into the
+            # payload) and the payload blob -- the corrupted owner keys included
+            items = np.ascontiguousarray(self.host_items.reshape(-1))
+            payload = self.d_blob.cpu().numpy()
+            self.t = [_pinned(x) for x in (items.view(np.uint8), np.arange(0, 5 * ntx + 1, 5, dtype=np.uint64),
+                                           payload, self.tx_sig_off.cpu().numpy().astype(np.uint64)) + sig_arrays]
+            p = [x.data_ptr() for x in self.t]
+            tb = _lib.TxcompBatch(ntx, p[0], p[1], p[2], payload.size, self.h_txid.data_ptr(), self.h_txst.data_ptr())
+            self.b = _lib.SignedTxcompBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], self.h_sst.data_ptr(),
+                                            self.h_fb.data_ptr())
+            self.pcie_tx_bytes = (items.nbytes + 8 * (5 * ntx + 1) + payload.size) / ntx
+            what = ("the components of each tx (cordahip_txcomp_submit: %.0f B per tx of Kryo items and payload; "
+                    "the GPU writes the %.0f B of leaves)" % (self.pcie_tx_bytes, self.leaf_bytes.numel() / ntx))
+            self.kernel = ("cordahip_txcomp_submit (host CSR): kryo encode + sha256_leaves + merkle_root per id slice, "
+                           "then cordahip_sig_verify lanes")
+        else:
+            self.t = [_pinned(x) for x in (
+                self.leaf_bytes.cpu().numpy(), self.leaf_off.cpu().numpy().astype(np.uint64),
+                self.tx_leaf_off.cpu().numpy().astype(np.uint64), self.tx_sig_off.cpu().numpy().astype(np.uint64))
+                + sig_arrays]
+            p = [x.data_ptr() for x in self.t]
+            tb = _lib.TxidBatch(ntx, p[0], p[1], p[2], self.h_txid.data_ptr(), self.h_txst.data_ptr())
+            self.b = _lib.SignedTxBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], self.h_sst.data_ptr(),
+                                        self.h_fb.data_ptr())
+            self.pcie_tx_bytes = (self.leaf_bytes.numel() + 8 * (self.leaf_off.numel() + ntx + 1)) / ntx
+            what = ("native Kryo leaves, %.0f B per tx" % (self.leaf_bytes.numel() / ntx) if self.native
+                    else "5 leaves of %s B" % list(C4_LEAF_LENS))
+        self.workload = ("C4 via the JVM boundary: %s over %d synthetic cash-issue txs per GPU in pinned "
+                         "host CSR memory (%s, 1-3 Ed25519 signers; PCIe included)"
+                         % ("cordahip_txcomp_submit" if self.components else "cordahip_tx_submit", ntx, what))
+        self.config = dict(self.config, boundary=("cordahip_txcomp_submit" if self.components else "cordahip_tx_submit")
+                           + " + cordahip_wait", host_memory="pinned CSR", components=self.components,
+                           pcie_id_bytes_per_tx=round(self.pcie_tx_bytes, 1))
 
     def step(self):
         import ctypes
         from corda_amd._lib import check, lib
         t = ctypes.c_uint64()
-        check(lib().cordahip_tx_submit(self.eng.ctx, ctypes.byref(self.b), ctypes.byref(t)), "cordahip_tx_submit")
+        submit = lib().cordahip_txcomp_submit if self.components else lib().cordahip_tx_submit
+        check(submit(self.eng.ctx, ctypes.byref(self.b), ctypes.byref(t)), "cordahip_tx(comp)_submit")
         check(lib().cordahip_wait(self.eng.ctx, t.value, -1), "cordahip_wait")
 
     def check(self):
@@ -819,9 +848,15 @@ class C4H(C4):
         C4.step(self)  # the device-resident path over the same bytes: its ids
         self.torch.cuda.synchronize(self.device)
         txid = self.txid.cpu()
-        return {"mismatches_vs_construction": int((self.h_txst != exp_st).sum()) + int((self.h_fb != exp_bad).sum()),
-                "txid_mismatches_vs_device_path": int((self.h_txid != txid).any(dim=1).sum()),
-                "accepted_txs": int((self.h_txst == 0).sum()), "txs": self.ntx, "sigs": self.ns}
+        out = {"mismatches_vs_construction": int((self.h_txst != exp_st).sum()) + int((self.h_fb != exp_bad).sum()),
+               "txid_mismatches_vs_device_path": int((self.h_txid != txid).any(dim=1).sum()),
+               "accepted_txs": int((self.h_txst == 0).sum()), "txs": self.ntx, "sigs": self.ns}
+        if self.components:  # the device path's leaves against the host encoder (C4 --device-encode's check)
+            dev = C4.check(self)
+            out["device_path_mismatches_vs_construction"] = dev["mismatches_vs_construction"]
+            for k in ("kryo_item_errors", "leaf_mismatches_vs_host_encoder", "leaves_checked_vs_host_encoder"):
+                out[k] = dev[k]
+        return out
 
     def cpu_baseline(self, sample):
         self.sig_status = self.h_sst
@@ -960,6 +995,9 @@ def main():
     ap.add_argument("--c4-txs", type=int, default=10_000_000 // 8)
     ap.add_argument("--native-leaves", action="store_true",
                     help="c4 / c4h: real-shaped cash-issue leaves from the native Kryo encoder (SURVEY 8f-4)")
+    ap.add_argument("--components", action="store_true",
+                    help="c4h: hand the library the transactions' Kryo components (cordahip_txcomp_submit); "
+                         "the GPU writes the leaves")
     ap.add_argument("--device-encode", action="store_true",
                     help="c4: native leaves encoded on the GPU every step from the components in HBM "
                          "(cordahip_kryo_encode_device; implies --native-leaves)")

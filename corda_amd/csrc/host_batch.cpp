@@ -31,6 +31,7 @@
 #include <future>
 
 #include "der.hpp"
+#include "pack_rows.hpp"
 #include "runtime.hpp"
 #include "status.hpp"
 
@@ -87,24 +88,6 @@ std::vector<Chunk> make_chunks(const std::vector<Unit>& units, uint64_t chunk) {
       sz = std::min<uint64_t>(top, 4 * sz);
     }
   return out;
-}
-
-// ---- the two sources of Ed25519 rows --------------------------------------------
-// Ed25519 row of lane i of a cordahip_sig_batch (message length L): the
-// Crypto.doVerify require()s and the engine's length check as the pre-status
-inline void pack_ed_row(const cordahip_sig_batch* b, const MsgView& mv, bool do_verify, uint64_t i, uint32_t L,
-                        uint8_t* key, uint8_t* sig, uint8_t* msg, uint8_t* pre) {
-  std::memcpy(key, b->key + b->key_off[i], 32);
-  const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
-  uint8_t st = CORDAHIP_STATUS_OK;
-  if (do_verify && (sl == 0 || L == 0)) st = CORDAHIP_STATUS_EMPTY;  // Crypto.kt:475-476
-  else if (sl != 64) st = CORDAHIP_STATUS_MALFORMED_SIG;           // EdDSAEngine: signature length
-  if (st == CORDAHIP_STATUS_OK) std::memcpy(sig, b->sig + b->sig_off[i], 64);
-  else std::memset(sig, 0, 64);
-  *pre = st;
-  if (!msg) return;  // device-side message (MsgView::dev): gathered on the GPU
-  if (L == 32) std::memcpy(msg, mv.ptr(i), 32);
-  else if (L) std::memcpy(msg, mv.ptr(i), L);
 }
 
 // ---- dense Ed25519 rows in host memory -------------------------------------------
@@ -195,32 +178,6 @@ int ed_pipeline(cordahip_ctx* ctx, Device& d, const std::vector<Unit>& units, co
   return (e || e1 || e2) ? CORDAHIP_ERR_HIP : CORDAHIP_SUCCESS;
 }
 
-// Lane classes of a generic batch: the per-lane checks that precede the
-// engines (statuses decided here are written at once).
-enum : uint16_t { kDirect = 0, kEc = 1, kEdBase = 2 };
-
-inline uint16_t classify(const cordahip_sig_batch* b, const MsgView& mv, uint64_t i, uint64_t& mlen) {
-  const uint8_t sch = b->scheme[i];
-  const uint64_t kl = b->key_off[i + 1] - b->key_off[i];
-  mlen = mv.len(i);
-  if (sch == CORDAHIP_SCHEME_ECDSA_SECP256K1_SHA256 || sch == CORDAHIP_SCHEME_ECDSA_SECP256R1_SHA256) {
-    if (kl != 33 && kl != 65) {
-      b->status[i] = CORDAHIP_STATUS_BAD_KEY;  // ECCurve.decodePoint: invalid point encoding
-      return kDirect;
-    }
-    return kEc;
-  }
-  if (sch != CORDAHIP_SCHEME_EDDSA_ED25519_SHA512) {
-    b->status[i] = CORDAHIP_STATUS_UNSUPPORTED;  // Crypto.kt:474 require(isSupportedSignatureScheme)
-    return kDirect;
-  }
-  if (kl != 32) {
-    b->status[i] = CORDAHIP_STATUS_BAD_KEY;  // EdDSAPublicKeySpec: "public-key length is wrong"
-    return kDirect;
-  }
-  return kEdBase;  // + the piece-local message-length group
-}
-
 // Per-piece results of the classification pass of one chunk.
 struct PieceInfo {
   std::vector<std::pair<uint64_t, uint64_t>> ed;  // (message length, lanes), piece-local group order
@@ -228,41 +185,6 @@ struct PieceInfo {
   uint64_t ec = 0, ec_bytes = 0;                 // ECDSA lanes and their message bytes
   bool too_long = false;
 };
-
-// ECDSA slot packing of lane i into row r (messages CSR at *mo)
-inline void pack_ec_row(const cordahip_sig_batch* b, const MsgView& mv, bool do_verify, uint64_t i, uint64_t r, uint8_t* hsc, uint8_t* hk,
-                        uint8_t* hkl, uint8_t* hs, uint8_t* hsl, uint8_t* hm, uint64_t* hmo, uint8_t* hp,
-                        uint64_t& mo, uint32_t* hidx) {
-  hsc[r] = b->scheme[i];
-  const uint64_t kl = b->key_off[i + 1] - b->key_off[i];  // 33 or 65 (classified)
-  std::memcpy(hk + r * 65, b->key + b->key_off[i], kl);
-  std::memset(hk + r * 65 + kl, 0, 65 - kl);
-  hkl[r] = (uint8_t)kl;
-  const uint64_t sl = b->sig_off[i + 1] - b->sig_off[i];
-  const uint64_t ml = mv.len(i);
-  uint8_t pre = CORDAHIP_STATUS_OK;
-  if (sl <= 72) {
-    std::memcpy(hs + r * 72, b->sig + b->sig_off[i], sl);
-    std::memset(hs + r * 72 + sl, 0, 72 - sl);
-    hsl[r] = (uint8_t)sl;
-  } else {
-    // longer than the slot: no r, s < n fits, so the DER rules alone decide (BC:
-    // well-formed -> false, else SignatureException); the kernel still decodes
-    // the key first, so key errors keep precedence
-    DerInt dr, ds;
-    pre = (ml == 0 && do_verify) ? CORDAHIP_STATUS_EMPTY
-          : der_decode_sig(b->sig + b->sig_off[i], (uint32_t)std::min<uint64_t>(sl, 0xffffffffu), dr, ds)
-              ? CORDAHIP_STATUS_BAD_SIG
-              : CORDAHIP_STATUS_MALFORMED_SIG;
-    std::memset(hs + r * 72, 0, 72);
-    hsl[r] = 72;
-  }
-  hp[r] = pre;
-  hmo[r] = mo;
-  if (hidx) hidx[r] = (uint32_t)(mv.tx_of[i] - mv.dev->t0);  // the row is gathered on the device
-  else std::memcpy(hm + mo, mv.ptr(i), ml);
-  mo += ml;
-}
 
 // One device's input shard [lo, hi) of a generic batch, streamed in chunks
 // through kPackStages BatchStages. Per chunk, on the host pool: (1) classify
@@ -491,7 +413,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
               pack_ec_row(b, mv, do_verify, i, er, st.h[5].as<uint8_t>(), st.h[6].as<uint8_t>(),
                           st.h[7].as<uint8_t>(), st.h[8].as<uint8_t>(), st.h[9].as<uint8_t>(), st.h[10].as<uint8_t>(),
                           st.h[11].as<uint64_t>(), st.h[12].as<uint8_t>(), mo,
-                          dev ? st.hidx[1].as<uint32_t>() : nullptr);
+                          dev ? st.hidx[1].as<uint32_t>() : nullptr, dev ? dev->t0 : 0);
               er++;
             } else if (c >= kEdBase) {
               const size_t j = c - kEdBase, gi = P.ed_global[j];

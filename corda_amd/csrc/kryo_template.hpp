@@ -142,7 +142,39 @@ KRYO_HD inline bool shape_walk(const cordahip_kryo_item& it, V& v) {
   }
 }
 
-// FNV-1a over the words and the span bytes
+// Up to 16 bytes p[0 .. min(n, 16)) as 4 little-endian words, zero-padded. On
+// the GPU: at most two aligned 16-byte loads, each holding one of the wanted
+// bytes (so both are mapped), and a funnel shift -- the shape walks read long
+// spans (class names, TransactionType's text) 16 bytes per load.
+KRYO_HD inline void span16(const uint8_t* p, uint32_t n, uint32_t w[4]) {
+  const uint32_t m = n < 16 ? n : 16;
+#if defined(__HIP_DEVICE_COMPILE__)
+  w[0] = w[1] = w[2] = w[3] = 0;
+  if (!m) return;
+  const uintptr_t qa = (uintptr_t)p, ca = qa & ~(uintptr_t)15;
+  const uint32_t s = (uint32_t)(qa - ca);
+  uint4 u0 = *reinterpret_cast<const uint4*>(ca), u1 = make_uint4(0, 0, 0, 0);
+  if (s + m - 1 >= 16) u1 = *reinterpret_cast<const uint4*>(ca + 16);
+  const uint32_t d[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+  const uint32_t dw = s >> 2, sb = s & 3;
+  uint32_t e[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++)
+    e[i] = dw == 0 ? d[i] : dw == 1 ? d[i + 1] : dw == 2 ? d[i + 2] : (i + 3 < 8 ? d[i + 3] : 0);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t x = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
+    const uint32_t k = m > 4 * (uint32_t)i ? m - 4 * i : 0;  // wanted bytes of word i
+    w[i] = k >= 4 ? x : (k ? x & ((1u << (8 * k)) - 1) : 0);
+  }
+#else
+  for (int i = 0; i < 4; i++) w[i] = 0;
+  for (uint32_t i = 0; i < m; i++) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+#endif
+}
+
+// FNV-1a over the words and each span's length, first 16 and last 16 bytes
+// (the hash only picks a table slot; shape_matches compares every byte)
 struct ShapeHash {
   uint64_t h = 1469598103934665603ull;
   KRYO_HD void mix(uint32_t x) {
@@ -152,19 +184,27 @@ struct ShapeHash {
   KRYO_HD void word(uint32_t x) { mix(x); }
   KRYO_HD void span(const uint8_t* p, uint32_t n) {
     mix(0x100 | n);
-    for (uint32_t i = 0; i < n; i++) mix(p[i]);
+    uint32_t w[4];
+    span16(p, n, w);
+    for (int i = 0; i < 4; i++) mix(w[i]);
+    if (n > 16) {
+      span16(p + n - 16, 16, w);
+      for (int i = 0; i < 4; i++) mix(w[i]);
+    }
   }
   KRYO_HD uint64_t value() const { return h ^ (h >> 29); }
 };
 
 // A shape as data: the GPU keeps one per table slot (the words and the span
 // BYTES, so the record outlives the call whose item it came from), and items
-// are compared with it as they are walked (ShapeCmp).
+// are compared with it as they are walked (ShapeCmp). Each span's bytes start
+// 16-byte aligned in `bytes`, zero-padded, so a compare reads them 16 at a time.
 struct ShapeRec {
-  static constexpr uint32_t kWords = 48, kSpans = 8, kBytes = 192;
+  static constexpr uint32_t kWords = 48, kSpans = 8, kBytes = 256;
   uint32_t nw, ns, nb, ok;
   uint32_t w[kWords];
   uint32_t sl[kSpans];
+  uint32_t so[kSpans];
   uint8_t bytes[kBytes];
 };
 
@@ -176,31 +216,62 @@ struct ShapeRecord {  // visitor: fills a record (ok = 0 when it does not fit)
     else r.ok = 0;
   }
   KRYO_HD void span(const uint8_t* p, uint32_t n) {
-    if (r.ns >= ShapeRec::kSpans || r.nb + n > ShapeRec::kBytes) {
+    const uint32_t padded = (n + 15) / 16 * 16;
+    if (r.ns >= ShapeRec::kSpans || r.nb + padded > ShapeRec::kBytes) {
       r.ok = 0;
       return;
     }
-    r.sl[r.ns++] = n;
-    for (uint32_t i = 0; i < n; i++) r.bytes[r.nb++] = p[i];
+    r.sl[r.ns] = n;
+    r.so[r.ns++] = r.nb;
+    for (uint32_t i = 0; i < padded; i++) r.bytes[r.nb + i] = i < n ? p[i] : 0;
+    r.nb += padded;
   }
 };
 
 struct ShapeCmp {  // visitor: eq stays true while the walk matches the record
   const ShapeRec& r;
-  uint32_t iw = 0, is = 0, ib = 0;
+  uint32_t iw = 0, is = 0;
+  uint32_t buf[4] = {0, 0, 0, 0};  // record words iw & ~3 .. + 3 (read 4 at a time)
   bool eq = true;
   KRYO_HD explicit ShapeCmp(const ShapeRec& x) : r(x) {}
   KRYO_HD void word(uint32_t x) {
-    eq = eq && iw < r.nw && r.w[iw] == x;
+    if (iw >= ShapeRec::kWords) {
+      eq = false;
+      return;
+    }
+    if ((iw & 3) == 0) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      const uint4 q = *reinterpret_cast<const uint4*>(&r.w[iw]);
+      buf[0] = q.x, buf[1] = q.y, buf[2] = q.z, buf[3] = q.w;
+#else
+      for (int i = 0; i < 4; i++) buf[i] = r.w[iw + i];
+#endif
+    }
+    const uint32_t k = iw & 3;
+    const uint32_t y = k == 0 ? buf[0] : k == 1 ? buf[1] : k == 2 ? buf[2] : buf[3];
+    eq = eq && iw < r.nw && y == x;
     iw++;
   }
   KRYO_HD void span(const uint8_t* p, uint32_t n) {
-    eq = eq && is < r.ns && r.sl[is] == n && ib + n <= r.nb;
-    for (uint32_t i = 0; eq && i < n; i++) eq = r.bytes[ib + i] == p[i];
+    eq = eq && is < r.ns && r.sl[is] == n;
+    const uint32_t o = eq ? r.so[is] : 0;
+    for (uint32_t i = 0; eq && i < n; i += 16) {
+      uint32_t w[4];
+      span16(p + i, n - i, w);
+#if defined(__HIP_DEVICE_COMPILE__)
+      const uint4 q = *reinterpret_cast<const uint4*>(&r.bytes[o + i]);
+      eq = q.x == w[0] && q.y == w[1] && q.z == w[2] && q.w == w[3];
+#else
+      for (int k = 0; k < 4; k++) {
+        uint32_t y = 0;
+        for (int b = 0; b < 4; b++) y |= (uint32_t)r.bytes[o + i + 4 * k + b] << (8 * b);
+        eq = eq && y == w[k];
+      }
+#endif
+    }
     is++;
-    ib += n;
   }
-  KRYO_HD bool done() const { return eq && iw == r.nw && is == r.ns && ib == r.nb; }
+  KRYO_HD bool done() const { return eq && iw == r.nw && is == r.ns; }
 };
 
 // hash of an item's shape; false: no shape
