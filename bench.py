@@ -985,7 +985,7 @@ def _clock_under_load(device_index, run_step, sync, ms_per_step):
                       "resident beside one extra untimed step of this workload; median over intervals"}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -1006,11 +1006,15 @@ def main():
     ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock sampling step")
     ap.add_argument("--global-log2", type=int, default=None,
                     help="C5 only: strong scaling over a fixed 2^G global batch (SURVEY 8d C5: G = 28)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
     if args.global_log2 and args.workload != "c5":
-        ap.error("--global-log2 applies to --workload c5")
+        raise SystemExit("bench.py: error: --global-log2 applies to --workload c5")
     if args.gpus < 1:
-        ap.error("--gpus must be >= 1")
+        raise SystemExit("bench.py: error: --gpus must be >= 1")
     if args.batch_log2 is None:
         args.batch_log2 = 20 if args.workload == "c1" else 24
 

@@ -306,7 +306,8 @@ def cash_issue_items(issuer_keys: np.ndarray, owner_keys: np.ndarray, notary_key
     the issue Command, the notary Party, the mustSign key, TransactionType.General) with their payloads
     in ONE byte blob: returns (blob uint8, items KRYO_ITEM_DTYPE[ntx, 5]) whose `data` fields are
     OFFSETS into the blob (add the blob's address -- host or device -- before encoding), and the
-    blob layout of the owner keys ({"owner_key": tx 0's offset, "cash_stride": bytes per tx}).
+    blob layout of the owner keys ({"owner_key": tx 0's offset, "cash_stride": bytes per tx}). The blob
+    is tx-major: the shared payloads, then each transaction's cash state, command and key.
     issuer_keys[t] (Ed25519 A) issues quantities[t] USD cents (issue reference 01) to the anonymised
     owner_keys[t] (an AnonymousParty, as CashIssueFlow's default confidential recipient), notary
     "Notary Service, Zurich, CH"; the command signer and mustSign key = the issuer key."""
@@ -335,9 +336,14 @@ def cash_issue_items(issuer_keys: np.ndarray, owner_keys: np.ndarray, notary_key
     cmd[:, oc:oc + 32] = ik
     party = np.frombuffer(notary + bytes(notary_key), np.uint8)
     gen = np.frombuffer(TRANSACTION_TYPE_GENERAL.encode("utf-16-le"), np.uint8)
-    parts = [cash.reshape(-1), cmd.reshape(-1), ik.reshape(-1), party, gen]
-    base = np.cumsum([0] + [p.size for p in parts])
-    blob = np.concatenate(parts)
+    # tx-major, as a JVM writing one transaction's components after another would: the shared
+    # payloads (the notary Party, the TransactionType name) first, then per transaction its
+    # cash state, command and key -- every id slice's components then lie in one prefix of the
+    # blob (what cordahip_txcomp_submit copies ahead of each slice)
+    shared = np.concatenate([party, gen])
+    rec = np.concatenate([cash, cmd, ik], axis=1)
+    stride = rec.shape[1]
+    blob = np.concatenate([shared, rec.reshape(-1)])
     items = np.zeros((ntx, 5), _lib.KRYO_ITEM_DTYPE)
     kinds = [_lib.KRYO_KINDS[k] for k in ("cash_state", "issue_command", "party", "ed25519_key", "kotlin_object")]
     items["kind"] = kinds
@@ -345,20 +351,20 @@ def cash_issue_items(issuer_keys: np.ndarray, owner_keys: np.ndarray, notary_key
     items["value"][:, 0] = quantities
     items["value"][:, 1] = nonces
     items["value"][:, 2] = ed  # the notary key's class
-    t = np.arange(ntx, dtype=np.uint64)
-    items["data"][:, 0] = base[0] + t * cash.shape[1]
+    t0 = shared.size + np.arange(ntx, dtype=np.uint64) * stride
+    items["data"][:, 0] = t0
     items["len"][:, 0] = cash.shape[1]
-    items["data"][:, 1] = base[1] + t * cmd.shape[1]
+    items["data"][:, 1] = t0 + cash.shape[1]
     items["len"][:, 1] = cmd.shape[1]
-    items["data"][:, 2] = base[3]
+    items["data"][:, 2] = 0
     items["len"][:, 2] = party.size
-    items["data"][:, 3] = base[2] + t * 32
+    items["data"][:, 3] = t0 + cash.shape[1] + cmd.shape[1]
     items["len"][:, 3] = 32
-    items["data"][:, 4] = base[4]
+    items["data"][:, 4] = party.size
     items["len"][:, 4] = gen.size // 2
     # where transaction t's owner key sits in the blob (bench corruption: a flipped
     # key byte changes the output leaf and so the id, as a flipped leaf byte does)
-    layout = {"owner_key": base[0] + oo, "cash_stride": cash.shape[1]}
+    layout = {"owner_key": shared.size + oo, "cash_stride": stride}
     return blob, items, layout
 
 

@@ -229,6 +229,7 @@ hipError_t kryo_state_ready(Device& d, hipStream_t s) {
   const volatile uint32_t* u = d.kryo_usage;
   if (d.kryo_fresh || u[0] > kryo_clear_threshold_templates() || u[1] > kryo_clear_threshold_slots()) {
     d.kryo_fresh = false;
+    d.kryo_templates_ok = false;  // an empty table: the next component batch builds its shapes
     d.kryo_usage[0] = d.kryo_usage[1] = 0;
     return kryo_clear(d.kryo_fixed.as<uint8_t>(), s);
   }
@@ -236,7 +237,7 @@ hipError_t kryo_state_ready(Device& d, hipStream_t s) {
 }
 // after a call's encoder launches: its usage counters to the host-mapped copy
 hipError_t kryo_usage_report(Device& d, hipStream_t s) {
-  return launch_store_to_host(kryo_usage_src(d.kryo_fixed.as<uint8_t>()), d.kryo_usage_dev, 8, s);
+  return launch_store_to_host(kryo_usage_src(d.kryo_fixed.as<uint8_t>()), d.kryo_usage_dev, kKryoUsageBytes, s);
 }
 // grows kryo_fixed if needed (once: its size is fixed), marking it fresh
 hipError_t kryo_fixed_ensure(Device& d) {
@@ -443,7 +444,8 @@ struct CompPlan {
   uint64_t slice_cap = 16;        // leaf bytes of the largest slice's bound (two slice buffers alternate)
   uint64_t max_items = 0;
   uint64_t copied = 0;            // payload prefix enqueued so far
-  static constexpr uint64_t kDirectWriters = 1u << 15;
+  bool templates_only = false;    // the steady-state encoder chain (misses redo the call)
+  static constexpr uint64_t kDirectWriters = 1u << 13;  // the direct encoder's writers (rarely any work)
 };
 
 hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound,
@@ -507,6 +509,8 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batc
         return hipErrorOutOfMemory;
     }
     if (hipError_t e = kryo_state_ready(d, d.stream)) return e;
+    if (hipError_t e = kryo_reset_misses(d.kryo_fixed.as<uint8_t>(), d.stream)) return e;
+    cp->templates_only = cp->templates_only && d.kryo_templates_ok;
   } else {
     leaf_buf = b->leaf_off[l1] - b->leaf_off[l0];
   }
@@ -565,7 +569,7 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
                                      cp->c->payload_len, n, cp->group[j], d.kryo_fixed.as<uint8_t>(), slots, slots + n,
                                      d.kryo_sizes.as<uint64_t>(), w.leaf_off.as<uint64_t>() + (ls0 - l0), sb,
                                      cp->slice_cap, w.comp_status.as<uint8_t>() + (ls0 - l0), d.kryo_ws.as<uint8_t>(),
-                                     CompPlan::kDirectWriters, d.kryo_temp.p, d.kryo_temp.cap, s);
+                                     CompPlan::kDirectWriters, d.kryo_temp.p, d.kryo_temp.cap, s, cp->templates_only);
       e = e ? e : launch_sha256_leaves(sb, w.leaf_off.as<uint64_t>() + (ls0 - l0), n,
                                        w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
     } else {
@@ -653,8 +657,11 @@ void reduce_txs(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b, uint64_t t
 // host. (r03 waited for each slice's ids on the host and copied them back as
 // messages: the GPU sat idle ~5 ms per C4 step until the first signatures were
 // packed.)
-int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b, uint64_t* tx_of,
-                     uint64_t lo, uint64_t hi, uint64_t slices, const cordahip_txcomp_batch* comps) {
+constexpr int kRedoFull = -1000;  // a templates-only component call missed: run it again with the full encoder
+
+int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b, uint64_t* tx_of,
+                          uint64_t lo, uint64_t hi, uint64_t slices, const cordahip_txcomp_batch* comps,
+                          bool templates_only) {
   std::lock_guard<std::mutex> g(d.tx_mu);  // d.tx (the ids) stays ours until every gather has run
   // component batches also use the GPU encoder's scratch (d.kryo_*) for the whole call
   std::unique_lock<std::mutex> gk(d.kryo_mu, std::defer_lock);
@@ -662,6 +669,7 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   if (comps) {
     gk.lock();
     plan.c = comps;
+    plan.templates_only = templates_only;
     cp = &plan;
   }
   int r = tx_acquire_host(d);
@@ -673,19 +681,17 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   const uint64_t s0 = b->tx_sig_off[lo], s1 = b->tx_sig_off[hi];
   // signature chunks of whole full-occupancy rounds of the Ed25519 ladder
   // (2^17 lanes: 2 waves x 1,024 SIMDs x 64), each waiting on device for the
-  // slice that holds its last transaction. Uniform slices with slice-aligned
-  // chunks of ~156K C4 signatures ran 1.19 ladder rounds each, the second at
-  // 19% occupancy: 12.8 ns per signature against ~10 for whole rounds
-  // (profiles/r04_f kernel trace, r04_i host trace). Chunks are half a round
-  // (the GPU starts after the leaf bytes of 2^16 signatures' transactions,
-  // ~0.5 ms of PCIe), the two Ed25519 streams keeping two chunks in flight so
-  // one chunk's end-of-grid tail overlaps the next chunk.
-  uint64_t chunk = 1u << 16;
+  // slice that holds its last transaction. r04 ran half rounds (2^16: the GPU
+  // starts after the leaf bytes of fewer transactions, and two Ed25519 streams
+  // keep two chunks in flight so one chunk's tail overlaps the next). Since the
+  // id kernels run at raised wave priority (tx.hip g_id_prio) a slice's ids no
+  // longer trail the ladders, and whole rounds win: interleaved on one corpus,
+  // c4h 84.1 against 81.6 M sig/s, c4h --components 75.0 against 72.3; 2^18:
+  // 70.3 (profiles/r05_c4h_chunk_ab/).
+  uint64_t chunk = 1u << 17;
   if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK")) chunk = std::max<uint64_t>(1, strtoull(v, nullptr, 10));
   // chunks double from `chunk` up to CORDAHIP_TX_SIG_CHUNK_MAX (default: chunk,
-  // i.e. constant half-round chunks: with the id slices following the chunks,
-  // 2^16-signature chunks ran 84.3-84.7 M/s against 81.3-82.4 for 2^16 then
-  // 2^17 and 54.8 for 2^15, profiles/r04_w)
+  // constant chunks; 2^16 doubling to 2^17 ran 83.9 against 84.1 M/s, r05)
   uint64_t chunk_max = chunk;
   if (const char* v = getenv("CORDAHIP_TX_SIG_CHUNK_MAX")) chunk_max = std::max<uint64_t>(chunk, strtoull(v, nullptr, 10));
   for (uint64_t x = s0, c = chunk; x < s1; x += c, c = std::min(chunk_max, 2 * c)) di.chunk_bound.push_back(x);
@@ -806,6 +812,17 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   const hipError_t e1 = hipStreamSynchronize(d.s_idcopy ? d.s_idcopy : d.stream), e2 = hipStreamSynchronize(d.stream);
   if (r == CORDAHIP_SUCCESS && (e1 != hipSuccess || e2 != hipSuccess)) r = CORDAHIP_ERR_HIP;
   if (r != CORDAHIP_SUCCESS) return r;
+  if (cp) {
+    // the encoder's misses in this call (kryo_usage_report ran on d.stream, drained above):
+    // a templates-only call with any is void; a full call without any lets the next
+    // call on this device take the templates-only chain
+    const uint32_t misses = static_cast<const volatile uint32_t*>(d.kryo_usage)[2];
+    if (cp->templates_only && misses) {
+      d.kryo_templates_ok = false;
+      return kRedoFull;
+    }
+    d.kryo_templates_ok = misses == 0;
+  }
   // the transactions no chunk reduced: chunk-edge ones, those without signatures
   std::sort(reduced.begin(), reduced.end());
   uint64_t t = lo;
@@ -815,6 +832,23 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
   }
   reduce_txs(ctx, b, t, hi);
   return r;
+}
+
+// A component batch runs the encoder's templates-only chain when the device's
+// last component batch needed no new template and no direct encoder
+// (Device::kryo_templates_ok): per id slice, shape -> scan -> template writes,
+// without the build / size / direct-write kernels whose empty launches sat on
+// each slice's critical path. An item that would need them is a miss; the call
+// then runs again with the full chain (its results overwrite every output).
+// CORDAHIP_KRYO_TEMPLATES_ONLY=0 always runs the full chain.
+int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b, uint64_t* tx_of, uint64_t lo,
+                     uint64_t hi, uint64_t slices, const cordahip_txcomp_batch* comps) {
+  static const bool spec = [] {
+    const char* v = getenv("CORDAHIP_KRYO_TEMPLATES_ONLY");
+    return !(v && v[0] == '0');
+  }();
+  const int r = signed_tx_device_once(ctx, d, b, tx_of, lo, hi, slices, comps, comps && spec);
+  return r == kRedoFull ? signed_tx_device_once(ctx, d, b, tx_of, lo, hi, slices, comps, false) : r;
 }
 
 int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b, const cordahip_txcomp_batch* comps = nullptr) {
@@ -1225,6 +1259,11 @@ static int init_impl(uint32_t device_mask, cordahip_ctx** out) {
       rc = CORDAHIP_ERR_OUT_OF_MEMORY;
       break;
     }
+    static const bool id_prio = !(getenv("CORDAHIP_ID_PRIO") && getenv("CORDAHIP_ID_PRIO")[0] == '0');
+    if (!id_prio && (tx_set_id_priority(0) != hipSuccess || kryo_set_priority(0) != hipSuccess)) {
+      rc = CORDAHIP_ERR_HIP;
+      break;
+    }
     if (launch_ed25519_btable(dev.btab, dev.stream) != hipSuccess ||
         launch_ecdsa_gtables(dev.gtab_k1, dev.gtab_r1, dev.stream) != hipSuccess ||
         hipEventRecord(dev.tx_ev, dev.stream) != hipSuccess || hipStreamSynchronize(dev.stream) != hipSuccess)
@@ -1528,7 +1567,7 @@ int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_ite
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     // the direct encoder's writers (items without a template): 2^15 threads,
     // 7 KB of level buffers each (224 MB)
-    const uint64_t dwriters = 1u << 15;
+    const uint64_t dwriters = 1u << 13;
     size_t temp_bytes = 0;
     if (kryo_scan_bytes(temp_bytes, n + 1, s) != hipSuccess) return CORDAHIP_ERR_HIP;
     if (d->kryo_sizes.cap < (n + 1) * 8 || d->kryo_temp.cap < temp_bytes || d->kryo_items.cap < n * 8 + 8 ||

@@ -76,10 +76,15 @@ constexpr uint32_t kRawSlot = 0xfffffffeu; // item_slot: a RAW leaf (copied)
 constexpr int32_t kNoTemplate = -2, kUnbuilt = -3;  // slot_size values besides a size (-1: an invalid shape)
 constexpr uint32_t kDefer = 0x80000000u;  // item_slot: the slot was claimed this call (verified in kryo_tsize)
 constexpr uint32_t kLeavesPerWave = 16;  // a wave writes the output span of this many leaves
+constexpr uint32_t kBuildWaves = 16;     // kryo_build: waves (new shapes taken in turn)
+constexpr uint32_t kDsizeBlocks = 64;    // kryo_dsize: blocks of 256 (direct items taken in turn)
 constexpr uint32_t kLevelSyms = kryo::kLevelBytes;  // levels 1..7 (level 0 is the leaf itself)
 // counters: [0] new shapes this call, [1] direct items this call, [2] templates
-// in the arena, [3] table slots in use (the last two persist with the table)
-enum { kCNew = 0, kCDirect = 1, kCArena = 2, kCUsed = 3 };
+// in the arena, [3] table slots in use (the last two persist with the table),
+// [4] misses: items that needed a new template or the direct encoder since the
+// host last reset it (a templates-only chain did not write their leaves)
+enum { kCNew = 0, kCDirect = 1, kCArena = 2, kCUsed = 3, kCMiss = 4 };
+constexpr uint8_t kKryoMiss = 4;  // item status of a miss (runtime.hpp)
 
 // Items as the encoder sees them. base == nullptr: `data` are device pointers
 // (cordahip_kryo_encode_device). Otherwise `data` are offsets into a payload of
@@ -103,10 +108,28 @@ struct ItemSrc {
   }
 };
 
+// Thread j's item when the batch is records of `group` items (a transaction's
+// components): kind-major within tiles of 64 records, so each wave takes one
+// kind (the shape walk does not diverge) while the waves of a tile read the
+// same 64 records' items and payload together. (r05's first mapping was
+// kind-major over the whole batch: every record's lines were fetched once per
+// kind, 5.1 KB of L2-fabric reads per cash-issue transaction in kryo_shape,
+// profiles/r05_pmc_kryo_traffic.json.) Threads past the last record: n.
+// the encoder's kernels run at the id kernels' raised wave priority (tx.hip g_id_prio)
+__device__ uint32_t g_kryo_prio = 1;
+__device__ inline void kryo_priority() {
+  if (g_kryo_prio) __builtin_amdgcn_s_setprio(3);
+}
+
 __device__ inline uint64_t item_of(uint64_t j, uint64_t n, uint32_t group) {
   if (group <= 1 || n % group) return j;
-  const uint64_t rec = n / group;  // records of `group` items: kind-major thread order
-  return (j % rec) * group + j / rec;
+  const uint64_t tile = j / (64ull * group), r = j % (64ull * group), rec = tile * 64 + r % 64;
+  return rec < n / group ? rec * group + r / 64 : n;
+}
+// threads the shape pass launches for n items (whole tiles of 64 records)
+inline uint64_t item_threads(uint64_t n, uint32_t group) {
+  if (group <= 1 || n % group) return n;
+  return (n / group + 63) / 64 * 64 * group;
 }
 
 // ---- 1. shapes ------------------------------------------------------------------
@@ -115,6 +138,7 @@ __device__ inline uint64_t item_of(uint64_t j, uint64_t n, uint32_t group) {
 // (slot_size still kUnbuilt) is compared after kryo_build, in kryo_tsize.
 __device__ inline void direct_item(uint32_t* direct, uint32_t* counters, uint64_t i) {
   direct[atomicAdd(&counters[kCDirect], 1u)] = (uint32_t)i;  // sized by kryo_dsize
+  atomicAdd(&counters[kCMiss], 1u);
 }
 
 // the size and status of an item of slot `slot` (built): false when it goes to the direct encoder
@@ -126,17 +150,21 @@ __device__ inline bool template_item(const cordahip_kryo_item& it, const kryo::S
   return true;
 }
 
-__global__ void __launch_bounds__(256) kryo_shape_kernel(ItemSrc items, uint64_t n, uint32_t group,
+// templates_only: no slot is claimed and nothing goes to the direct encoder; an
+// item without a built template of its shape is a miss (kKryoMiss, size 0,
+// item_slot kNoSlot: kryo_twrite does not write it).
+__global__ void __launch_bounds__(256) kryo_shape_kernel(ItemSrc items, uint64_t n, uint32_t group, bool templates_only,
                                                          unsigned long long* __restrict__ table,
                                                          const int32_t* __restrict__ slot_size,
                                                          const kryo::ShapeRec* __restrict__ rec,
                                                          uint32_t* __restrict__ item_slot, uint32_t* __restrict__ shape_list,
                                                          uint64_t* __restrict__ sizes, uint8_t* __restrict__ status,
                                                          uint32_t* __restrict__ direct, uint32_t* __restrict__ counters) {
+  kryo_priority();
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j == 0) sizes[n] = 0;  // the scan's last element: off[n] = the total
-  if (j >= n) return;
   const uint64_t i = item_of(j, n, group);
+  if (i >= n) return;
   const cordahip_kryo_item it = items[i];
   uint64_t size = 0;
   uint8_t st = 0;
@@ -157,6 +185,7 @@ __global__ void __launch_bounds__(256) kryo_shape_kernel(ItemSrc items, uint64_t
     uint32_t k = (uint32_t)h & (kSlots - 1);
     for (uint32_t probe = 0; probe < kMaxProbe; probe++, k = (k + 1) & (kSlots - 1)) {
       unsigned long long v = __hip_atomic_load(&table[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v == 0 && templates_only) break;  // an unknown shape: a miss
       if (v == 0) {
         v = atomicCAS(&table[k], 0ull, mine);
         if (v == 0) {  // claimed: this item represents a new shape
@@ -175,14 +204,23 @@ __global__ void __launch_bounds__(256) kryo_shape_kernel(ItemSrc items, uint64_t
   }
   if (slot != kNoSlot) {
     const int32_t z = claimed ? kUnbuilt : slot_size[slot];
-    if (z == kUnbuilt) {  // built after this kernel: compared in kryo_tsize
+    if (z == kUnbuilt && !templates_only) {  // built after this kernel: compared in kryo_tsize
+      atomicAdd(&counters[kCMiss], 1u);
       item_slot[i] = slot | kDefer;
       return;
     }
-    if (!template_item(it, rec[slot], z, size, st)) slot = kNoSlot;
+    if (z == kUnbuilt || !template_item(it, rec[slot], z, size, st)) slot = kNoSlot;
   }
   item_slot[i] = slot;
-  if (slot == kNoSlot) direct_item(direct, counters, i);
+  if (slot == kNoSlot) {
+    if (templates_only) {
+      atomicAdd(&counters[kCMiss], 1u);
+      size = 0;
+      st = kKryoMiss;
+    } else {
+      direct_item(direct, counters, i);
+    }
+  }
   sizes[i] = size;
   status[i] = st;
 }
@@ -269,6 +307,7 @@ __global__ void __launch_bounds__(256) kryo_tsize_kernel(ItemSrc items, uint64_t
                                                          const kryo::ShapeRec* __restrict__ rec,
                                                          uint64_t* __restrict__ sizes, uint8_t* __restrict__ status,
                                                          uint32_t* __restrict__ direct, uint32_t* __restrict__ counters) {
+  kryo_priority();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t slot = item_slot[i];
@@ -412,6 +451,7 @@ __global__ void __launch_bounds__(256) kryo_twrite_kernel(ItemSrc items, uint64_
                                                           const uint32_t* __restrict__ slot_map,
                                                           const uint32_t* __restrict__ arena, uint8_t* __restrict__ out,
                                                           uint64_t cap, uint8_t* __restrict__ status) {
+  kryo_priority();
   __shared__ LeafMeta meta_s[4][kLeavesPerWave];
   __shared__ uint32_t bound_s[4][kLeavesPerWave + 1];
   __shared__ uint32_t queue_s[4][kQueue];
@@ -584,15 +624,19 @@ hipError_t kryo_clear(uint8_t* fixed, hipStream_t s) {
   e = e ? e : hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(k.slot_size), (int)kUnbuilt, kSlots, s);
   return e ? e : hipMemsetAsync(k.counters, 0, 64, s);
 }
-// counters[kCArena], counters[kCUsed] (device) -> usage[0..1] (host-mapped), after a call
+// counters[kCArena .. kCMiss + 1] (device) -> usage[0..3] (host-mapped), after a call
 const uint32_t* kryo_usage_src(uint8_t* fixed) { return KryoState(fixed).counters + kCArena; }
+hipError_t kryo_reset_misses(uint8_t* fixed, hipStream_t s) {
+  return hipMemsetAsync(KryoState(fixed).counters + kCMiss, 0, 4, s);
+}
 uint32_t kryo_clear_threshold_slots() { return kSlots / 2; }
 uint32_t kryo_clear_threshold_templates() { return kBuilders - 64; }
 
 hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
                               uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
                               uint64_t* sizes, uint64_t* off, uint8_t* out, uint64_t cap, uint8_t* status,
-                              uint8_t* dws, uint64_t dwriters, void* scan_temp, size_t scan_bytes, hipStream_t s) {
+                              uint8_t* dws, uint64_t dwriters, void* scan_temp, size_t scan_bytes, hipStream_t s,
+                              bool templates_only) {
   const ItemSrc items{d_items, data_base, data_len};
   const KryoState k(fixed);
   hipError_t e = hipMemsetAsync(k.counters, 0, 8, s);  // kCNew, kCDirect
@@ -600,14 +644,21 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* 
     e = e ? e : hipMemsetAsync(off, 0, 8, s);
     return e;
   }
-  const uint32_t blocks = (uint32_t)((n + 255) / 256);
-  hipLaunchKernelGGL(kryo_shape_kernel, dim3(blocks), dim3(256), 0, s, items, n, group, k.table, k.slot_size, k.rec,
-                     item_slot, k.shape_list, sizes, status, direct, k.counters);
-  hipLaunchKernelGGL(kryo_build_kernel, dim3(256), dim3(64), 0, s, items, k.table, k.shape_list, k.counters, k.rec,
-                     k.slot_size, k.slot_map, k.arena);
-  hipLaunchKernelGGL(kryo_tsize_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, items, n, item_slot,
-                     k.slot_size, k.rec, sizes, status, direct, k.counters);
-  hipLaunchKernelGGL(kryo_dsize_kernel, dim3(1024), dim3(256), 0, s, items, direct, k.counters, sizes, status);
+  hipLaunchKernelGGL(kryo_shape_kernel, dim3((uint32_t)((item_threads(n, group) + 255) / 256)), dim3(256), 0, s, items,
+                     n, group, templates_only, k.table, k.slot_size, k.rec, item_slot, k.shape_list, sizes, status,
+                     direct, k.counters);
+  // build, tsize, dsize (and dwrite) serve new shapes and direct items; in steady
+  // state they find nothing to do, yet beside the Ed25519 ladders of a component
+  // batch each empty launch of build / dsize / dwrite took 0.07-0.47 ms on the
+  // slice's critical path (profiles/r05_c4h_rare_ab: 57.8 -> 68.0 M sig/s without
+  // them). The templates-only chain leaves them out and reports misses instead.
+  if (!templates_only) {
+    hipLaunchKernelGGL(kryo_build_kernel, dim3(kBuildWaves), dim3(64), 0, s, items, k.table, k.shape_list, k.counters,
+                       k.rec, k.slot_size, k.slot_map, k.arena);
+    hipLaunchKernelGGL(kryo_tsize_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, items, n, item_slot,
+                       k.slot_size, k.rec, sizes, status, direct, k.counters);
+    hipLaunchKernelGGL(kryo_dsize_kernel, dim3(kDsizeBlocks), dim3(256), 0, s, items, direct, k.counters, sizes, status);
+  }
   e = hipGetLastError();
   size_t tb = scan_bytes;
   e = e ? e : hipcub::DeviceScan::ExclusiveSum(scan_temp, tb, sizes, off, (int)(n + 1), s);
@@ -615,10 +666,13 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* 
   const uint64_t waves = (n + kLeavesPerWave - 1) / kLeavesPerWave;
   hipLaunchKernelGGL(kryo_twrite_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, items, n, off, item_slot,
                      k.slot_map, k.arena, out, cap, status);
+  if (templates_only) return hipGetLastError();
   hipLaunchKernelGGL(kryo_dwrite_kernel, dim3((uint32_t)std::max<uint64_t>(1, dwriters / 256)), dim3(256), 0, s, items,
                      direct, k.counters, off, out, cap, status, dws);
   return hipGetLastError();
 }
+
+hipError_t kryo_set_priority(uint32_t on) { return hipMemcpyToSymbol(HIP_SYMBOL(g_kryo_prio), &on, 4); }
 
 hipError_t kryo_scan_bytes(size_t& bytes, uint64_t n1, hipStream_t s) {
   bytes = 0;

@@ -39,20 +39,29 @@ hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uin
 hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
                               hipStream_t s);
 hipError_t launch_store_to_host(const void* src, void* dst, uint64_t n, hipStream_t s);
+hipError_t tx_set_id_priority(uint32_t on);  // the id kernels' raised wave priority (current device)
+hipError_t kryo_set_priority(uint32_t on);   // the same for the Kryo encoder's kernels
 // kryo_device.hip: the GPU Kryo leaf encoder (shapes, templates, sizes, scan, writes)
 size_t kryo_fixed_scratch_bytes();                     // shape table, records, templates (persistent per device)
 size_t kryo_direct_ws_bytes(uint64_t writers);         // the direct encoder's level buffers
 hipError_t kryo_scan_bytes(size_t& bytes, uint64_t n1, hipStream_t s);
 hipError_t kryo_clear(uint8_t* fixed, hipStream_t s);  // empty the shape table (and the template arena)
-const uint32_t* kryo_usage_src(uint8_t* fixed);        // device: [templates in the arena, table slots in use]
+// device: [templates in the arena, table slots in use, misses since kryo_reset_misses, 0]
+const uint32_t* kryo_usage_src(uint8_t* fixed);
+constexpr size_t kKryoUsageBytes = 16;
+hipError_t kryo_reset_misses(uint8_t* fixed, hipStream_t s);
 uint32_t kryo_clear_threshold_slots();
 uint32_t kryo_clear_threshold_templates();
-// data_base != nullptr: items' `data` are offsets into data_len bytes at data_base
+// data_base != nullptr: items' `data` are offsets into data_len bytes at data_base.
+// templates_only: the steady-state chain -- no new shapes built, no direct encoder;
+// an item that would need either is a miss (counted, its leaf not written, status
+// kKryoMiss) and the caller redoes the batch with templates_only false.
+constexpr uint8_t kKryoMiss = 4;
 hipError_t launch_kryo_encode(const cordahip_kryo_item* items, const uint8_t* data_base, uint64_t data_len,
                               uint64_t n, uint32_t group, uint8_t* fixed,
                               uint32_t* item_slot, uint32_t* direct, uint64_t* sizes, uint64_t* off, uint8_t* out,
                               uint64_t cap, uint8_t* status, uint8_t* dws, uint64_t dwriters, void* scan_temp,
-                              size_t scan_bytes, hipStream_t s);
+                              size_t scan_bytes, hipStream_t s, bool templates_only = false);
 hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s);
 hipError_t launch_comp_check(const uint8_t* item_status, const uint64_t* tx_item_off, uint64_t ntx, uint8_t* tx_status,
                              hipStream_t s);
@@ -239,6 +248,7 @@ struct Device {
   // allocated, cleared when a call reports it over half full (kryo_usage: a
   // host-mapped copy of its usage counters, stored after each call)
   bool kryo_fresh = false;
+  bool kryo_templates_ok = false;  // the last component batch had no encoder misses (cordahip.cpp)
   uint32_t* kryo_usage = nullptr;
   uint32_t* kryo_usage_dev = nullptr;
   hipEvent_t kryo_ev = nullptr;

@@ -21,6 +21,22 @@
 
 namespace cordahip {
 
+// The transaction-id kernels run at raised wave priority (s_setprio 3): beside
+// the Ed25519 ladders of a signed-tx batch they are the id slices' critical
+// path -- a signature chunk's prep waits for its slice's ids -- and at equal
+// priority the ladder waves took most of the issue slots (a 2^16-signature
+// slice's SHA-256 0.46-0.51 ms beside a ladder against 0.13 ms alone,
+// profiles/r05_c4h_components_timeline_skiprare_ab.txt). Total work is
+// unchanged; the ladders take the slots the id waves leave. 0: off
+// (CORDAHIP_ID_PRIO=0, tx_set_id_priority).
+__device__ uint32_t g_id_prio = 1;
+
+__device__ inline void id_priority() {
+  if (g_id_prio) __builtin_amdgcn_s_setprio(3);
+}
+
+hipError_t tx_set_id_priority(uint32_t on) { return hipMemcpyToSymbol(HIP_SYMBOL(g_id_prio), &on, 4); }
+
 // tx-level statuses beyond the lane statuses (include/cordahip.h)
 static constexpr uint8_t kTxNoLeaves = 6;      // MerkleTreeException
 static constexpr uint8_t kTxNoSignatures = 7;  // SignedTransaction init: require(sigs.isNotEmpty())
@@ -52,6 +68,7 @@ CDEV void sha256_node(uint32_t out[8], const uint32_t a[8], const uint32_t b[8])
 __global__ void __launch_bounds__(256) sha256_leaves_kernel(const uint8_t* __restrict__ bytes,
                                                            const uint64_t* __restrict__ off, uint64_t nleaves,
                                                            uint32_t* __restrict__ hashes /* [nleaves][8] BE words */) {
+  id_priority();
   __shared__ unsigned int cnt[9], order[256];
   const uint64_t mine = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (threadIdx.x < 9) cnt[threadIdx.x] = 0;
@@ -91,6 +108,7 @@ __global__ void __launch_bounds__(256) sha256_leaves_kernel(const uint8_t* __res
 __global__ void __launch_bounds__(256) merkle_root_kernel(uint32_t* __restrict__ hashes,
                                                          const uint64_t* __restrict__ tx_leaf_off, uint64_t ntx,
                                                          uint8_t* __restrict__ txid, uint8_t* __restrict__ tx_status) {
+  id_priority();
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntx) return;
   const uint64_t lo = tx_leaf_off[t], hi = tx_leaf_off[t + 1];

@@ -188,3 +188,49 @@ def test_cash_issue_corpus_many_slices(engine, oracle, chunk):
     assert [res[0][t].tobytes() for t in range(0, ntx, 997)] == ids
     assert (res[1] == 0).sum() == ntx - len(range(3, ntx, 10))
     _compare(engine, leaves, res, sigs)
+
+
+def test_templates_only_chain_and_its_redo(engine, oracle):
+    """Once a device's component batches stop needing new templates and the direct
+    encoder, the next batch runs the templates-only chain (no build / size / direct-write
+    kernels); a batch that then brings new shapes (strings of lengths not seen before)
+    and direct items (a 70,000-character string, beyond a template) misses and is run
+    again with the full chain. Every call's outputs equal the leaf path's."""
+    rng = np.random.default_rng(54)
+    ntx = 3000
+    blob, items, _ = cash_issue_items(rng.integers(0, 256, (ntx, 32), dtype=np.uint8),
+                                      rng.integers(0, 256, (ntx, 32), dtype=np.uint8), bytes(range(32)),
+                                      rng.integers(1, 10**9, ntx), rng.integers(-2**63, 2**63 - 1, ntx))
+    it = items.reshape(-1).copy()
+    host_it = it.copy()
+    host_it["data"] += np.uint64(blob.ctypes.data)
+    hb, ho = _lib.kryo_encode_array(host_it)
+    cash_leaves = [[hb[int(ho[5 * t + j]):int(ho[5 * t + j + 1])].tobytes() for j in range(5)] for t in range(ntx)]
+    ids_l, _ = engine.tx_ids(cash_leaves)
+    cash_sigs = [[(ED,) + _sign(oracle, hashlib.sha256(b"tpl%d" % t).digest(), ids_l[t].tobytes())]
+                 for t in range(ntx)]
+    cash_sigs[17] = [(ED, cash_sigs[17][0][1], bytes(64))]
+    tio = np.arange(0, 5 * ntx + 1, 5, dtype=np.uint64)
+
+    def cash_call():
+        res = engine.signed_txcomp_verify_arrays(blob, it, tio, cash_sigs)
+        _compare(engine, cash_leaves, res, cash_sigs)
+        assert res[1][17] == 1 and (res[1] == 0).sum() == ntx - 1
+
+    for _ in range(3):  # the shapes built, then calls without misses: templates-only from here
+        cash_call()
+    r = random.Random(54)
+    lens = r.sample(range(1500, 3000), 40)
+    txs = [[("String", "".join(chr(97 + r.randrange(26)) for _ in range(n)), 0), ("int", r.randrange(2**31), 0)]
+           for n in lens]
+    txs[7].append(("String", "w" * 70_000, 0))
+    leaves = [[K.leaf(k, v, c) for k, v, c in tx] for tx in txs]
+    ids = [_oracle_id(oracle, lv) for lv in leaves]
+    sigs = [[(ED,) + _sign(oracle, hashlib.sha256(b"new%d" % t).digest(), ids[t])] for t in range(len(txs))]
+    for _ in range(2):  # misses (redone); then the full chain again (direct items every time)
+        res = engine.signed_txcomp_verify(txs, sigs)
+        assert [res[0][t].tobytes() for t in range(len(txs))] == ids
+        assert (res[1] == 0).all()
+        _compare(engine, leaves, res, sigs)
+    for _ in range(3):
+        cash_call()
