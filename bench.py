@@ -480,8 +480,8 @@ class C4:
                        "device_encode": self.device_encode}
         if self.device_encode:
             self.kernel = "kryo_size + scan + kryo_write + " + C4.kernel
-            # the encoder's L2-to-fabric bytes per tx (tools/gpu_pmc_kryo2.sh -> pmc_kryo_traffic.py)
-            self.extra_pmc = ("r04_pmc_kryo_traffic.json", ntx)
+            # the encoder's L2-to-fabric bytes per tx (tools/gpu_r5n.sh -> pmc_kryo_traffic.py)
+            self.extra_pmc = ("r05_pmc_kryo_traffic.json", ntx)
             self.config["component_bytes_per_tx"] = round(self.d_blob.numel() / ntx, 1)
         if not self.native:
             self.config["leaf_lens"] = list(C4_LEAF_LENS)

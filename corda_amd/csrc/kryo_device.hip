@@ -108,28 +108,37 @@ struct ItemSrc {
   }
 };
 
-// Thread j's item when the batch is records of `group` items (a transaction's
-// components): kind-major within tiles of 64 records, so each wave takes one
-// kind (the shape walk does not diverge) while the waves of a tile read the
-// same 64 records' items and payload together. (r05's first mapping was
-// kind-major over the whole batch: every record's lines were fetched once per
-// kind, 5.1 KB of L2-fabric reads per cash-issue transaction in kryo_shape,
-// profiles/r05_pmc_kryo_traffic.json.) Threads past the last record: n.
 // the encoder's kernels run at the id kernels' raised wave priority (tx.hip g_id_prio)
 __device__ uint32_t g_kryo_prio = 1;
 __device__ inline void kryo_priority() {
   if (g_kryo_prio) __builtin_amdgcn_s_setprio(3);
 }
 
+// Thread j's item when the batch is records of `group` items (a transaction's
+// components): kind-major within tiles of 64 records, one tile per block of
+// 64 x group threads, so each wave takes one kind (the shape walk does not
+// diverge) while one CU reads the tile's items and payload. (r05's first
+// mapping was kind-major over the whole batch: every record's lines were
+// fetched once per kind, 5.1 KB of L2-fabric reads per cash-issue
+// transaction; tiles of 256-thread blocks split a record's kinds over two
+// XCDs' L2s; profiles/r05_pmc_kryo_*.) Threads past the last record: n.
 __device__ inline uint64_t item_of(uint64_t j, uint64_t n, uint32_t group) {
   if (group <= 1 || n % group) return j;
   const uint64_t tile = j / (64ull * group), r = j % (64ull * group), rec = tile * 64 + r % 64;
   return rec < n / group ? rec * group + r / 64 : n;
 }
-// threads the shape pass launches for n items (whole tiles of 64 records)
+inline bool grouped(uint64_t n, uint32_t group) { return group > 1 && group <= 16 && n % group == 0; }
+// the shape pass's block size and threads for n items (whole tiles of 64 records)
+inline uint32_t shape_block(uint64_t n, uint32_t group) { return grouped(n, group) ? 64 * group : 256; }
 inline uint64_t item_threads(uint64_t n, uint32_t group) {
-  if (group <= 1 || n % group) return n;
+  if (!grouped(n, group)) return n;
   return (n / group + 63) / 64 * 64 * group;
+}
+
+// one atomic add per wave for the lanes (of those active) where pred holds
+__device__ inline void wave_count(uint32_t* p, bool pred) {
+  const uint64_t b = __ballot(pred);
+  if (pred && (uint32_t)__lane_id() == (uint32_t)(__ffsll((unsigned long long)b) - 1)) atomicAdd(p, (uint32_t)__popcll(b));
 }
 
 // ---- 1. shapes ------------------------------------------------------------------
@@ -138,7 +147,6 @@ inline uint64_t item_threads(uint64_t n, uint32_t group) {
 // (slot_size still kUnbuilt) is compared after kryo_build, in kryo_tsize.
 __device__ inline void direct_item(uint32_t* direct, uint32_t* counters, uint64_t i) {
   direct[atomicAdd(&counters[kCDirect], 1u)] = (uint32_t)i;  // sized by kryo_dsize
-  atomicAdd(&counters[kCMiss], 1u);
 }
 
 // the size and status of an item of slot `slot` (built): false when it goes to the direct encoder
@@ -150,16 +158,42 @@ __device__ inline bool template_item(const cordahip_kryo_item& it, const kryo::S
   return true;
 }
 
+// The slot of shape hash h: found (its tag), claimed (an empty slot, CAS), or
+// kNoSlot (no room within kMaxProbe probes; templates_only: not in the table).
+// The probes are agent-scope loads (another XCD may claim a slot during the
+// kernel), which the L2 does not keep: one per wave per distinct hash, not one
+// per item (r05: 5 x 128 B of fabric reads per cash-issue transaction).
+__device__ inline uint32_t probe_slot(unsigned long long* table, uint64_t h, uint64_t i, bool templates_only,
+                                      bool& claimed) {
+  const uint32_t tag = (uint32_t)(h >> 32);
+  const unsigned long long mine = ((unsigned long long)tag << 32) | (unsigned long long)(i + 1);
+  uint32_t k = (uint32_t)h & (kSlots - 1);
+  claimed = false;
+  for (uint32_t probe = 0; probe < kMaxProbe; probe++, k = (k + 1) & (kSlots - 1)) {
+    unsigned long long v = __hip_atomic_load(&table[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == 0 && templates_only) return kNoSlot;  // an unknown shape: a miss
+    if (v == 0) {
+      v = atomicCAS(&table[k], 0ull, mine);
+      if (v == 0) {  // claimed: this item represents a new shape
+        claimed = true;
+        return k;
+      }
+    }
+    if ((uint32_t)(v >> 32) == tag) return k;
+  }
+  return kNoSlot;
+}
+
 // templates_only: no slot is claimed and nothing goes to the direct encoder; an
 // item without a built template of its shape is a miss (kKryoMiss, size 0,
 // item_slot kNoSlot: kryo_twrite does not write it).
-__global__ void __launch_bounds__(256) kryo_shape_kernel(ItemSrc items, uint64_t n, uint32_t group, bool templates_only,
-                                                         unsigned long long* __restrict__ table,
-                                                         const int32_t* __restrict__ slot_size,
-                                                         const kryo::ShapeRec* __restrict__ rec,
-                                                         uint32_t* __restrict__ item_slot, uint32_t* __restrict__ shape_list,
-                                                         uint64_t* __restrict__ sizes, uint8_t* __restrict__ status,
-                                                         uint32_t* __restrict__ direct, uint32_t* __restrict__ counters) {
+__global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_t n, uint32_t group, bool templates_only,
+                                                          unsigned long long* __restrict__ table,
+                                                          const int32_t* __restrict__ slot_size,
+                                                          const kryo::ShapeRec* __restrict__ rec,
+                                                          uint32_t* __restrict__ item_slot, uint32_t* __restrict__ shape_list,
+                                                          uint64_t* __restrict__ sizes, uint8_t* __restrict__ status,
+                                                          uint32_t* __restrict__ direct, uint32_t* __restrict__ counters) {
   kryo_priority();
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j == 0) sizes[n] = 0;  // the scan's last element: off[n] = the total
@@ -177,44 +211,39 @@ __global__ void __launch_bounds__(256) kryo_shape_kernel(ItemSrc items, uint64_t
     return;
   }
   uint64_t h = 0;
+  const bool hashed = kryo::shape_hash_of(it, h);
+  // the first hashed lane probes for every lane of its hash; other hashes probe alone
+  const uint64_t hb = __ballot(hashed);
+  const int lead = hb ? __ffsll((unsigned long long)hb) - 1 : 0;
+  const uint64_t h0 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(h >> 32), lead) << 32) |
+                      (uint32_t)__shfl((int)(uint32_t)h, lead);
+  const bool follower = hashed && h == h0 && (int)__lane_id() != lead;
   uint32_t slot = kNoSlot;
   bool claimed = false;
-  if (kryo::shape_hash_of(it, h)) {
-    const uint32_t tag = (uint32_t)(h >> 32);
-    const unsigned long long mine = ((unsigned long long)tag << 32) | (unsigned long long)(i + 1);
-    uint32_t k = (uint32_t)h & (kSlots - 1);
-    for (uint32_t probe = 0; probe < kMaxProbe; probe++, k = (k + 1) & (kSlots - 1)) {
-      unsigned long long v = __hip_atomic_load(&table[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (v == 0 && templates_only) break;  // an unknown shape: a miss
-      if (v == 0) {
-        v = atomicCAS(&table[k], 0ull, mine);
-        if (v == 0) {  // claimed: this item represents a new shape
-          slot = k;
-          claimed = true;
-          shape_list[atomicAdd(&counters[kCNew], 1u)] = k;
-          atomicAdd(&counters[kCUsed], 1u);
-          break;
-        }
-      }
-      if ((uint32_t)(v >> 32) == tag) {
-        slot = k;
-        break;
-      }
-    }
+  if (hashed && !follower) slot = probe_slot(table, h, i, templates_only, claimed);
+  const uint32_t lead_slot = (uint32_t)__shfl((int)slot, lead);
+  if (follower) slot = lead_slot;  // claimed by the leader: slot_size is kUnbuilt, deferred below
+  if (claimed) {
+    shape_list[atomicAdd(&counters[kCNew], 1u)] = slot;
+    atomicAdd(&counters[kCUsed], 1u);
   }
+  bool deferred = false;
   if (slot != kNoSlot) {
     const int32_t z = claimed ? kUnbuilt : slot_size[slot];
     if (z == kUnbuilt && !templates_only) {  // built after this kernel: compared in kryo_tsize
-      atomicAdd(&counters[kCMiss], 1u);
-      item_slot[i] = slot | kDefer;
-      return;
+      deferred = true;
+    } else if (z == kUnbuilt || !template_item(it, rec[slot], z, size, st)) {
+      slot = kNoSlot;
     }
-    if (z == kUnbuilt || !template_item(it, rec[slot], z, size, st)) slot = kNoSlot;
+  }
+  wave_count(&counters[kCMiss], deferred || slot == kNoSlot);
+  if (deferred) {
+    item_slot[i] = slot | kDefer;
+    return;
   }
   item_slot[i] = slot;
   if (slot == kNoSlot) {
     if (templates_only) {
-      atomicAdd(&counters[kCMiss], 1u);
       size = 0;
       st = kKryoMiss;
     } else {
@@ -644,8 +673,9 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* 
     e = e ? e : hipMemsetAsync(off, 0, 8, s);
     return e;
   }
-  hipLaunchKernelGGL(kryo_shape_kernel, dim3((uint32_t)((item_threads(n, group) + 255) / 256)), dim3(256), 0, s, items,
-                     n, group, templates_only, k.table, k.slot_size, k.rec, item_slot, k.shape_list, sizes, status,
+  const uint32_t sb = shape_block(n, group), g = grouped(n, group) ? group : 1;
+  hipLaunchKernelGGL(kryo_shape_kernel, dim3((uint32_t)((item_threads(n, group) + sb - 1) / sb)), dim3(sb), 0, s, items,
+                     n, g, templates_only, k.table, k.slot_size, k.rec, item_slot, k.shape_list, sizes, status,
                      direct, k.counters);
   // build, tsize, dsize (and dwrite) serve new shapes and direct items; in steady
   // state they find nothing to do, yet beside the Ed25519 ladders of a component

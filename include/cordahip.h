@@ -403,8 +403,12 @@ int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_ite
  * (MerkleTransaction.kt:51-62) and the GPU writes the leaf preimages
  * (serializedHash, MerkleTransaction.kt:16-18; the encoder of
  * cordahip_kryo_encode_device) ahead of K3 / K4, so tx ids need no JVM
- * re-serialisation and PCIe carries the components (~600 B per cash-issue
- * transaction) instead of the leaves (1,717 B). Replaces the same reference
+ * re-serialisation and PCIe carries the components (~540 B per cash-issue
+ * transaction: 160 B of items, 379 B of payload) instead of the leaves
+ * (1,717 B). Once a device's component batches need no new template and no
+ * direct encoder, it runs a templates-only encoder chain; a call that then
+ * meets a new shape runs again with the full chain before it returns (same
+ * outputs, about twice the time for that call). Replaces the same reference
  * calls as cordahip_tx_submit: SignedTransaction.checkSignaturesAreValid
  * (SignedTransaction.kt:95-100) + the id of verifySignatures (:70-85,
  * WireTransaction.kt:48).
