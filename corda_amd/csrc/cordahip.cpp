@@ -578,18 +578,18 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
                                     w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
       });
     }
+    // the ids, and in the same launch: a component the encoder rejected (no id for its
+    // transaction, CORDAHIP_TX_BAD_COMPONENT) and the stores into pinned caller arrays
+    // through their device mapping (three launches per slice before r05)
+    const uint8_t* st_base =
+        cp ? reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(w.comp_status.p) - l0) : nullptr;
+    const bool mapped = ts1 > ts0 && map_txid && map_status;
     e = e ? e : launch_merkle_root(hash_base, w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), ts1 - ts0,
-                                   w.txid.as<uint8_t>() + (ts0 - t0) * 32, w.tx_status.as<uint8_t>() + (ts0 - t0), s);
-    if (cp) {  // a component the encoder rejected: no id for its transaction
-      const uint8_t* st_base =
-          reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(w.comp_status.p) - l0);
-      e = e ? e : launch_comp_check(st_base, w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), ts1 - ts0,
-                                    w.tx_status.as<uint8_t>() + (ts0 - t0), s);
-    }
+                                   w.txid.as<uint8_t>() + (ts0 - t0) * 32, w.tx_status.as<uint8_t>() + (ts0 - t0), s,
+                                   st_base, mapped ? map_txid + ts0 * 32 : nullptr, mapped ? map_status + ts0 : nullptr);
     e = e ? e : hipEventRecord(kev[j], s);  // the slice's ids are in HBM: its signatures may gather them
-    if (ts1 > ts0 && map_txid && map_status) {  // pinned caller arrays: stored by a kernel
-      e = e ? e : launch_store_to_host(w.txid.as<uint8_t>() + (ts0 - t0) * 32, map_txid + ts0 * 32, (ts1 - ts0) * 32, s);
-      e = e ? e : launch_store_to_host(w.tx_status.as<uint8_t>() + (ts0 - t0), map_status + ts0, ts1 - ts0, s);
+    if (mapped) {
+      // stored by merkle_root
     } else if (ts1 > ts0) {
       e = e ? e : blocked("ids D2H", [&] {
         return hipMemcpyAsync(b->txid + ts0 * 32, w.txid.as<uint8_t>() + (ts0 - t0) * 32, (ts1 - ts0) * 32, d2h, s);

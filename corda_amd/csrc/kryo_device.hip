@@ -227,12 +227,32 @@ __global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_
     shape_list[atomicAdd(&counters[kCNew], 1u)] = slot;
     atomicAdd(&counters[kCUsed], 1u);
   }
+  // a wave whose items all have one slot (the common case: one kind per wave) compares
+  // them with a copy of the record in LDS instead of 64 lanes re-reading it through the L2
+  __shared__ kryo::ShapeRec srec[16];
+  const uint64_t act = __ballot(true);
+  const uint32_t s0 = (uint32_t)__shfl((int)slot, __ffsll((unsigned long long)act) - 1);
+  const bool uni = s0 != kNoSlot && __ballot(slot == s0) == act;
+  const kryo::ShapeRec* rp = rec + (slot == kNoSlot ? 0 : slot);
+  if (uni) {
+    kryo::ShapeRec* mine = &srec[threadIdx.x >> 6];
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
+    const uint32_t nact = (uint32_t)__popcll(act);
+    constexpr uint32_t kQ = sizeof(kryo::ShapeRec) / 16;
+    static_assert(sizeof(kryo::ShapeRec) % 16 == 0, "ShapeRec in uint4s");
+    for (uint32_t q = rank; q < kQ; q += nact)
+      reinterpret_cast<uint4*>(mine)[q] = reinterpret_cast<const uint4*>(rec + s0)[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    rp = mine;
+  }
   bool deferred = false;
   if (slot != kNoSlot) {
     const int32_t z = claimed ? kUnbuilt : slot_size[slot];
     if (z == kUnbuilt && !templates_only) {  // built after this kernel: compared in kryo_tsize
       deferred = true;
-    } else if (z == kUnbuilt || !template_item(it, rec[slot], z, size, st)) {
+    } else if (z == kUnbuilt || !template_item(it, *rp, z, size, st)) {
       slot = kNoSlot;
     }
   }
@@ -668,7 +688,9 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* 
                               bool templates_only) {
   const ItemSrc items{d_items, data_base, data_len};
   const KryoState k(fixed);
-  hipError_t e = hipMemsetAsync(k.counters, 0, 8, s);  // kCNew, kCDirect
+  // kCNew, kCDirect (the templates-only chain neither claims nor lists: no reset, one
+  // launch less per id slice)
+  hipError_t e = templates_only ? hipSuccess : hipMemsetAsync(k.counters, 0, 8, s);
   if (e || n == 0) {
     e = e ? e : hipMemsetAsync(off, 0, 8, s);
     return e;

@@ -35,7 +35,8 @@ hipError_t launch_ed25519_sign(const uint8_t* seeds, const uint8_t* msgs, uint32
 hipError_t launch_sha256_leaves(const uint8_t* bytes, const uint64_t* off, uint64_t nleaves, uint32_t* hashes,
                                 hipStream_t s);
 hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uint64_t ntx, uint8_t* txid,
-                              uint8_t* tx_status, hipStream_t s);
+                              uint8_t* tx_status, hipStream_t s, const uint8_t* item_status = nullptr,
+                              uint8_t* map_txid = nullptr, uint8_t* map_status = nullptr);
 hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
                               hipStream_t s);
 hipError_t launch_store_to_host(const void* src, void* dst, uint64_t n, hipStream_t s);
@@ -63,8 +64,6 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* items, const uint8_t* da
                               uint64_t cap, uint8_t* status, uint8_t* dws, uint64_t dwriters, void* scan_temp,
                               size_t scan_bytes, hipStream_t s, bool templates_only = false);
 hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s);
-hipError_t launch_comp_check(const uint8_t* item_status, const uint64_t* tx_item_off, uint64_t ntx, uint8_t* tx_status,
-                             hipStream_t s);
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
                             uint8_t* tx_status, hipStream_t s);
 hipError_t launch_pmt_verify(const uint32_t* leaf_hashes, const uint64_t* tx_leaf_off, const uint8_t* tok,

@@ -39,6 +39,7 @@ hipError_t tx_set_id_priority(uint32_t on) { return hipMemcpyToSymbol(HIP_SYMBOL
 
 // tx-level statuses beyond the lane statuses (include/cordahip.h)
 static constexpr uint8_t kTxNoLeaves = 6;      // MerkleTreeException
+static constexpr uint8_t kTxBadComponent = 9;  // a component the encoder rejected (cordahip.h)
 static constexpr uint8_t kTxNoSignatures = 7;  // SignedTransaction init: require(sigs.isNotEmpty())
 
 // SHA-256(a || b) for two 32-byte digests (state words, big-endian): the
@@ -105,20 +106,52 @@ __global__ void __launch_bounds__(256) sha256_leaves_kernel(const uint8_t* __res
 // Level j holds m_j real nodes; positions >= m_j are the padding constant
 // Z_j (Z_0 = zeroHash, Z_{j+1} = H(Z_j, Z_j)), exactly the padded tree of
 // MerkleTree.kt:33-66.
+//
+// Optional, for the pipelined signed-tx slices (one launch instead of three):
+// item_status != nullptr -- component batches: a tx with a component the
+// encoder rejected gets kTxBadComponent (item_status is indexed like hashes,
+// by absolute leaf index); map_txid / map_status != nullptr -- the id and
+// status also go to the caller's pinned arrays through their device mapping.
+CDEV void merkle_emit(uint64_t t, const uint32_t root[8], uint8_t st, uint8_t* __restrict__ txid,
+                      uint8_t* __restrict__ tx_status, uint8_t* __restrict__ map_txid, uint8_t* __restrict__ map_status) {
+  const uint4 r0 = make_uint4(bswap32(root[0]), bswap32(root[1]), bswap32(root[2]), bswap32(root[3]));
+  const uint4 r1 = make_uint4(bswap32(root[4]), bswap32(root[5]), bswap32(root[6]), bswap32(root[7]));
+  uint4* o = reinterpret_cast<uint4*>(txid + t * 32);
+  o[0] = r0;
+  o[1] = r1;
+  if (tx_status) tx_status[t] = st;
+  if (map_txid) {
+    uint8_t* d = map_txid + t * 32;
+    if (((uintptr_t)d & 15) == 0) {
+      reinterpret_cast<uint4*>(d)[0] = r0;
+      reinterpret_cast<uint4*>(d)[1] = r1;
+    } else {
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(o);
+      for (int i = 0; i < 32; i++) d[i] = b[i];
+    }
+  }
+  if (map_status) map_status[t] = st;
+}
+
 __global__ void __launch_bounds__(256) merkle_root_kernel(uint32_t* __restrict__ hashes,
                                                          const uint64_t* __restrict__ tx_leaf_off, uint64_t ntx,
-                                                         uint8_t* __restrict__ txid, uint8_t* __restrict__ tx_status) {
+                                                         uint8_t* __restrict__ txid, uint8_t* __restrict__ tx_status,
+                                                         const uint8_t* __restrict__ item_status,
+                                                         uint8_t* __restrict__ map_txid, uint8_t* __restrict__ map_status) {
   id_priority();
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntx) return;
   const uint64_t lo = tx_leaf_off[t], hi = tx_leaf_off[t + 1];
   uint64_t m = hi - lo;
   if (m == 0) {
-    if (tx_status) tx_status[t] = kTxNoLeaves;
-#pragma unroll
-    for (int i = 0; i < 32; i++) txid[t * 32 + i] = 0;
+    const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    merkle_emit(t, zero, kTxNoLeaves, txid, tx_status, map_txid, map_status);
     return;
   }
+  uint8_t st = kStatusOk;
+  if (item_status)
+    for (uint64_t i = lo; i < hi; i++)
+      if (item_status[i] != 0) st = kTxBadComponent;
   uint32_t* v = hashes + lo * 8;
   uint32_t z[8];  // Z_zlevel
 #pragma unroll
@@ -154,12 +187,10 @@ __global__ void __launch_bounds__(256) merkle_root_kernel(uint32_t* __restrict__
     m = half;
   }
   // root = v[0]; emit big-endian bytes (SecureHash byte order)
-  uint4* o = reinterpret_cast<uint4*>(txid + t * 32);
   const uint4* pv = reinterpret_cast<const uint4*>(v);
   const uint4 r0 = pv[0], r1 = pv[1];
-  o[0] = make_uint4(bswap32(r0.x), bswap32(r0.y), bswap32(r0.z), bswap32(r0.w));
-  o[1] = make_uint4(bswap32(r1.x), bswap32(r1.y), bswap32(r1.z), bswap32(r1.w));
-  if (tx_status) tx_status[t] = kStatusOk;
+  const uint32_t root[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+  merkle_emit(t, root, st, txid, tx_status, map_txid, map_status);
 }
 
 // gather: msgs[s] = txid[sig_tx[s]] (each signature signs its tx id, SignedTransaction.kt:98)
@@ -239,22 +270,6 @@ __global__ void __launch_bounds__(256) tx_reduce_kernel(const uint8_t* __restric
   tx_status[t] = st;
 }
 
-// Component-level tx batches: a transaction with a component the Kryo encoder
-// rejected (item status != 0: invalid, or beyond the slice's leaf buffer) has
-// no id -- CORDAHIP_TX_BAD_COMPONENT (after merkle_root wrote its status).
-// item_status is indexed by absolute item number (a shifted base pointer).
-static constexpr uint8_t kTxBadComponent = 9;
-__global__ void __launch_bounds__(256) comp_check_kernel(const uint8_t* __restrict__ item_status,
-                                                        const uint64_t* __restrict__ tx_item_off, uint64_t ntx,
-                                                        uint8_t* __restrict__ tx_status) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntx) return;
-  for (uint64_t i = tx_item_off[t]; i < tx_item_off[t + 1]; i++)
-    if (item_status[i] != 0) {
-      tx_status[t] = kTxBadComponent;
-      return;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // K6: FilteredTransaction.verify (MerkleTransaction.kt:134-140) ->
@@ -373,10 +388,11 @@ hipError_t launch_sha256_leaves(const uint8_t* bytes, const uint64_t* off, uint6
   return hipGetLastError();
 }
 hipError_t launch_merkle_root(uint32_t* hashes, const uint64_t* tx_leaf_off, uint64_t ntx, uint8_t* txid,
-                              uint8_t* tx_status, hipStream_t s) {
+                              uint8_t* tx_status, hipStream_t s, const uint8_t* item_status, uint8_t* map_txid,
+                              uint8_t* map_status) {
   if (!ntx) return hipSuccess;
   hipLaunchKernelGGL(merkle_root_kernel, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, s, hashes, tx_leaf_off,
-                     ntx, txid, tx_status);
+                     ntx, txid, tx_status, item_status, map_txid, map_status);
   return hipGetLastError();
 }
 hipError_t launch_gather_txid(const uint8_t* txid, const uint64_t* tx_sig_off, uint64_t ntx, uint8_t* msgs,
@@ -397,13 +413,6 @@ hipError_t launch_store_to_host(const void* src, void* dst, uint64_t n, hipStrea
 hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(gather_rows32_kernel, dim3((uint32_t)((2 * n + 255) / 256)), dim3(256), 0, s, txid, idx, n, rows);
-  return hipGetLastError();
-}
-hipError_t launch_comp_check(const uint8_t* item_status, const uint64_t* tx_item_off, uint64_t ntx, uint8_t* tx_status,
-                             hipStream_t s) {
-  if (!ntx) return hipSuccess;
-  hipLaunchKernelGGL(comp_check_kernel, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, s, item_status, tx_item_off,
-                     ntx, tx_status);
   return hipGetLastError();
 }
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
