@@ -173,15 +173,25 @@ class Engine:
             tio[1:] = np.cumsum([len(tx) for tx in txs], dtype=np.uint64)
         return self.signed_txcomp_verify_arrays(np.ascontiguousarray(blob), items, tio, sigs, async_=async_)
 
-    def signed_txcomp_verify_arrays(self, payload, items, tx_item_off, sigs, async_: bool = False):
+    def signed_txcomp_verify_arrays(self, payload, items, tx_item_off, sigs, async_: bool = False,
+                                    pinned_out: bool = False):
         """The array form: payload uint8, items KRYO_ITEM_DTYPE whose `data` are offsets into payload,
-        tx_item_off uint64[ntx + 1]; sigs[t] = [(scheme, key, sig), ...]."""
+        tx_item_off uint64[ntx + 1]; sigs[t] = [(scheme, key, sig), ...]. pinned_out: txid and
+        tx_status in page-locked memory (the library's kernels then store them through their
+        device mapping, as for a JVM's pinned direct buffers)."""
         n = len(tx_item_off) - 1
         payload = np.ascontiguousarray(payload, dtype=np.uint8)
         items = np.ascontiguousarray(items)
         tio = np.ascontiguousarray(tx_item_off, dtype=np.uint64)
-        txid = np.zeros((max(n, 1), 32), dtype=np.uint8)
-        st = np.zeros(max(n, 1), dtype=np.uint8)
+        pins = ()
+        if pinned_out:
+            import torch
+            pins = (torch.zeros((max(n, 1), 32), dtype=torch.uint8).pin_memory(),
+                    torch.zeros(max(n, 1), dtype=torch.uint8).pin_memory())
+            txid, st = pins[0].numpy(), pins[1].numpy()
+        else:
+            txid = np.zeros((max(n, 1), 32), dtype=np.uint8)
+            st = np.zeros(max(n, 1), dtype=np.uint8)
         tb = TxcompBatch(n, _ptr(items) if len(items) else None, _ptr(tio), _ptr(payload) if payload.size else None,
                          payload.size, _ptr(txid), _ptr(st))
         flat = [x for per in sigs for x in per]
@@ -196,7 +206,7 @@ class Engine:
         sbatch = SignedTxcompBatch(tb, _ptr(so), _ptr(sch), _ptr(kb), _ptr(ko), _ptr(sb), _ptr(sgo), _ptr(sst),
                                    _ptr(fb))
         res = lambda: (txid[:n], st[:n], fb[:n], sst[:len(flat)])  # noqa: E731
-        keep = (payload, items, tio, txid, st, so, sch, kb, ko, sb, sgo, sst, fb, tb, sbatch)
+        keep = (payload, items, tio, txid, st, so, sch, kb, ko, sb, sgo, sst, fb, tb, sbatch, pins)
         if async_:
             t = ctypes.c_uint64()
             check(lib().cordahip_txcomp_submit(self._ctx, ctypes.byref(sbatch), ctypes.byref(t)),

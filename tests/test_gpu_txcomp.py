@@ -133,15 +133,18 @@ def test_bad_components(engine, oracle):
     assert list(st) == [0, _lib.TX_BAD_COMPONENT, 0, _lib.TX_BAD_COMPONENT, 0]
     assert list(fb) == [-1] * 5 and list(sst) == [0, 9, 0, 9, 0]
     assert ids[0].tobytes() == tid and ids[4].tobytes() == tid
-    # a payload offset past the end of the payload
+    # a payload offset past the end of the payload; the outputs in pageable, then in pinned
+    # memory (merkle_root stores the ids and statuses through the device mapping)
     blob, items, has = _lib.kryo_pack([c for tx in txs[:1] for c in tx])
     items = items.copy()
     items["data"] = np.where(has, items["data"], 0)
-    items2 = np.concatenate([items, items])
+    items2 = np.concatenate([items, items, items])
     items2[4]["data"] = len(blob) - 3  # the second tx's key: 32 bytes from 3 before the end
-    tio = np.array([0, 3, 6], np.uint64)
-    ids, st, fb, sst = engine.signed_txcomp_verify_arrays(blob, items2, tio, sigs[:2])
-    assert list(st) == [0, _lib.TX_BAD_COMPONENT] and ids[0].tobytes() == tid
+    tio = np.array([0, 3, 6, 6, 9], np.uint64)  # the third tx has no components
+    for pinned in (False, True):
+        ids, st, fb, sst = engine.signed_txcomp_verify_arrays(blob, items2, tio, sigs[:4], pinned_out=pinned)
+        assert list(st) == [0, _lib.TX_BAD_COMPONENT, _lib.TX_NO_LEAVES, 0], pinned
+        assert ids[0].tobytes() == tid and ids[3].tobytes() == tid and not ids[2].any()
 
 
 @pytest.mark.parametrize("chunk", [None, "4096"])
@@ -175,7 +178,7 @@ def test_cash_issue_corpus_many_slices(engine, oracle, chunk):
         os.environ["CORDAHIP_TX_SIG_CHUNK"] = chunk
     try:
         res = engine.signed_txcomp_verify_arrays(blob, it, tio, sigs)
-        tk = engine.signed_txcomp_verify_arrays(blob, it, tio, sigs, async_=True)
+        tk = engine.signed_txcomp_verify_arrays(blob, it, tio, sigs, async_=True, pinned_out=True)
         res2 = tk.wait()
     finally:
         if chunk:
