@@ -559,7 +559,20 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
     e = e ? e : hipMemcpyAsync(w.tx_leaf_off.as<uint64_t>() + (ts0 - t0), b->tx_leaf_off + ts0, (ts1 - ts0 + 1) * 8, h2d, sc);
     e = e ? e : hipEventRecord(cev[j], sc);
     e = e ? e : hipStreamWaitEvent(s, cev[j], 0);
-    if (cp) {
+    if (cp && cp->templates_only) {
+      // steady state: shapes, then every leaf's SHA-256 straight from its template
+      // (no leaf bytes in HBM)
+      uint32_t* slots = d.kryo_items.as<uint32_t>();
+      const uint64_t n = ls1 - ls0;
+      const cordahip_kryo_item* it = w.comp_items.as<cordahip_kryo_item>() + (ls0 - l0);
+      uint8_t* cst = w.comp_status.as<uint8_t>() + (ls0 - l0);
+      e = e ? e : launch_kryo_shape(it, w.payload.as<uint8_t>(), cp->c->payload_len, n, cp->group[j],
+                                    d.kryo_fixed.as<uint8_t>(), slots, slots + n, d.kryo_sizes.as<uint64_t>(), cst, s,
+                                    true);
+      e = e ? e : launch_kryo_hash(it, w.payload.as<uint8_t>(), cp->c->payload_len, n, cp->group[j],
+                                   d.kryo_fixed.as<uint8_t>(), slots, d.kryo_sizes.as<uint64_t>(), cst,
+                                   w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
+    } else if (cp) {
       // the slice's leaves on the GPU (the template encoder) into one of two
       // alternating slice buffers, offsets relative to that buffer
       uint8_t* sb = w.leaf_bytes.as<uint8_t>() + (j % 2) * cp->slice_cap;

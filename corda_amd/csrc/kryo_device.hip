@@ -43,6 +43,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "kryo_template.hpp"
+#include "sha2_device.hpp"
 
 namespace cordahip {
 
@@ -638,6 +639,141 @@ __global__ void __launch_bounds__(256) kryo_dwrite_kernel(ItemSrc items, const u
   }
 }
 
+// ---- 7. leaf hashes straight from the templates (the templates-only chain) ---------
+// The component-level signed-tx slices need the leaves only as SHA-256 input:
+// one lane per leaf assembles each 64-byte message block from its template in
+// registers (the same 16-byte pieces kryo_twrite stores: the constant copy for
+// the leaf's own alignment with the descriptor's payload window merged in;
+// pieces of other kinds byte by byte from the symbols) and compresses it, so
+// no leaf is written, scanned or read back (shape -> scan -> twrite ->
+// sha256_leaves was 4 launches and 2 x 2.15 GB of leaf traffic per C4 call).
+// Interleaved on one corpus: c4h --components 77.0 against 74.6 M sig/s with the
+// writes (profiles/r05_fused_hash_ab.json); without the descriptors loaded a
+// block ahead the fused kernel lost (73.3: a descriptor round trip before each
+// block's payload loads).
+// Threads take items as kryo_shape does (a wave = one kind of 64 transactions:
+// equal lengths); a RAW leaf is its item's bytes; an item without a template
+// (a miss, status != 0) gets a zero hash -- its call is redone or its
+// transaction rejected.
+struct HashSrc {
+  uint32_t kind;  // 0 template, 1 RAW, 2 none
+  const uint8_t* tmpl;
+  const uint8_t* data;
+  int64_t value;
+  uint32_t len;
+};
+
+// bytes [16 p, 16 p + 16) of the leaf (len > 16 p), zero past its end, as 4 little-endian
+// words; desc: the piece's descriptor (template leaves; loaded a block ahead by the caller)
+__device__ inline uint64_t piece_desc(const HashSrc& h, uint32_t p) {
+  return h.kind == 0 && 16 * p < h.len ? reinterpret_cast<const uint64_t*>(h.tmpl + kOffDesc)[p + 1] : 0;  // copy 0
+}
+__device__ inline void leaf_piece(const HashSrc& h, uint32_t p, uint64_t desc, uint32_t* v) {
+  const uint32_t lo = 16 * p, last = min(15u, h.len - 1 - lo);
+  if (h.kind == 1) {
+    load_window(h.data + lo, 0, last, v);
+  } else {
+    const uint32_t pm = (uint32_t)desc & 0xffff, kind = (uint32_t)(desc >> 16) & 3;
+    if (kind != kDescBytes) {
+      const uint4 tv = *reinterpret_cast<const uint4*>(h.tmpl + kOffTb + 16 + lo);
+      v[0] = tv.x, v[1] = tv.y, v[2] = tv.z, v[3] = tv.w;
+      if (pm) {
+        uint32_t w[4];
+        load_window(h.data + (int32_t)(desc >> 32), __builtin_ctz(pm), 31 - __builtin_clz(pm), w);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint32_t mk = byte_mask32((pm >> (4 * i)) & 15);
+          v[i] = (v[i] & ~mk) | (w[i] & mk);
+        }
+      }
+      return;  // the copy and the descriptor are zero past the leaf
+    }
+    const uint32_t* syms = reinterpret_cast<const uint32_t*>(h.tmpl);
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = 0;
+    for (uint32_t t = 0; t <= last; t++)
+      v[t >> 2] |= (uint32_t)kryo::sym_byte(syms[lo + t], h.data, h.value) << (8 * (t & 3));
+    return;
+  }
+  if (last < 15) {  // RAW: the window holds only the leaf's bytes
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int keep = (int)last + 1 - 4 * i;  // bytes of word i inside the leaf
+      v[i] = keep >= 4 ? v[i] : keep <= 0 ? 0u : v[i] & ((1u << (8 * keep)) - 1);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(1024) kryo_hash_kernel(ItemSrc items, uint64_t n, uint32_t group,
+                                                         const uint32_t* __restrict__ item_slot,
+                                                         const uint32_t* __restrict__ slot_map,
+                                                         const uint32_t* __restrict__ arena,
+                                                         const uint64_t* __restrict__ sizes,
+                                                         const uint8_t* __restrict__ status,
+                                                         uint32_t* __restrict__ hashes /* [n][8] BE words */) {
+  kryo_priority();
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = item_of(j, n, group);
+  if (i >= n) return;
+  HashSrc h;
+  h.kind = 2;
+  if (status[i] == 0) {
+    const cordahip_kryo_item it = items[i];
+    const uint32_t slot = item_slot[i];
+    h.data = it.data;
+    h.value = it.value;
+    h.len = (uint32_t)sizes[i];
+    if (slot == kRawSlot) {
+      h.kind = 1;
+    } else if (slot != kNoSlot && !(slot & kDefer)) {
+      h.kind = 0;
+      h.tmpl = reinterpret_cast<const uint8_t*>(arena + (size_t)slot_map[slot] * kTmplWords);
+    }
+  }
+  uint32_t st[8];
+  if (h.kind == 2) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) st[k] = 0;
+  } else {
+    sha256_init(st);
+    const uint32_t nb = (h.len + 9 + 63) / 64;
+    // the descriptors one block ahead: a block's payload loads then issue with its
+    // constant-copy loads instead of after a descriptor round trip
+    uint64_t dn[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) dn[q] = piece_desc(h, q);
+    for (uint32_t b = 0; b < nb; b++) {
+      uint32_t w[16];
+      uint64_t dc[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        dc[q] = dn[q];
+        dn[q] = piece_desc(h, 4 * (b + 1) + q);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t p = 4 * b + q;
+        uint32_t v[4] = {0, 0, 0, 0};
+        if (16 * p < h.len) leaf_piece(h, p, dc[q], v);
+        if (h.len >= 16 * p && h.len < 16 * p + 16) {  // the padding's first byte
+          const uint32_t t = h.len - 16 * p;
+          v[t >> 2] |= 0x80u << (8 * (t & 3));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) w[4 * q + k] = bswap32(v[k]);
+      }
+      if (b == nb - 1) {
+        w[14] = 0;
+        w[15] = h.len * 8;
+      }
+      sha256_block(st, w);
+    }
+  }
+  uint4* o = reinterpret_cast<uint4*>(hashes + i * 8);
+  o[0] = make_uint4(st[0], st[1], st[2], st[3]);
+  o[1] = make_uint4(st[4], st[5], st[6], st[7]);
+}
+
 }  // namespace
 
 // The encoder's persistent per-device state (cordahip.cpp allocates
@@ -681,6 +817,19 @@ hipError_t kryo_reset_misses(uint8_t* fixed, hipStream_t s) {
 uint32_t kryo_clear_threshold_slots() { return kSlots / 2; }
 uint32_t kryo_clear_threshold_templates() { return kBuilders - 64; }
 
+hipError_t launch_kryo_shape(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
+                             uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
+                             uint64_t* sizes, uint8_t* status, hipStream_t s, bool templates_only) {
+  if (n == 0) return hipSuccess;
+  const ItemSrc items{d_items, data_base, data_len};
+  const KryoState k(fixed);
+  const uint32_t sb = shape_block(n, group), g = grouped(n, group) ? group : 1;
+  hipLaunchKernelGGL(kryo_shape_kernel, dim3((uint32_t)((item_threads(n, group) + sb - 1) / sb)), dim3(sb), 0, s, items,
+                     n, g, templates_only, k.table, k.slot_size, k.rec, item_slot, k.shape_list, sizes, status,
+                     direct, k.counters);
+  return hipGetLastError();
+}
+
 hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
                               uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
                               uint64_t* sizes, uint64_t* off, uint8_t* out, uint64_t cap, uint8_t* status,
@@ -695,10 +844,8 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* 
     e = e ? e : hipMemsetAsync(off, 0, 8, s);
     return e;
   }
-  const uint32_t sb = shape_block(n, group), g = grouped(n, group) ? group : 1;
-  hipLaunchKernelGGL(kryo_shape_kernel, dim3((uint32_t)((item_threads(n, group) + sb - 1) / sb)), dim3(sb), 0, s, items,
-                     n, g, templates_only, k.table, k.slot_size, k.rec, item_slot, k.shape_list, sizes, status,
-                     direct, k.counters);
+  e = launch_kryo_shape(d_items, data_base, data_len, n, group, fixed, item_slot, direct, sizes, status, s,
+                        templates_only);
   // build, tsize, dsize (and dwrite) serve new shapes and direct items; in steady
   // state they find nothing to do, yet beside the Ed25519 ladders of a component
   // batch each empty launch of build / dsize / dwrite took 0.07-0.47 ms on the
@@ -725,6 +872,18 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* 
 }
 
 hipError_t kryo_set_priority(uint32_t on) { return hipMemcpyToSymbol(HIP_SYMBOL(g_kryo_prio), &on, 4); }
+
+hipError_t launch_kryo_hash(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
+                            uint64_t n, uint32_t group, uint8_t* fixed, const uint32_t* item_slot,
+                            const uint64_t* sizes, const uint8_t* status, uint32_t* hashes, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const ItemSrc items{d_items, data_base, data_len};
+  const KryoState k(fixed);
+  const uint32_t sb = shape_block(n, group), g = grouped(n, group) ? group : 1;
+  hipLaunchKernelGGL(kryo_hash_kernel, dim3((uint32_t)((item_threads(n, group) + sb - 1) / sb)), dim3(sb), 0, s, items,
+                     n, g, item_slot, k.slot_map, k.arena, sizes, status, hashes);
+  return hipGetLastError();
+}
 
 hipError_t kryo_scan_bytes(size_t& bytes, uint64_t n1, hipStream_t s) {
   bytes = 0;

@@ -63,6 +63,15 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* items, const uint8_t* da
                               uint32_t* item_slot, uint32_t* direct, uint64_t* sizes, uint64_t* off, uint8_t* out,
                               uint64_t cap, uint8_t* status, uint8_t* dws, uint64_t dwriters, void* scan_temp,
                               size_t scan_bytes, hipStream_t s, bool templates_only = false);
+// the shape pass alone (sizes, item_slot, statuses; kCMiss counts misses)
+hipError_t launch_kryo_shape(const cordahip_kryo_item* items, const uint8_t* data_base, uint64_t data_len, uint64_t n,
+                             uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct, uint64_t* sizes,
+                             uint8_t* status, hipStream_t s, bool templates_only);
+// SHA-256 of every item's leaf straight from its template (after a templates-only shape
+// pass): hashes[n][8] big-endian words, zero for items with a nonzero status
+hipError_t launch_kryo_hash(const cordahip_kryo_item* items, const uint8_t* data_base, uint64_t data_len, uint64_t n,
+                            uint32_t group, uint8_t* fixed, const uint32_t* item_slot, const uint64_t* sizes,
+                            const uint8_t* status, uint32_t* hashes, hipStream_t s);
 hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s);
 hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
                             uint8_t* tx_status, hipStream_t s);

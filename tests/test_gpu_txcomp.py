@@ -237,3 +237,34 @@ def test_templates_only_chain_and_its_redo(engine, oracle):
         _compare(engine, leaves, res, sigs)
     for _ in range(3):
         cash_call()
+
+
+def test_fused_template_hashes_every_kind(engine, oracle):
+    """The templates-only chain hashes leaves straight from their templates (no leaf bytes):
+    a batch of every kind -- RAW leaves of 0..200 bytes, strings, keys, parties, commands,
+    cash states, boxed primitives -- run until its shapes are built (full chain), then again
+    (templates-only): ids equal the oracle's over the restatement's leaves every time."""
+    rng = random.Random(55)
+    ref_keys = [bytes.fromhex(v["A"]) for v in TK._key_vectors()]
+    # few distinct shapes (the table then holds them all: no direct items, so the later
+    # calls run the templates-only chain)
+    cash_pool = [TK._cash_state(rng, ref_keys) for _ in range(6)]
+    party_pool = [TK._party(rng, ref_keys) for _ in range(6)]
+    txs = []
+    for t in range(300):
+        comps = [("cash_state", rng.choice(cash_pool), 52), ("party", rng.choice(party_pool), 52),
+                 ("issue_command", ("net.corda.contracts.asset.Cash$Commands$Issue", rng.randrange(-2**63, 2**63),
+                                    [(45, rng.choice(ref_keys)) for _ in range(rng.randrange(1, 4))]), 10),
+                 ("raw", bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 15, 16, 17, 55, 56, 63, 64, 200]))), 0),
+                 ("ed25519_key", rng.choice(ref_keys), 45), ("int", rng.randrange(-2**31, 2**31), 0),
+                 ("long", rng.randrange(-2**63, 2**63), 0), ("String", "tx%d" % (t % 7), 0),
+                 ("kotlin_object", K.TRANSACTION_TYPE_GENERAL, 0)]
+        rng.shuffle(comps)
+        txs.append(comps[:rng.randrange(1, len(comps) + 1)])
+    leaves = [[K.leaf(k, v, c) for k, v, c in tx] for tx in txs]
+    ids = [_oracle_id(oracle, lv) for lv in leaves]
+    sigs = [[(ED,) + _sign(oracle, hashlib.sha256(b"fth%d" % t).digest(), ids[t])] for t in range(len(txs))]
+    for _ in range(4):
+        res = engine.signed_txcomp_verify(txs, sigs)
+        assert [res[0][t].tobytes() for t in range(len(txs))] == ids
+        assert (res[1] == 0).all() and (res[3] == 0).all()
