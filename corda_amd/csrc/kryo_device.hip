@@ -64,12 +64,14 @@ constexpr uint32_t kTmplSyms = 4096;       // leaf bytes a template covers (long
 //                          the block's kind (bits 16..17: 0 constants only, 1 every patched
 //                          byte t is payload byte delta + t, 2 anything else: byte by byte),
 //                          delta (bits 32..63, signed)
-//   work [2][kTmplSyms] u8 the builder's byte scratch
+//   mid  [16] u32          leaf hashing: [0] kc, the leading 64-byte blocks whose bytes are
+//                          all constants, [1..8] the SHA-256 state after them (kryo_hash
+//                          starts there: 6 of a cash-issue transaction's 30 blocks)
 constexpr uint32_t kTB = kTmplSyms + 48;   // 16 pad + up to 15 shift + the leaf + 16 pad + 1 (a multiple of 16)
 constexpr uint32_t kBlk = kTB / 16;        // blocks per copy
 constexpr size_t kOffTb = (size_t)kTmplSyms * 4, kOffDesc = kOffTb + 16 * (size_t)kTB,
-                 kOffWork = kOffDesc + 16 * (size_t)kBlk * 8,
-                 kTmplBytes = (kOffWork + 2 * (size_t)kTmplSyms + 255) / 256 * 256;
+                 kOffMid = kOffDesc + 16 * (size_t)kBlk * 8,
+                 kTmplBytes = (kOffMid + 64 + 255) / 256 * 256;
 constexpr size_t kTmplWords = kTmplBytes / 4;
 constexpr uint32_t kDescConst = 0, kDescLinear = 1, kDescBytes = 2;
 constexpr uint32_t kNoSlot = 0xffffffffu;  // item_slot: no shape (direct encoder)
@@ -344,6 +346,28 @@ __global__ void __launch_bounds__(64) kryo_build_kernel(ItemSrc items, const uns
         }
         reinterpret_cast<uint64_t*>(base + kOffDesc)[x] =
             (uint64_t)pm | ((uint64_t)kind << 16) | ((uint64_t)(uint32_t)(int32_t)delta << 32);
+      }
+      if (threadIdx.x == 0) {  // the midstate of the leading all-constant message blocks
+        uint32_t st[8], kc = 0;
+        sha256_init(st);
+        for (; 64 * (kc + 1) <= (uint32_t)size; kc++) {
+          uint32_t w[16];
+          bool cst = true;
+          for (uint32_t q = 0; q < 16; q++) {
+            uint32_t x = 0;
+            for (uint32_t t = 0; t < 4; t++) {
+              const uint32_t sym = syms[64 * kc + 4 * q + t];
+              cst = cst && (sym & kryo::kSymTypeMask) == kryo::kSymConst;
+              x = (x << 8) | (sym & 0xffu);
+            }
+            w[q] = x;
+          }
+          if (!cst) break;
+          sha256_block(st, w);
+        }
+        uint32_t* mid = reinterpret_cast<uint32_t*>(base + kOffMid);
+        mid[0] = kc;
+        for (int q = 0; q < 8; q++) mid[1 + q] = st[q];
       }
     }
     __syncthreads();
@@ -736,13 +760,22 @@ __global__ void __launch_bounds__(1024) kryo_hash_kernel(ItemSrc items, uint64_t
     for (int k = 0; k < 8; k++) st[k] = 0;
   } else {
     sha256_init(st);
+    uint32_t b0 = 0;
+    if (h.kind == 0) {  // start after the template's all-constant blocks
+      const uint32_t* mid = reinterpret_cast<const uint32_t*>(h.tmpl + kOffMid);
+      b0 = mid[0];
+      if (b0) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) st[k] = mid[1 + k];
+      }
+    }
     const uint32_t nb = (h.len + 9 + 63) / 64;
     // the descriptors one block ahead: a block's payload loads then issue with its
     // constant-copy loads instead of after a descriptor round trip
     uint64_t dn[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) dn[q] = piece_desc(h, q);
-    for (uint32_t b = 0; b < nb; b++) {
+    for (int q = 0; q < 4; q++) dn[q] = piece_desc(h, 4 * b0 + q);
+    for (uint32_t b = b0; b < nb; b++) {
       uint32_t w[16];
       uint64_t dc[4];
 #pragma unroll
