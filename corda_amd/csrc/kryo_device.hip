@@ -213,31 +213,27 @@ __global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_
     status[i] = st;
     return;
   }
-  uint64_t h = 0;
-  const bool hashed = kryo::shape_hash_of(it, h);
-  // the first hashed lane probes for every lane of its hash; other hashes probe alone
-  const uint64_t hb = __ballot(hashed);
-  const int lead = hb ? __ffsll((unsigned long long)hb) - 1 : 0;
-  const uint64_t h0 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(h >> 32), lead) << 32) |
-                      (uint32_t)__shfl((int)(uint32_t)h, lead);
-  const bool follower = hashed && h == h0 && (int)__lane_id() != lead;
-  uint32_t slot = kNoSlot;
-  bool claimed = false;
-  if (hashed && !follower) slot = probe_slot(table, h, i, templates_only, claimed);
-  const uint32_t lead_slot = (uint32_t)__shfl((int)slot, lead);
-  if (follower) slot = lead_slot;  // claimed by the leader: slot_size is kUnbuilt, deferred below
-  if (claimed) {
-    shape_list[atomicAdd(&counters[kCNew], 1u)] = slot;
-    atomicAdd(&counters[kCUsed], 1u);
-  }
-  // a wave whose items all have one slot (the common case: one kind per wave) compares
-  // them with a copy of the record in LDS instead of 64 lanes re-reading it through the L2
+  // 1. The wave's first lane hashes its item and finds its slot. 2. When that slot
+  // holds a built template, every lane compares its item with the slot's record
+  // (copied to LDS): one walk per item in the common case, a wave of one kind of
+  // the same shape (r05: a hash walk plus a compare walk per item). 3. Lanes that
+  // do not match hash their own item and probe (new shapes, other kinds, collisions).
   __shared__ kryo::ShapeRec srec[16];
   const uint64_t act = __ballot(true);
-  const uint32_t s0 = (uint32_t)__shfl((int)slot, __ffsll((unsigned long long)act) - 1);
-  const bool uni = s0 != kNoSlot && __ballot(slot == s0) == act;
-  const kryo::ShapeRec* rp = rec + (slot == kNoSlot ? 0 : slot);
-  if (uni) {
+  const int lead = __ffsll((unsigned long long)act) - 1;
+  const bool is_lead = (int)__lane_id() == lead;
+  uint32_t slot = kNoSlot;
+  bool claimed = false;
+  if (is_lead) {
+    uint64_t h = 0;
+    if (kryo::shape_hash_of(it, h)) slot = probe_slot(table, h, i, templates_only, claimed);
+  }
+  const uint32_t s0 = (uint32_t)__shfl((int)slot, lead);
+  const bool c0 = __shfl((int)claimed, lead) != 0;
+  const int32_t z0 = (s0 != kNoSlot && !c0) ? slot_size[s0] : kUnbuilt;
+  const bool built0 = z0 != kUnbuilt && z0 != kNoTemplate;
+  bool done = false;
+  if (built0) {
     kryo::ShapeRec* mine = &srec[threadIdx.x >> 6];
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
     const uint32_t nact = (uint32_t)__popcll(act);
@@ -248,14 +244,28 @@ __global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    rp = mine;
+    if (template_item(it, *mine, z0, size, st)) {
+      slot = s0;
+      done = true;
+    } else if (is_lead) {
+      slot = kNoSlot;  // the slot's record is another shape (a hash collision): direct
+      done = true;
+    }
+  }
+  if (!done && !is_lead) {
+    uint64_t h = 0;
+    if (kryo::shape_hash_of(it, h)) slot = probe_slot(table, h, i, templates_only, claimed);
+  }
+  if (claimed) {
+    shape_list[atomicAdd(&counters[kCNew], 1u)] = slot;
+    atomicAdd(&counters[kCUsed], 1u);
   }
   bool deferred = false;
-  if (slot != kNoSlot) {
+  if (!done && slot != kNoSlot) {
     const int32_t z = claimed ? kUnbuilt : slot_size[slot];
     if (z == kUnbuilt && !templates_only) {  // built after this kernel: compared in kryo_tsize
       deferred = true;
-    } else if (z == kUnbuilt || !template_item(it, *rp, z, size, st)) {
+    } else if (z == kUnbuilt || !template_item(it, rec[slot], z, size, st)) {
       slot = kNoSlot;
     }
   }
