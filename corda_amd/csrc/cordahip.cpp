@@ -491,7 +491,11 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batc
       cp->max_items = std::max(cp->max_items, b->tx_leaf_off[bound[j + 1]] - b->tx_leaf_off[bound[j]]);
     }
     cp->copied = 0;
-    leaf_buf = 2 * cp->slice_cap;
+    // the templates-only chain hashes the leaves from their templates: no leaf buffers
+    // (the full chain's two slice buffers are bounded at 4 KB + 4 B per payload byte per
+    // component: ~1.4 GB each for C4's 2^17-signature slices)
+    cp->templates_only = cp->templates_only && d.kryo_templates_ok;
+    leaf_buf = cp->templates_only ? 0 : 2 * cp->slice_cap;
     if (w.comp_items.ensure(std::max<uint64_t>(nleaves, 1) * sizeof(cordahip_kryo_item)) ||
         w.payload.ensure(std::max<uint64_t>(ns ? cp->pay_end.back() : 0, 16)) ||
         w.comp_status.ensure(std::max<uint64_t>(nleaves, 1)))
@@ -510,7 +514,7 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batc
     }
     if (hipError_t e = kryo_state_ready(d, d.stream)) return e;
     if (hipError_t e = kryo_reset_misses(d.kryo_fixed.as<uint8_t>(), d.stream)) return e;
-    cp->templates_only = cp->templates_only && d.kryo_templates_ok;
+    cp->templates_only = cp->templates_only && d.kryo_templates_ok;  // kryo_state_ready may have cleared the table
   } else {
     leaf_buf = b->leaf_off[l1] - b->leaf_off[l0];
   }

@@ -207,8 +207,15 @@ __global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_
   uint8_t st = 0;
   if (it.kind == CORDAHIP_KRYO_RAW) {
     item_slot[i] = kRawSlot;
-    if (it.len && !it.data) st = 1;
-    else size = it.len;
+    if (it.len && !it.data) {
+      st = 1;
+    } else if (templates_only && it.len >> 32) {  // kryo_hash takes 32-bit lengths: the full chain
+      st = kKryoMiss;
+      item_slot[i] = kNoSlot;
+      atomicAdd(&counters[kCMiss], 1u);
+    } else {
+      size = it.len;
+    }
     sizes[i] = size;
     status[i] = st;
     return;
@@ -621,10 +628,12 @@ __global__ void __launch_bounds__(256) kryo_twrite_kernel(ItemSrc items, uint64_
         } else {
           const uint8_t* tp = reinterpret_cast<const uint8_t*>(m.tmpl);
           const uint32_t idx = (uint32_t)(16 + (int64_t)m.sh + pb);  // a multiple of 16
+          // the descriptor and the constant copy load together (the copy's address needs
+          // no descriptor); the payload window follows the descriptor
           const uint64_t desc = reinterpret_cast<const uint64_t*>(tp + kOffDesc)[m.sh * kBlk + idx / 16];
+          const uint4 tv = *reinterpret_cast<const uint4*>(tp + kOffTb + (size_t)m.sh * kTB + idx);
           const uint32_t pm = (uint32_t)desc & 0xffff, kind = (uint32_t)(desc >> 16) & 3;
           if (kind != kDescBytes) {
-            const uint4 tv = *reinterpret_cast<const uint4*>(tp + kOffTb + (size_t)m.sh * kTB + idx);
             v[0] = tv.x, v[1] = tv.y, v[2] = tv.z, v[3] = tv.w;
             if (pm) {
               uint32_t w[4];
