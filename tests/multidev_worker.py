@@ -130,6 +130,39 @@ def main():
     if [int(x) for x in a[1]] != want_st:
         bad["signed_tx_expected"] = True
 
+    # 4b. component-level signed transactions (cordahip_txcomp_submit): the cash-issue
+    # corpus sharded over the devices, each with its own encoder state; three calls
+    # (shapes built, then the templates-only chain) against a one-device context
+    from corda_amd import _lib
+    from corda_amd.corpus import cash_issue_items
+    r2 = np.random.default_rng(77 + k)
+    nc = 600 + 13 * k
+    blob, items, _ = cash_issue_items(r2.integers(0, 256, (nc, 32), dtype=np.uint8),
+                                      r2.integers(0, 256, (nc, 32), dtype=np.uint8), bytes(range(32)),
+                                      r2.integers(1, 10**9, nc), r2.integers(-2**63, 2**63 - 1, nc))
+    it = items.reshape(-1).copy()
+    host_it = it.copy()
+    host_it["data"] += np.uint64(blob.ctypes.data)
+    hb, ho = _lib.kryo_encode_array(host_it)
+    cl = [[hb[int(ho[5 * t + q]):int(ho[5 * t + q + 1])].tobytes() for q in range(5)] for t in range(nc)]
+    cids, _ = one.tx_ids(cl)
+    csl = []
+    for t in range(nc):
+        orc.oracle_ed25519_sign(hashlib.sha256(b"comp%d" % (t % 5)).digest(), cids[t].tobytes(), 32, pub, sig)
+        s = sig.raw if t % 11 != 3 else sig.raw[:9] + bytes([sig.raw[9] ^ 2]) + sig.raw[10:]
+        csl.append([(ED, pub.raw, s)])
+    tio = np.arange(0, 5 * nc + 1, 5, dtype=np.uint64)
+    cb = one.signed_txcomp_verify_arrays(blob, it, tio, csl)
+    for call in range(3):
+        ca = eng.signed_txcomp_verify_arrays(blob, it, tio, csl, pinned_out=call == 2)
+        for name, x, y in zip(("ids", "tx_status", "first_bad", "sig_status"), ca, cb):
+            if not np.array_equal(x, y):
+                bad["txcomp_%d_%s" % (call, name)] = True
+    if [int(x) for x in cb[1]] != [1 if t % 11 == 3 else 0 for t in range(nc)]:
+        bad["txcomp_expected"] = True
+    if not np.array_equal(cb[0], cids[:nc]):
+        bad["txcomp_ids_vs_leaf_path"] = True
+
     # 5. filtered transactions: the PartialMerkleTree goldens
     cases = _load("pmt_vectors.json", "cases")
     cs = [cases[i % len(cases)] for i in range(199)]

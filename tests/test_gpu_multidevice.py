@@ -5,7 +5,9 @@ Device objects on HIP device 0, each with its own streams, workspaces and
 tables, so the shard split, one worker per device, ragged shard tails and the
 reassembly of statuses / verdict words run for real. tests/multidev_worker.py
 drives the generic CSR batch (both sections), the dense host rows, tx ids,
-signed and filtered transactions and the C5 stream, and compares every result
+signed transactions (leaves and components: each device's own encoder state,
+the templates-only chain from the third call), filtered transactions and the
+C5 stream, and compares every result
 with the goldens / oracle and with a one-device context. Small pipeline chunks
 (CORDAHIP_HOST_CHUNK / CORDAHIP_STREAM_CHUNK) make every shard span several
 chunks and reuse all pipeline stages; CORDAHIP_TX_SLICES=5 runs every device's
