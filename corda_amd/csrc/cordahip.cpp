@@ -767,14 +767,23 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
     r = CORDAHIP_ERR_OUT_OF_MEMORY;
   if (r == CORDAHIP_SUCCESS && issue_through(0) != hipSuccess) r = CORDAHIP_ERR_HIP;
   // each signature signs its transaction's id (SignedTransaction.kt:98): the
-  // pipeline finds it through tx_of, this shard's part built now, while the
-  // first slice's leaf bytes cross PCIe (~0.45 ms of host time for C4 that
-  // preceded every copy in r04_p)
-  if (r == CORDAHIP_SUCCESS)
-    ctx->host->parallel_for(hi - lo, 4096, [&](uint64_t x, uint64_t y) {
-      for (uint64_t t = lo + x; t < lo + y; t++)
-        for (uint64_t q = b->tx_sig_off[t]; q < b->tx_sig_off[t + 1]; q++) tx_of[q] = t;
+  // pipeline finds it through tx_of, filled chunk by chunk just ahead of its use
+  // (fill_to, from di.advance) -- built whole before the first chunk it held the
+  // first pack ~0.5 ms (r05 host trace: C4's 2.5 M signatures)
+  uint64_t filled = s0;  // tx_of holds signatures [s0, filled)
+  auto fill_to = [&](uint64_t s_end) {
+    s_end = std::min(s_end, s1);
+    if (s_end <= filled) return;
+    const uint64_t* so = b->tx_sig_off;
+    const uint64_t ta = (uint64_t)(std::upper_bound(so + lo, so + hi + 1, filled) - so) - 1;
+    const uint64_t tb = (uint64_t)(std::upper_bound(so + lo, so + hi + 1, s_end - 1) - so);
+    const uint64_t f0 = filled;
+    ctx->host->parallel_for(tb - ta, 4096, [&](uint64_t x, uint64_t y) {
+      for (uint64_t t = ta + x; t < ta + y; t++)
+        for (uint64_t q = std::max(so[t], f0); q < std::min(so[t + 1], s_end); q++) tx_of[q] = t;
     });
+    filled = s_end;
+  };
   std::vector<std::pair<uint64_t, uint64_t>> reduced;  // tx ranges the chunks reduced
   if (r == CORDAHIP_SUCCESS && s1 > s0) {
     di.txid = d.tx.txid.as<uint8_t>();
@@ -784,6 +793,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
     di.advance = [&](uint64_t sig_end, bool after) {
       // after: the slices of the next `lookahead` chunks' signatures
       const uint64_t e = after ? std::min(s1, sig_end + lookahead * chunk_max) : sig_end;
+      fill_to(e);
       const uint64_t tx = tx_of[e - 1];
       const size_t j = (size_t)(std::upper_bound(di.tx_bound.begin(), di.tx_bound.end(), tx) - di.tx_bound.begin()) - 1;
       return issue_through(j);
@@ -823,10 +833,12 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
       r = CORDAHIP_ERR_HIP;
     }
   }
+  const double tr0 = tracing() ? now_ms() : 0;
   // slices no signature asked for (transactions without signatures at the end)
   if (r == CORDAHIP_SUCCESS && issue_through(slices) != hipSuccess) r = CORDAHIP_ERR_HIP;
   // every slice writes the caller's txid / tx_status: drain before returning, errors included
   const hipError_t e1 = hipStreamSynchronize(d.s_idcopy ? d.s_idcopy : d.stream), e2 = hipStreamSynchronize(d.stream);
+  const double tr1 = tracing() ? now_ms() : 0;
   if (r == CORDAHIP_SUCCESS && (e1 != hipSuccess || e2 != hipSuccess)) r = CORDAHIP_ERR_HIP;
   if (r != CORDAHIP_SUCCESS) return r;
   if (cp) {
@@ -848,6 +860,9 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
     t = std::max(t, rg.second);
   }
   reduce_txs(ctx, b, t, hi);
+  if (tracing())
+    fprintf(stderr, "[cordahip] dev %d signed tx tail: id streams drained %.2f ms, edge reduce %.2f ms\n", d.id,
+            tr1 - tr0, now_ms() - tr1);
   return r;
 }
 
