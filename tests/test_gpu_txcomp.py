@@ -255,7 +255,8 @@ def test_fused_template_hashes_every_kind(engine, oracle):
         comps = [("cash_state", rng.choice(cash_pool), 52), ("party", rng.choice(party_pool), 52),
                  ("issue_command", ("net.corda.contracts.asset.Cash$Commands$Issue", rng.randrange(-2**63, 2**63),
                                     [(45, rng.choice(ref_keys)) for _ in range(rng.randrange(1, 4))]), 10),
-                 ("raw", bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 15, 16, 17, 55, 56, 63, 64, 200]))), 0),
+                 ("raw", bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 15, 16, 17, 55, 56, 63, 64, 200])))
+                  if t % 97 else rng.randbytes(5000 if t % 2 else 70_000), 0),
                  ("ed25519_key", rng.choice(ref_keys), 45), ("int", rng.randrange(-2**31, 2**31), 0),
                  ("long", rng.randrange(-2**63, 2**63), 0), ("String", "tx%d" % (t % 7), 0),
                  ("kotlin_object", K.TRANSACTION_TYPE_GENERAL, 0)]
