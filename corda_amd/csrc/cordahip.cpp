@@ -868,9 +868,10 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
 
 // A component batch runs the encoder's templates-only chain when the device's
 // last component batch needed no new template and no direct encoder
-// (Device::kryo_templates_ok): per id slice, shape -> scan -> template writes,
-// without the build / size / direct-write kernels whose empty launches sat on
-// each slice's critical path. An item that would need them is a miss; the call
+// (Device::kryo_templates_ok): per id slice, the shape pass and the leaf hashes
+// straight from the templates (kryo_hash: no leaf bytes), without the build /
+// size / direct-write kernels whose empty launches sat on each slice's critical
+// path. An item that would need them is a miss; the call
 // then runs again with the full chain (its results overwrite every output).
 // CORDAHIP_KRYO_TEMPLATES_ONLY=0 always runs the full chain.
 int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b, uint64_t* tx_of, uint64_t lo,

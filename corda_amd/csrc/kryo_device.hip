@@ -10,27 +10,31 @@
 //   1. kryo_shape: every item's shape hash (a streaming walk of the inputs the
 //      encoder branches on) picks a slot of a 2^16-slot table; an empty slot is
 //      claimed with one 64-bit CAS (hash | item) and the item becomes the
-//      shape's representative.
+//      shape's representative. Items of shapes built by earlier calls are
+//      compared with the slot's exact record (shape_matches; the hash only
+//      picks the slot) and sized here.
 //   2. kryo_build: one wave per NEW shape records the representative's shape
 //      (structure words and span bytes, ShapeRec) in the slot and traces it
 //      through the encoder (KoutT<true>, the OutputChunked level buffers in
 //      LDS): a symbol per leaf byte -- a constant, payload byte k, or byte j of
-//      the item's value -- stored in 4 copies shifted by 0..3 bytes, so every
-//      output dword reads its 4 symbols with one aligned 16-byte load.
-//   3. kryo_tsize: every item is compared with its slot's record
-//      (shape_matches: exact; the hash only picked the slot) and sized from
-//      the template (RAW: its length); items without a shape, with a hash
-//      collision, or whose shape has no template go on a list for the direct
-//      encoder, which sizes them (kryo_dsize, counting mode).
+//      the item's value; then 16 copies of the constant bytes shifted by 0..15,
+//      a descriptor per 16-byte block and shift, and the SHA-256 midstate of the
+//      leading all-constant blocks.
+//   3. kryo_tsize: items of shapes claimed in this call, compared and sized
+//      after kryo_build; items without a shape, with a hash collision, or whose
+//      shape has no template go on a list for the direct encoder, which sizes
+//      them (kryo_dsize, counting mode).
 //   4. an exclusive scan of the sizes into the CSR offsets (hipcub).
-//   5. kryo_twrite: a wave per 32 consecutive leaves writes their bytes in
-//      output order, one aligned dword per lane (64 lanes = 256 contiguous
-//      bytes per store instruction); a dword of constant symbols is 4 selects,
-//      payload and value bytes are fetched per byte; the dword a leaf ends in
-//      carries the next leaves' first bytes.
+//   5. kryo_twrite: a wave writes the output span of 16 consecutive leaves in
+//      16-byte blocks, one per lane (1 KB per store instruction): the constant
+//      copy for the block's alignment with the descriptor's payload window
+//      merged in; the rare blocks (leaf boundaries, value bytes, RAW edges) go
+//      to a per-wave LDS queue and are written byte by byte afterwards.
 //   6. kryo_dwrite: the listed items through the direct encoder (per-thread
-//      level buffers in a workspace), after kryo_twrite: their byte stores
-//      replace what kryo_twrite left in the dwords they share.
+//      level buffers in a workspace); its byte stores share no byte with
+//      kryo_twrite's.
+//   7. kryo_hash (the component-level signed-tx slices, once every shape is
+//      built): each leaf's SHA-256 straight from its template, no leaf bytes.
 // The table, the records and the templates persist across calls on a device
 // (a template is derived metadata of a shape, never a cached leaf: every call
 // writes every leaf from its own items), so batches of recurring shapes build
