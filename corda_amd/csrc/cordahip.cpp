@@ -277,7 +277,8 @@ hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* ke
 // Enqueue Ed25519 verification of n dense lanes on stream s (device already current).
 hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
-                             unsigned long long* verdict, uint32_t flags, hipStream_t s, int slot) {
+                             unsigned long long* verdict, uint32_t flags, hipStream_t s, int slot,
+                             const std::function<hipError_t()>* before_msgs) {
   std::lock_guard<std::mutex> g(d.ed_mu[slot]);
   DevBuf& ws = d.ed_ws[slot];
   hipEvent_t& ev = d.ed_ev[slot];
@@ -310,7 +311,7 @@ hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs
   hipError_t e = hipStreamWaitEvent(s, ev, 0);
   e = e ? e
         : launch_ed25519_verify(keys, sigs, msgs, msg_len, n, d.btab, pre, status, verdict, ws.as<uint32_t>(),
-                                ws.cap / ed25519_ws_lane_bytes() / 64 * 64, flags, s);
+                                ws.cap / ed25519_ws_lane_bytes() / 64 * 64, flags, s, before_msgs);
   e = e ? e : hipEventRecord(ev, s);
   return e;
 }
@@ -788,6 +789,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
   if (r == CORDAHIP_SUCCESS && s1 > s0) {
     di.txid = d.tx.txid.as<uint8_t>();
     di.t0 = lo;
+    di.split_prep = cp == nullptr;
     // before a chunk's copies: the slices it needs; after them: `lookahead` more,
     // so PCIe carries leaf bytes while the GPU verifies the chunk
     di.advance = [&](uint64_t sig_end, bool after) {

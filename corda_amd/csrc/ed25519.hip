@@ -22,6 +22,8 @@
 #define FE_USE_ASM2 1
 #endif
 #include <hip/hip_runtime.h>
+
+#include <functional>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -475,16 +477,13 @@ CDEV void store_table8(uint32_t* __restrict__ rec, const ge_p3& base) {
 #ifndef ED_PREP_WAVES
 #define ED_PREP_WAVES 2
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_PREP_WAVES))) ed25519_prep_half_kernel(
-    const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
-    uint32_t msg_len, uint64_t base, uint64_t m, const uint8_t* __restrict__ pre_status,
-    uint8_t* __restrict__ status, uint32_t* __restrict__ ws, uint32_t empty_is_error) {
-  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (li >= m) return;
-  const uint64_t i = base + li;
-  uint32_t* rec = ws + li * kWhLaneWords;
+// Phase 1 of the prep (no message): decode A and R, the pre-engine statuses, the
+// tables [k](-A), [k](-R). Returns the lane's status (kStatusPending: verify);
+// abyte = EdDSAPublicKey.Abyte, Rw = R's bytes, both for the SHA-512 of phase 2.
+CDEV uint8_t prep_keys_phase(const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, uint64_t i,
+                             uint32_t msg_len, const uint8_t* __restrict__ pre_status, uint32_t empty_is_error,
+                             uint32_t* __restrict__ rec, uint32_t abyte[8], uint32_t Rw[8]) {
   uint8_t st = kStatusPending;
-  uint32_t abyte[8], Rw[8];
   load8(Rw, reinterpret_cast<const uint32_t*>(sigs + i * 64));
   {
     // A (i2p decode: y not range checked) and R (strict decode: encode(R') ==
@@ -525,6 +524,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_PRE
     store_table8(tab, P);
     PHASE_BARRIER();
   }
+  return st;
+}
+
+// Phase 2 (the message): SHA-512(R || A || M), h, S_eff, the lattice reduction,
+// e = c1 S_eff mod L -> the record's scalars (zero for decided lanes).
+CDEV void prep_msg_phase(const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs, uint32_t msg_len,
+                         uint64_t i, uint8_t st, const uint32_t abyte[8], const uint32_t Rw[8],
+                         uint32_t* __restrict__ rec) {
   uint32_t ka[8], kr[8], e[8];
   bool c0neg = false;
   if (st == kStatusPending) {
@@ -541,11 +548,57 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_PRE
 #pragma unroll
     for (int q = 0; q < 8; q++) ka[q] = kr[q] = e[q] = 0;
   }
-  status[i] = st;
   store8(rec + kWhKa, ka);
   store8(rec + kWhKr, kr);
   store8(rec + kWhE, e);
   reinterpret_cast<uint4*>(rec + kWhFlags)[0] = make_uint4(c0neg ? 1u : 0u, 0u, 0u, 0u);
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_PREP_WAVES))) ed25519_prep_half_kernel(
+    const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
+    uint32_t msg_len, uint64_t base, uint64_t m, const uint8_t* __restrict__ pre_status,
+    uint8_t* __restrict__ status, uint32_t* __restrict__ ws, uint32_t empty_is_error) {
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= m) return;
+  const uint64_t i = base + li;
+  uint32_t* rec = ws + li * kWhLaneWords;
+  uint32_t abyte[8], Rw[8];
+  const uint8_t st = prep_keys_phase(keys, sigs, i, msg_len, pre_status, empty_is_error, rec, abyte, Rw);
+  prep_msg_phase(sigs, msgs, msg_len, i, st, abyte, Rw, rec);
+  status[i] = st;
+}
+
+// The same prep in two launches, for batches whose messages arrive after their
+// keys and signatures (the signed-tx chunks: each message is its transaction's
+// id, gathered on the device once the id slice is done): phase 1 needs no
+// message and runs while the ids are computed; it leaves the lane's status in
+// `status` and Abyte in the record's scalar words, which phase 2 overwrites.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_PREP_WAVES))) ed25519_prep_keys_kernel(
+    const uint8_t* __restrict__ keys, const uint8_t* __restrict__ sigs, uint32_t msg_len, uint64_t base, uint64_t m,
+    const uint8_t* __restrict__ pre_status, uint8_t* __restrict__ status, uint32_t* __restrict__ ws,
+    uint32_t empty_is_error) {
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= m) return;
+  const uint64_t i = base + li;
+  uint32_t* rec = ws + li * kWhLaneWords;
+  uint32_t abyte[8], Rw[8];
+  status[i] = prep_keys_phase(keys, sigs, i, msg_len, pre_status, empty_is_error, rec, abyte, Rw);
+  store8(rec + kWhKa, abyte);
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_PREP_WAVES))) ed25519_prep_msg_kernel(const uint8_t* __restrict__ sigs,
+                                                               const uint8_t* __restrict__ msgs, uint32_t msg_len,
+                                                               uint64_t base, uint64_t m,
+                                                               const uint8_t* __restrict__ status,
+                                                               uint32_t* __restrict__ ws) {
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= m) return;
+  const uint64_t i = base + li;
+  uint32_t* rec = ws + li * kWhLaneWords;
+  uint32_t abyte[8], Rw[8];
+  load8(abyte, rec + kWhKa);
+  load8(Rw, reinterpret_cast<const uint32_t*>(sigs + i * 64));
+  prep_msg_phase(sigs, msgs, msg_len, i, status[i], abyte, Rw, rec);
 }
 
 // ---------------------------------------------------------------------------
@@ -671,15 +724,31 @@ size_t ed25519_ws_lane_bytes() { return kWhLaneWords * sizeof(uint32_t); }
 hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
                                  uint64_t n, const uint32_t* btab, const uint8_t* pre_status, uint8_t* status,
                                  unsigned long long* verdict, uint32_t* ws, uint64_t ws_lanes, uint32_t flags,
-                                 hipStream_t s) {
+                                 hipStream_t s, const std::function<hipError_t()>* before_msgs) {
   if (n == 0) return hipSuccess;
   if (!ws || ws_lanes < 64 || ws_lanes % 64) return hipErrorInvalidValue;
+  bool msgs_ready = before_msgs == nullptr;
   for (uint64_t base = 0; base < n; base += ws_lanes) {
     const uint64_t m = n - base < ws_lanes ? n - base : ws_lanes;
     const uint32_t blocks = (uint32_t)((m + 255) / 256);
-    hipLaunchKernelGGL(ed25519_prep_half_kernel, dim3(blocks), dim3(256), 0, s, keys, sigs, msgs, msg_len, base, m,
-                       pre_status, status, ws, (flags & 1u) ? 0u : 1u);
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipSuccess;
+    if (msgs_ready) {
+      hipLaunchKernelGGL(ed25519_prep_half_kernel, dim3(blocks), dim3(256), 0, s, keys, sigs, msgs, msg_len, base, m,
+                         pre_status, status, ws, (flags & 1u) ? 0u : 1u);
+      e = hipGetLastError();
+    } else {
+      // keys and R first; the messages' producer (enqueued by before_msgs on the same
+      // stream) then runs beside this launch's tail, phase 2 after it
+      hipLaunchKernelGGL(ed25519_prep_keys_kernel, dim3(blocks), dim3(256), 0, s, keys, sigs, msg_len, base, m,
+                         pre_status, status, ws, (flags & 1u) ? 0u : 1u);
+      e = hipGetLastError();
+      e = e ? e : (*before_msgs)();
+      msgs_ready = true;
+      if (e == hipSuccess)
+        hipLaunchKernelGGL(ed25519_prep_msg_kernel, dim3(blocks), dim3(256), 0, s, sigs, msgs, msg_len, base, m, status,
+                           ws);
+      e = e ? e : hipGetLastError();
+    }
     if (e == hipSuccess) e = launch_ed25519_ladder(base, m, btab, ws, status, verdict, s);
     if (e != hipSuccess) return e;
   }

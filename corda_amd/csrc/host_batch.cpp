@@ -474,10 +474,15 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     // device-id messages: each section's stream waits for the id slice holding
     // the chunk's last transaction, then gathers its rows from the ids in HBM
     const hipEvent_t ids_ready = dev ? dev->wait_for(mv.tx_of[a + m - 1]) : nullptr;
-    if (dev && ne) {
-      e = e ? e : hipStreamWaitEvent(es, ids_ready, 0);
-      e = e ? e : launch_gather_rows32(dev->txid, st.didx[0].as<uint32_t>(), ne, st.d[2].as<uint8_t>(), es);
-    }
+    // one length group (the ids): the keys' half of the prep is enqueued first and the
+    // wait for the ids + the gather after it, so key / R decoding and their tables
+    // do not wait for the chunk's id slice
+    const bool split = dev && dev->split_prep && ne && ng == 1;
+    const std::function<hipError_t()> gather_ids = [&]() -> hipError_t {
+      hipError_t x = hipStreamWaitEvent(es, ids_ready, 0);
+      return x ? x : launch_gather_rows32(dev->txid, st.didx[0].as<uint32_t>(), ne, st.d[2].as<uint8_t>(), es);
+    };
+    if (dev && ne && !split) e = e ? e : gather_ids();
     st.direct = out_pinned && ng == 1 && ne == m && nc == 0 && a % 64 == 0;
     const uint64_t words = (m + 63) / 64;
     if (st.direct && b->verdict && st.dverdict.ensure(words * 8) != hipSuccess) st.direct = false;
@@ -488,7 +493,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
                               st.d[2].as<uint8_t>() + gmsg[gi], (uint32_t)lens[gi], cnt, st.d[3].as<uint8_t>() + r0,
                               st.d[4].as<uint8_t>() + r0,
                               st.direct && b->verdict ? st.dverdict.as<unsigned long long>() : nullptr, b->flags,
-                              es, slot);
+                              es, slot, split ? &gather_ids : nullptr);
     }
     if (st.direct) {
       e = e ? e : launch_store_to_host(st.d[4].p, dst_status + a, m, es);

@@ -28,7 +28,8 @@ size_t ed25519_btable_bytes();
 hipError_t launch_ed25519_verify(const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs, uint32_t msg_len,
                                  uint64_t n, const uint32_t* btab, const uint8_t* pre_status, uint8_t* status,
                                  unsigned long long* verdict, uint32_t* ws, uint64_t ws_lanes, uint32_t flags,
-                                 hipStream_t s);
+                                 hipStream_t s,
+                                 const std::function<hipError_t()>* before_msgs = nullptr);
 size_t ed25519_ws_lane_bytes();
 hipError_t launch_ed25519_sign(const uint8_t* seeds, const uint8_t* msgs, uint32_t msg_len, uint64_t n,
                                const uint32_t* btab, uint8_t* pubs, uint8_t* sigs, hipStream_t s);
@@ -349,9 +350,12 @@ hipError_t blocked(const char* what, F&& f) {
 
 int hip_err(hipError_t e);
 hipError_t ensure_streams(Device& d);
+// before_msgs != nullptr: the messages are produced on stream s by that callback,
+// which runs after the keys' half of the prep is enqueued (launch_ed25519_verify)
 hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
-                             unsigned long long* verdict, uint32_t flags, hipStream_t s, int slot = 0);
+                             unsigned long long* verdict, uint32_t flags, hipStream_t s, int slot = 0,
+                             const std::function<hipError_t()>* before_msgs = nullptr);
 // d.ec_mu must be held
 hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
                              const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs, const uint64_t* msg_off,
@@ -412,6 +416,10 @@ struct DeviceIds {
   std::vector<uint64_t> tx_bound;          // slice j = transactions [tx_bound[j], tx_bound[j + 1])
   std::vector<hipEvent_t> ready;           // ready[j]: slice j's ids are in txid (recorded on the id stream)
   std::vector<uint64_t> chunk_bound;       // the signature pipeline's chunk boundaries (signature indices)
+  // Ed25519 chunks run the prep's key half before waiting for their ids (leaf
+  // batches: +1.5% c4h interleaved; component batches, whose heavier id kernels
+  // then meet more prep beside them: -1.8%, profiles/r05_prep_split_ab/)
+  bool split_prep = false;
   // called before a chunk's copies are enqueued (after = false: the id slices
   // the chunk ending at sig_end needs) and after them (after = true: a few more)
   std::function<hipError_t(uint64_t sig_end, bool after)> advance;
