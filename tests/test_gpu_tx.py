@@ -248,3 +248,38 @@ def test_native_cash_issue_leaves_feed_tx_ids(engine, oracle):
         off[1:] = np.cumsum([len(x) for x in tx])
         assert oracle.oracle_tx_id(blob.ctypes.data, off.ctypes.data, len(tx), out) == 0
         assert out.raw == i.tobytes()
+
+
+def test_signed_tx_golden_edge_signatures(engine, oracle):
+    """The Ed25519 golden catalogue's keys and signatures (bad keys, non-canonical
+    and off-curve R, S >= L, small-order points, malformed lengths, ...) as the
+    signatures of transactions, so they run through the signed-tx pipeline -- whose
+    leaf batches decode keys before their ids arrive (the prep's key half, then the
+    gather and the message half) -- each checked against the C oracle over its
+    transaction's id; then the per-transaction first failing signature."""
+    vs = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ed25519_vectors.json")))["vectors"]
+    rng = random.Random(61)
+    ntx = 400
+    txs = [[bytes(rng.getrandbits(8) for _ in range(n)) for n in (450, 150, 140, 43, 55)] for _ in range(ntx)]
+    ids, _ = engine.tx_ids(txs)
+    sigs, want = [], []
+    k = 0
+    for t in range(ntx):
+        per, st = [], []
+        for _ in range(rng.choice([1, 2, 3])):
+            v = vs[k % len(vs)]
+            k += 1
+            pub, sig = bytes.fromhex(v["pub"]), bytes.fromhex(v["sig"])
+            per.append((ED, pub, sig))
+            msg = ids[t].tobytes()
+            st.append(oracle.oracle_ed25519_verify(pub, len(pub), sig, len(sig), msg, len(msg)))
+        sigs.append(per)
+        want.append(st)
+    got_ids, tx_st, first_bad, sig_st = engine.signed_tx_verify(txs, sigs)
+    flat_want = [x for st in want for x in st]
+    assert [int(x) for x in sig_st] == flat_want
+    for t in range(ntx):
+        bad = [q for q, x in enumerate(want[t]) if x != 0]
+        assert int(first_bad[t]) == (bad[0] if bad else -1), t
+        assert int(tx_st[t]) == (want[t][bad[0]] if bad else 0), t
+    assert any(x == 3 for x in flat_want) and any(x == 1 for x in flat_want)  # bad keys and bad signatures ran
