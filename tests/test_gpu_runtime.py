@@ -286,10 +286,23 @@ k1 = [v for v in vs if v["scheme"] == 2][:150]
 r1 = [v for v in vs if v["scheme"] == 3][:173]
 rows = k1 + r1 + ed[:200]
 h = lambda x: bytes.fromhex(x)
+orc = load_oracle()
 with Engine(1) as eng:
     st, _ = eng.verify_batch([v.get("scheme", 4) for v in rows], [h(v["pub"]) for v in rows],
                              [h(v["sig"]) for v in rows], [h(v["msg"]) for v in rows])
+    # a signed-tx batch whose signature chunk spans several workspace launches: the first
+    # runs the prep's key half before the ids' gather, the later ones the fused prep
+    import random
+    rng = random.Random(7)
+    txs = [[bytes(rng.getrandbits(8) for _ in range(n)) for n in (45, 15, 14)] for _ in range(150)]
+    ids, _ = eng.tx_ids(txs)
+    sg = [[(4, h(ed[(2 * t + q) %% len(ed)]["pub"]), h(ed[(2 * t + q) %% len(ed)]["sig"])) for q in range(2)]
+          for t in range(len(txs))]
+    _, _, _, sst = eng.signed_tx_verify(txs, sg)
+    want_tx = [orc.oracle_ed25519_verify(k, len(k), s, len(s), ids[t].tobytes(), 32)
+               for t in range(len(txs)) for (_, k, s) in sg[t]]
 bad = [(i, int(s), v["status"]) for i, (v, s) in enumerate(zip(rows, st)) if int(s) != v["status"]]
+bad += [("tx", i, int(a), b) for i, (a, b) in enumerate(zip(sst, want_tx)) if int(a) != b]
 print(json.dumps({"n": len(rows), "bad": bad[:10]}))
 sys.exit(1 if bad else 0)
 """
