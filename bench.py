@@ -480,7 +480,7 @@ class C4:
                        "device_encode": self.device_encode}
         if self.device_encode:
             self.kernel = "kryo_size + scan + kryo_write + " + C4.kernel
-            # the encoder's L2-to-fabric bytes per tx (tools/gpu_r5n.sh -> pmc_kryo_traffic.py)
+            # the encoder's L2-to-fabric bytes per tx (tools/leases/gpu_r5n.sh -> tools/pmc_kryo_traffic.py)
             self.extra_pmc = ("r05_pmc_kryo_traffic.json", ntx)
             self.config["component_bytes_per_tx"] = round(self.d_blob.numel() / ntx, 1)
         if not self.native:
