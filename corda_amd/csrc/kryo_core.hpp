@@ -509,7 +509,8 @@ struct Reader {
     r.key = span(r.key_len);
     r.name_len = u16();
     r.name = span(r.name_len);
-    if (r.key_len == 0 || (r.name_len && (der_tlv_len(r.name, r.name_len) != r.name_len || r.name[0] != 0x30)))
+    // a truncated payload leaves name null with name_len set: test ok first
+    if (!ok || r.key_len == 0 || (r.name_len && (der_tlv_len(r.name, r.name_len) != r.name_len || r.name[0] != 0x30)))
       ok = false;
     return r;
   }

@@ -208,3 +208,58 @@ def test_unaligned_output_buffer(engine, shift):
     b = buf.cpu().numpy()
     assert (b[:shift] == 0xEE).all() and (b[shift + total:] == 0xEE).all()  # nothing outside the buffer
     assert _leaves(out, off, n) == host
+
+
+def test_malformed_composites_match_the_host_encoder(engine):
+    """Truncated and byte-flipped composite payloads (cash states, parties, issue
+    commands: the kinds whose payload the encoder parses) on the GPU against the host
+    encoder item by item: invalid exactly when the host rejects the item, otherwise
+    the same leaf. A truncated cash-state party once left its name pointer null with a
+    length set (found by tools/kryo_fuzz.cpp under ASan): the device reads of such
+    an item must stay inside its payload."""
+    rng = random.Random(31)
+    ref_keys = [bytes.fromhex(v["A"]) for v in TK._key_vectors()]
+    seeds = [("cash_state", TK._cash_state(rng, ref_keys, big=i % 5 == 0), 52) for i in range(10)]
+    seeds += [("party", TK._party(rng, ref_keys, big=i == 0), 50) for i in range(6)]
+    seeds += [("issue_command", ("net.corda.contracts.asset.Cash$Commands$Issue", rng.randrange(-2**63, 2**63),
+                                 [(45, rng.choice(ref_keys)) for _ in range(1 + i % 3)]), 10) for i in range(6)]
+    sblob, sarr, _ = _lib.kryo_pack(seeds)
+    parts, rows = [], []
+    pos = 0
+    for j, it in enumerate(sarr):
+        p = bytes(sblob[int(it["data"]):int(it["data"]) + int(it["len"])])
+        variants = []
+        cuts = range(len(p)) if j in (0, 10, 16) else sorted(rng.sample(range(len(p)), min(len(p), 24)))
+        variants += [p[:k] for k in cuts]
+        for _ in range(24):
+            q = bytearray(p)
+            for _ in range(rng.randrange(1, 4)):
+                q[rng.randrange(min(len(q), 16)) if rng.random() < 0.7 else rng.randrange(len(q))] ^= 1 << rng.randrange(8)
+            variants.append(bytes(q))
+        for v in variants:
+            r = it.copy()
+            r["data"], r["len"] = pos, len(v)
+            rows.append(r)
+            parts.append(v)
+            pos += len(v)
+    blob = np.frombuffer(b"".join(parts) + b"\0", np.uint8).copy()  # one spare byte: len-0 items point inside
+    arr = np.array(rows, dtype=sarr.dtype)
+    has = np.ones(len(arr), bool)
+    out, off, status = engine.kryo_encode_packed_device(blob, arr, has)
+    st = status.cpu().numpy()
+    got = _leaves(out, off, len(arr))
+    host_arr = arr.copy()
+    host_arr["data"] += np.uint64(blob.ctypes.data)
+    nbad = 0
+    for i in range(len(arr)):
+        try:
+            hb, _ = _lib.kryo_encode_array(host_arr[i:i + 1])
+            want = hb.tobytes()
+        except Exception:
+            want = None
+        if want is None:
+            nbad += 1
+            assert st[i] == 1 and got[i] == b"", i
+        else:
+            assert st[i] == 0 and got[i] == want, i
+    assert 0 < nbad < len(arr), (nbad, len(arr))
