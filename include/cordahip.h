@@ -89,6 +89,9 @@ int cordahip_free_pinned(cordahip_ctx* ctx, void* host);
 
 /* ---- generic signature batch (host memory) ------------------------------ *
  * Variable-length fields are CSR: item i's key is key[key_off[i] .. key_off[i+1]).
+ * Every CSR array in this header is the caller's contract, not checked: offsets
+ * non-decreasing and the last one within its buffer (the JVM binding builds
+ * them from its own arrays); lengths and contents are checked.
  * Key encodings: Ed25519 = the 32-byte A (Kryo wire form, Kryo.kt:386); ECDSA =
  * SEC1 point (the SPKI BIT STRING payload, Crypto.kt:348-355).
  * verdict (optional): bit (i % 64) of word (i / 64) = (status[i] == OK).
