@@ -19,7 +19,11 @@
 //      the direct encoder's leaf (the GPU's scheme against the direct encoder).
 // Exit 0 when every check holds; a sanitizer report aborts the process.
 //
-// usage: kryo_fuzz SEEDS_FILE ROUNDS RNG_SEED
+// usage: kryo_fuzz SEEDS_FILE ROUNDS RNG_SEED [--dump OUT]
+//   --dump: also write every mutant and the host encoder's result for it (kind u32,
+//   class_id u32, value i64, len u64, nbytes u64, has_data u8, payload; valid u8,
+//   leaf size u64, leaf) for the device encoder's agreement run
+//   (tools/agree_kryo_fuzz.py).
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -145,10 +149,12 @@ int fail(const char* what, uint64_t round, uint64_t i) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (argc != 4) {
-    std::fprintf(stderr, "usage: kryo_fuzz SEEDS ROUNDS RNG_SEED\n");
+  if (argc != 4 && !(argc == 6 && std::strcmp(argv[4], "--dump") == 0)) {
+    std::fprintf(stderr, "usage: kryo_fuzz SEEDS ROUNDS RNG_SEED [--dump OUT]\n");
     return 2;
   }
+  FILE* dump = argc == 6 ? std::fopen(argv[5], "wb") : nullptr;
+  if (argc == 6 && !dump) return fail("cannot open the dump file", 0, 0);
   std::vector<Seed> seeds;
   if (!read_seeds(argv[1], seeds)) return fail("bad seeds file", 0, 0);
   const uint64_t rounds = std::strtoull(argv[2], nullptr, 10);
@@ -168,6 +174,26 @@ int main(int argc, char** argv) {
     for (uint64_t i = 0; i < n; i++) {
       uint64_t off[2] = {7, 7};
       const int rc = cordahip_kryo_encode(&batch[i], 1, nullptr, 0, off);
+      if (dump) {
+        const cordahip_kryo_item& it = batch[i];
+        const uint64_t nbytes = it.data ? payload_bytes(it.kind, it.len) : 0;
+        const uint8_t has = it.data != nullptr;
+        std::fwrite(&it.kind, 4, 1, dump);
+        std::fwrite(&it.class_id, 4, 1, dump);
+        std::fwrite(&it.value, 8, 1, dump);
+        std::fwrite(&it.len, 8, 1, dump);
+        std::fwrite(&nbytes, 8, 1, dump);
+        std::fwrite(&has, 1, 1, dump);
+        if (nbytes) std::fwrite(it.data, 1, nbytes, dump);
+        const uint8_t valid = rc != CORDAHIP_ERR_INVALID_ARG;
+        const uint64_t size = valid ? off[1] : 0;
+        std::vector<uint8_t> leaf(size ? size : 1);
+        if (size && cordahip_kryo_encode(&it, 1, leaf.data(), size, off) != CORDAHIP_SUCCESS)
+          return fail("dump write", round, i);
+        std::fwrite(&valid, 1, 1, dump);
+        std::fwrite(&size, 8, 1, dump);
+        if (size) std::fwrite(leaf.data(), 1, size, dump);
+      }
       if (rc == CORDAHIP_ERR_INVALID_ARG) {
         all_ok = false;
         continue;
@@ -201,6 +227,7 @@ int main(int argc, char** argv) {
     shapes += st[0];
     bytes += total;
   }
+  if (dump) std::fclose(dump);
   std::printf("{\"rounds\": %llu, \"items\": %llu, \"valid\": %llu, \"templated\": %llu, \"shapes\": %llu, "
               "\"leaf_bytes\": %llu}\n",
               (unsigned long long)rounds, (unsigned long long)items, (unsigned long long)valid,
