@@ -496,7 +496,6 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batc
     // (the full chain's two slice buffers are bounded at 4 KB + 4 B per payload byte per
     // component: ~1.4 GB each for C4's 2^17-signature slices)
     cp->templates_only = cp->templates_only && d.kryo_templates_ok;
-    leaf_buf = cp->templates_only ? 0 : 2 * cp->slice_cap;
     if (w.comp_items.ensure(std::max<uint64_t>(nleaves, 1) * sizeof(cordahip_kryo_item)) ||
         w.payload.ensure(std::max<uint64_t>(ns ? cp->pay_end.back() : 0, 16)) ||
         w.comp_status.ensure(std::max<uint64_t>(nleaves, 1)))
@@ -516,6 +515,11 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batc
     if (hipError_t e = kryo_state_ready(d, d.stream)) return e;
     if (hipError_t e = kryo_reset_misses(d.kryo_fixed.as<uint8_t>(), d.stream)) return e;
     cp->templates_only = cp->templates_only && d.kryo_templates_ok;  // kryo_state_ready may have cleared the table
+    // sized after that: a cleared table runs the full chain, which writes leaves
+    leaf_buf = cp->templates_only ? 0 : 2 * cp->slice_cap;
+    if (tracing())
+      fprintf(stderr, "[cordahip] dev %d component call: %s chain (templates %u, slots %u in use)\n", d.id,
+              cp->templates_only ? "templates-only" : "full encoder", d.kryo_usage[0], d.kryo_usage[1]);
   } else {
     leaf_buf = b->leaf_off[l1] - b->leaf_off[l0];
   }
@@ -848,6 +852,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
     // a templates-only call with any is void; a full call without any lets the next
     // call on this device take the templates-only chain
     const uint32_t misses = static_cast<const volatile uint32_t*>(d.kryo_usage)[2];
+    if (tracing()) fprintf(stderr, "[cordahip] dev %d component call: %u encoder misses\n", d.id, misses);
     if (cp->templates_only && misses) {
       d.kryo_templates_ok = false;
       return kRedoFull;
@@ -883,6 +888,9 @@ int signed_tx_device(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batc
     return !(v && v[0] == '0');
   }();
   const int r = signed_tx_device_once(ctx, d, b, tx_of, lo, hi, slices, comps, comps && spec);
+  if (r == kRedoFull && tracing())
+    fprintf(stderr, "[cordahip] dev %d component call: templates-only chain missed, redone with the full encoder\n",
+            d.id);
   return r == kRedoFull ? signed_tx_device_once(ctx, d, b, tx_of, lo, hi, slices, comps, false) : r;
 }
 

@@ -22,7 +22,8 @@
 // usage: kryo_fuzz SEEDS_FILE ROUNDS RNG_SEED [--dump OUT]
 //   --dump: also write every mutant and the host encoder's result for it (kind u32,
 //   class_id u32, value i64, len u64, nbytes u64, has_data u8, payload; valid u8,
-//   leaf size u64, leaf) for the device encoder's agreement run
+//   leaf size u64, leaf, templated u8 (the item alone rebuilds from a template, or a
+//   valid RAW item), shape hash u64 (0: none), exact-shape fingerprint u64) for the device encoder's agreement run
 //   (tools/agree_kryo_fuzz.py).
 #include <cstdint>
 #include <cstdio>
@@ -31,7 +32,7 @@
 #include <memory>
 #include <vector>
 
-#include "../include/cordahip.h"
+#include "../corda_amd/csrc/kryo_template.hpp"
 
 extern "C" int kryo_template_check(const cordahip_kryo_item* items, uint64_t n, uint64_t cap_syms, uint64_t* stats);
 
@@ -193,6 +194,31 @@ int main(int argc, char** argv) {
         std::fwrite(&valid, 1, 1, dump);
         std::fwrite(&size, 8, 1, dump);
         if (size) std::fwrite(leaf.data(), 1, size, dump);
+        uint64_t tst[6], h = 0;
+        // 4096: the GPU arena's template size (kryo_device.hip kTmplSyms)
+        const bool templ = kryo_template_check(&it, 1, 4096, tst) == 0 && tst[1] == 1;
+        const uint8_t tb = templ || (valid && it.kind == CORDAHIP_KRYO_RAW);
+        if (!cordahip::kryo::shape_hash_of(it, h)) h = 0;
+        // the exact shape (the record the GPU compares), FNV-1a over its used part: two
+        // shapes under one hash make the second one go direct
+        uint64_t fp = 1469598103934665603ull;
+        if (h) {
+          cordahip::kryo::ShapeRec rec;
+          std::memset(&rec, 0, sizeof rec);
+          cordahip::kryo::ShapeRecord rv(rec);
+          cordahip::kryo::shape_walk(it, rv);
+          auto mix = [&](const void* p, size_t nb) {
+            for (size_t q = 0; q < nb; q++) fp = (fp ^ static_cast<const uint8_t*>(p)[q]) * 1099511628211ull;
+          };
+          mix(&rec.nw, 16);
+          mix(rec.w, 4 * (rec.nw < rec.kWords ? rec.nw : rec.kWords));
+          mix(rec.sl, 4 * (rec.ns < rec.kSpans ? rec.ns : rec.kSpans));
+          mix(rec.so, 4 * (rec.ns < rec.kSpans ? rec.ns : rec.kSpans));
+          mix(rec.bytes, rec.nb < rec.kBytes ? rec.nb : rec.kBytes);
+        }
+        std::fwrite(&tb, 1, 1, dump);
+        std::fwrite(&h, 8, 1, dump);
+        std::fwrite(&fp, 8, 1, dump);
       }
       if (rc == CORDAHIP_ERR_INVALID_ARG) {
         all_ok = false;
