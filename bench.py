@@ -794,10 +794,17 @@ class C4H(C4):
         ar = np.arange(ns + 1, dtype=np.uint64)
         sig_arrays = (np.full(ns, 4, np.uint8), self.keys.cpu().numpy().reshape(-1), ar * 32,
                       self.sigs.cpu().numpy().reshape(-1), ar * 64)
-        self.h_txid = _pinned(np.zeros((ntx, 32), np.uint8))
-        self.h_txst = _pinned(np.zeros(ntx, np.uint8))
-        self.h_sst = _pinned(np.zeros(ns, np.uint8))
-        self.h_fb = _pinned(np.zeros(ntx, np.int64))
+        # --inflight K: up to K calls outstanding (the JVM submitting consecutive
+        # ResolveTransactionsFlow batches), each with its own output arrays; a step
+        # submits one call, waiting first for the oldest when K are outstanding
+        self.inflight = max(1, int(getattr(args, "inflight", 1) or 1))
+        self.outs = [tuple(_pinned(x) for x in (np.zeros((ntx, 32), np.uint8), np.zeros(ntx, np.uint8),
+                                                np.zeros(ns, np.uint8), np.zeros(ntx, np.int64)))
+                     for _ in range(self.inflight)]
+        self.h_txid, self.h_txst, self.h_sst, self.h_fb = self.outs[0]
+        self.pending = []  # (ticket, slot), oldest first
+        self.next_slot = 0
+        self.bs = []
         if self.components:
             # what the JVM hands over instead of leaves: the Kryo items (data = offsets into the
             # payload) and the payload blob -- the corrupted owner keys included
@@ -806,9 +813,10 @@ class C4H(C4):
             self.t = [_pinned(x) for x in (items.view(np.uint8), np.arange(0, 5 * ntx + 1, 5, dtype=np.uint64),
                                            payload, self.tx_sig_off.cpu().numpy().astype(np.uint64)) + sig_arrays]
             p = [x.data_ptr() for x in self.t]
-            tb = _lib.TxcompBatch(ntx, p[0], p[1], p[2], payload.size, self.h_txid.data_ptr(), self.h_txst.data_ptr())
-            self.b = _lib.SignedTxcompBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], self.h_sst.data_ptr(),
-                                            self.h_fb.data_ptr())
+            for txid, txst, sst, fb in self.outs:
+                tb = _lib.TxcompBatch(ntx, p[0], p[1], p[2], payload.size, txid.data_ptr(), txst.data_ptr())
+                self.bs.append(_lib.SignedTxcompBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], sst.data_ptr(),
+                                                      fb.data_ptr()))
             self.pcie_tx_bytes = (items.nbytes + 8 * (5 * ntx + 1) + payload.size) / ntx
             what = ("the components of each tx (cordahip_txcomp_submit: %.0f B per tx of Kryo items and payload; "
                     "the GPU writes the %.0f B of leaves)" % (self.pcie_tx_bytes, self.leaf_bytes.numel() / ntx))
@@ -820,9 +828,10 @@ class C4H(C4):
                 self.tx_leaf_off.cpu().numpy().astype(np.uint64), self.tx_sig_off.cpu().numpy().astype(np.uint64))
                 + sig_arrays]
             p = [x.data_ptr() for x in self.t]
-            tb = _lib.TxidBatch(ntx, p[0], p[1], p[2], self.h_txid.data_ptr(), self.h_txst.data_ptr())
-            self.b = _lib.SignedTxBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], self.h_sst.data_ptr(),
-                                        self.h_fb.data_ptr())
+            for txid, txst, sst, fb in self.outs:
+                tb = _lib.TxidBatch(ntx, p[0], p[1], p[2], txid.data_ptr(), txst.data_ptr())
+                self.bs.append(_lib.SignedTxBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], sst.data_ptr(),
+                                                  fb.data_ptr()))
             self.pcie_tx_bytes = (self.leaf_bytes.numel() + 8 * (self.leaf_off.numel() + ntx + 1)) / ntx
             what = ("native Kryo leaves, %.0f B per tx" % (self.leaf_bytes.numel() / ntx) if self.native
                     else "5 leaves of %s B" % list(C4_LEAF_LENS))
@@ -831,25 +840,46 @@ class C4H(C4):
                          % ("cordahip_txcomp_submit" if self.components else "cordahip_tx_submit", ntx, what))
         self.config = dict(self.config, boundary=("cordahip_txcomp_submit" if self.components else "cordahip_tx_submit")
                            + " + cordahip_wait", host_memory="pinned CSR", components=self.components,
-                           pcie_id_bytes_per_tx=round(self.pcie_tx_bytes, 1))
+                           pcie_id_bytes_per_tx=round(self.pcie_tx_bytes, 1), inflight=self.inflight)
+        if self.inflight > 1:
+            self.workload += ("; up to %d calls outstanding (a step submits one; the timed region ends when every "
+                              "call it submitted has completed)" % self.inflight)
+
+    def _wait_oldest(self):
+        import ctypes  # noqa: F401
+        from corda_amd._lib import check, lib
+        t, _ = self.pending.pop(0)
+        check(lib().cordahip_wait(self.eng.ctx, t, -1), "cordahip_wait")
 
     def step(self):
         import ctypes
         from corda_amd._lib import check, lib
+        if len(self.pending) >= self.inflight:
+            self._wait_oldest()
+        busy = {k for _, k in self.pending}
+        slot = next(k for k in range(self.inflight) if k not in busy)
         t = ctypes.c_uint64()
         submit = lib().cordahip_txcomp_submit if self.components else lib().cordahip_tx_submit
-        check(submit(self.eng.ctx, ctypes.byref(self.b), ctypes.byref(t)), "cordahip_tx(comp)_submit")
-        check(lib().cordahip_wait(self.eng.ctx, t.value, -1), "cordahip_wait")
+        check(submit(self.eng.ctx, ctypes.byref(self.bs[slot]), ctypes.byref(t)), "cordahip_tx(comp)_submit")
+        self.pending.append((t.value, slot))
+
+    def drain(self):
+        while self.pending:
+            self._wait_oldest()
 
     def check(self):
-        import torch
+        import torch  # noqa: F401
+        self.drain()
         exp_st = self.exp_status.cpu()
         exp_bad = self.exp_bad.cpu()
         C4.step(self)  # the device-resident path over the same bytes: its ids
         self.torch.cuda.synchronize(self.device)
         txid = self.txid.cpu()
-        out = {"mismatches_vs_construction": int((self.h_txst != exp_st).sum()) + int((self.h_fb != exp_bad).sum()),
-               "txid_mismatches_vs_device_path": int((self.h_txid != txid).any(dim=1).sum()),
+        # every output set (one per outstanding call) against the construction and the device path
+        out = {"mismatches_vs_construction": sum(int((st != exp_st).sum()) + int((fb != exp_bad).sum())
+                                                 for _, st, _, fb in self.outs),
+               "txid_mismatches_vs_device_path": sum(int((ti != txid).any(dim=1).sum()) for ti, _, _, _ in self.outs),
+               "output_sets_checked": len(self.outs),
                "accepted_txs": int((self.h_txst == 0).sum()), "txs": self.ntx, "sigs": self.ns}
         if self.components:  # the device path's leaves against the host encoder (C4 --device-encode's check)
             dev = C4.check(self)
@@ -1001,6 +1031,8 @@ def parse_args(argv=None):
     ap.add_argument("--device-encode", action="store_true",
                     help="c4: native leaves encoded on the GPU every step from the components in HBM "
                          "(cordahip_kryo_encode_device; implies --native-leaves)")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="c4h: calls outstanding at once (consecutive batches overlap on the device)")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock sampling step")
@@ -1090,9 +1122,16 @@ def main():
         if world > 1 and verdict is not None:
             gather_verdicts(verdict, world)  # the only data-path collective (RCCL all-gather)
 
+    drain = getattr(wl, "drain", None)  # workloads with calls outstanding (c4h --inflight)
+
+    def sync_all():
+        if drain is not None:
+            drain()
+        sync()
+
     for _ in range(args.warmup):
         step()
-    sync()
+    sync_all()
     if world > 1:
         dist.barrier()
     sync()
@@ -1101,7 +1140,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(*evs[k])
-    sync()
+    sync_all()  # every call the timed steps submitted has completed
     if world > 1:
         dist.barrier()
     sync()
@@ -1121,7 +1160,7 @@ def main():
     # the shader clock this box holds under this workload (one more, untimed step)
     clock = None
     if not stub and not args.no_clock:
-        clock = _clock_under_load(local_rank, step, sync, elapsed * 1e3 / args.steps)
+        clock = _clock_under_load(local_rank, step, sync_all, elapsed * 1e3 / args.steps)
     chk = wl.check()
     elapsed = max_over_ranks(elapsed, device)
     for key in ("mismatches_vs_construction", "mismatches_vs_oracle_open_lanes"):

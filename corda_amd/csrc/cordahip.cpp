@@ -212,32 +212,55 @@ uint64_t env_lanes(const char* name, uint64_t dflt) {
   return x >= 64 ? x / 64 * 64 : dflt;
 }
 
+// a zeroed 64-byte host-mapped buffer (the encoder's usage reports)
+hipError_t usage_buffer(uint32_t*& h, uint32_t*& dp) {
+  if (h) return hipSuccess;
+  void* hp = nullptr;
+  void* dv = nullptr;
+  if (hipHostMalloc(&hp, 64, hipHostMallocMapped) != hipSuccess) return hipErrorOutOfMemory;
+  if (hipHostGetDevicePointer(&dv, hp, 0) != hipSuccess) {
+    (void)hipHostFree(hp);
+    return hipErrorUnknown;
+  }
+  std::memset(hp, 0, 64);
+  h = static_cast<uint32_t*>(hp);
+  dp = static_cast<uint32_t*>(dv);
+  return hipSuccess;
+}
+
 // The Kryo encoder's persistent state ready for a call on stream s (kryo_mu
 // held, d.kryo_fixed allocated): zeroed when freshly allocated; cleared when the
-// usage the last call reported passes half the table or nearly fills the
-// template arena (recurring shapes then rebuild once).
+// usage a call reported passes half the table or nearly fills the template
+// arena (recurring shapes then rebuild once). The reports are snapshots of
+// counters that only grow between clears, so the largest one is the latest; a
+// report may lag by the calls still running (cordahip_kryo_encode_device's is
+// read without waiting for its stream): the table then clears one call later,
+// and until then new shapes take the direct encoder -- slower, never wrong.
 hipError_t kryo_state_ready(Device& d, hipStream_t s) {
-  if (!d.kryo_usage) {
-    void* h = nullptr;
-    void* dp = nullptr;
-    if (hipHostMalloc(&h, 64, hipHostMallocMapped) != hipSuccess) return hipErrorOutOfMemory;
-    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) return hipErrorUnknown;
-    std::memset(h, 0, 64);
-    d.kryo_usage = static_cast<uint32_t*>(h);
-    d.kryo_usage_dev = static_cast<uint32_t*>(dp);
-  }
-  const volatile uint32_t* u = d.kryo_usage;
-  if (d.kryo_fresh || u[0] > kryo_clear_threshold_templates() || u[1] > kryo_clear_threshold_slots()) {
+  if (hipError_t e = usage_buffer(d.kryo_usage, d.kryo_usage_dev)) return e;
+  uint32_t templates = 0, slots = 0;
+  for (const uint32_t* p : {(const uint32_t*)d.kryo_usage, (const uint32_t*)d.set[0].kryo_usage,
+                            (const uint32_t*)d.set[1].kryo_usage})
+    if (p) {
+      const volatile uint32_t* u = p;
+      templates = std::max<uint32_t>(templates, (uint32_t)u[0]);
+      slots = std::max<uint32_t>(slots, (uint32_t)u[1]);
+    }
+  if (d.kryo_fresh || templates > kryo_clear_threshold_templates() || slots > kryo_clear_threshold_slots()) {
     d.kryo_fresh = false;
     d.kryo_templates_ok = false;  // an empty table: the next component batch builds its shapes
-    d.kryo_usage[0] = d.kryo_usage[1] = 0;
+    d.kryo_gen++;                 // a call that started before the clear does not vouch for the new table
+    for (uint32_t* p : {d.kryo_usage, d.set[0].kryo_usage, d.set[1].kryo_usage})
+      if (p) p[0] = p[1] = 0;
     return kryo_clear(d.kryo_fixed.as<uint8_t>(), s);
   }
   return hipSuccess;
 }
-// after a call's encoder launches: its usage counters to the host-mapped copy
-hipError_t kryo_usage_report(Device& d, hipStream_t s) {
-  return launch_store_to_host(kryo_usage_src(d.kryo_fixed.as<uint8_t>()), d.kryo_usage_dev, kKryoUsageBytes, s);
+// after a call's encoder launches: its usage counters to the host-mapped copy of
+// its set (nullptr: cordahip_kryo_encode_device's own)
+hipError_t kryo_usage_report(Device& d, TxSet* set, hipStream_t s) {
+  return launch_store_to_host(kryo_usage_src(d.kryo_fixed.as<uint8_t>()),
+                              set ? set->kryo_usage_dev : d.kryo_usage_dev, kKryoUsageBytes, s);
 }
 // grows kryo_fixed if needed (once: its size is fixed), marking it fresh
 hipError_t kryo_fixed_ensure(Device& d) {
@@ -364,11 +387,11 @@ TimedCall* timed_begin(Device& d, hipStream_t s) {
   return tc;
 }
 
-// Acquire d.tx for a host tx path (tx_mu held): the last device-path user may
-// still be running kernels on its own stream.
-int tx_acquire_host(Device& d) {
+// A leased set's buffers for a host tx path: the last device-path user of the
+// set may still be running kernels on its own stream.
+int tx_acquire_host(Device& d, TxSet& set) {
   if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
-  if (hipEventSynchronize(d.tx_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
+  if (hipEventSynchronize(set.tx_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
   return CORDAHIP_SUCCESS;
 }
 
@@ -377,13 +400,14 @@ int tx_acquire_host(Device& d) {
 // kernels get base pointers shifted by the shard's first byte / first leaf.
 int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uint64_t t0, uint64_t t1) {
   (void)ctx;
-  std::lock_guard<std::mutex> g(d.tx_mu);
-  if (int rc = tx_acquire_host(d)) return rc;
+  SetLease lease(d);
+  TxSet& S = lease.get();
+  if (int rc = tx_acquire_host(d, S)) return rc;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1];
   const uint64_t nleaves = l1 - l0;
   const uint64_t b0 = b->leaf_off[l0], b1 = b->leaf_off[l1];
-  TxWork& w = d.tx;
+  TxWork& w = S.tx;
   if (w.leaf_bytes.ensure(std::max<uint64_t>(b1 - b0, 16)) || w.leaf_off.ensure((nleaves + 1) * 8) ||
       w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
       w.txid.ensure(ntx * 32) || w.tx_status.ensure(ntx))
@@ -401,8 +425,9 @@ int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uin
                                  w.tx_status.as<uint8_t>(), s);
   e = e ? e : hipMemcpyAsync(b->txid + t0 * 32, w.txid.p, ntx * 32, hipMemcpyDeviceToHost, s);
   e = e ? e : hipMemcpyAsync(b->tx_status + t0, w.tx_status.p, ntx, hipMemcpyDeviceToHost, s);
-  e = e ? e : hipEventRecord(d.tx_ev, s);
-  e = e ? e : hipEventSynchronize(d.tx_ev);
+  e = e ? e : hipEventRecord(S.tx_ev, s);
+  e = e ? e : hipEventSynchronize(S.tx_ev);
+  if (e != hipSuccess) (void)hipStreamSynchronize(s);
   return hip_err(e);
 }
 
@@ -416,7 +441,7 @@ int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
 }
 
 // The tx ids of one device's shard, in slices on the device's context stream
-// (d.tx_mu held, the previous users of d.tx finished): slice j's leaf bytes and
+// (the set S leased, its previous users finished): slice j's leaf bytes and
 // offsets go H2D into their region of whole-shard buffers (offset arrays
 // unchanged, shifted base pointers) on d.s_idcopy, followed by cev[j]; its
 // SHA-256 and Merkle kernels run on the context stream behind cev[j], then
@@ -449,11 +474,11 @@ struct CompPlan {
   static constexpr uint64_t kDirectWriters = 1u << 13;  // the direct encoder's writers (rarely any work)
 };
 
-hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound,
-                          CompPlan* cp) {
+hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, TxSet& S, int set_idx, const cordahip_txid_batch* b,
+                          const std::vector<uint64_t>& bound, CompPlan* cp) {
   const uint64_t t0 = bound.front(), t1 = bound.back(), ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
-  TxWork& w = d.tx;
+  TxWork& w = S.tx;
   uint64_t leaf_buf = 0;
   if (cp) {
     const cordahip_txcomp_batch* c = cp->c;
@@ -512,14 +537,15 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batc
           kryo_fixed_ensure(d))
         return hipErrorOutOfMemory;
     }
+    if (hipError_t e = usage_buffer(S.kryo_usage, S.kryo_usage_dev)) return e;
     if (hipError_t e = kryo_state_ready(d, d.stream)) return e;
-    if (hipError_t e = kryo_reset_misses(d.kryo_fixed.as<uint8_t>(), d.stream)) return e;
+    if (hipError_t e = kryo_reset_misses(d.kryo_fixed.as<uint8_t>(), (uint32_t)set_idx, d.stream)) return e;
     cp->templates_only = cp->templates_only && d.kryo_templates_ok;  // kryo_state_ready may have cleared the table
     // sized after that: a cleared table runs the full chain, which writes leaves
     leaf_buf = cp->templates_only ? 0 : 2 * cp->slice_cap;
     if (tracing())
-      fprintf(stderr, "[cordahip] dev %d component call: %s chain (templates %u, slots %u in use)\n", d.id,
-              cp->templates_only ? "templates-only" : "full encoder", d.kryo_usage[0], d.kryo_usage[1]);
+      fprintf(stderr, "[cordahip] dev %d set %d component call: %s chain (templates %u, slots %u in use)\n", d.id,
+              set_idx, cp->templates_only ? "templates-only" : "full encoder", S.kryo_usage[0], S.kryo_usage[1]);
   } else {
     leaf_buf = b->leaf_off[l1] - b->leaf_off[l0];
   }
@@ -530,12 +556,13 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, const cordahip_txid_batc
   return hipSuccess;
 }
 
-hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::vector<uint64_t>& bound, size_t j0,
-                          size_t j1, std::vector<hipEvent_t>& ev, std::vector<hipEvent_t>& cev,
-                          std::vector<hipEvent_t>& kev, uint8_t* map_txid, uint8_t* map_status, CompPlan* cp) {
+hipError_t tx_ids_enqueue(Device& d, TxSet& S, int set_idx, const cordahip_txid_batch* b,
+                          const std::vector<uint64_t>& bound, size_t j0, size_t j1, std::vector<hipEvent_t>& ev,
+                          std::vector<hipEvent_t>& cev, std::vector<hipEvent_t>& kev, uint8_t* map_txid,
+                          uint8_t* map_status, CompPlan* cp) {
   const uint64_t t0 = bound.front();
   const uint64_t l0 = b->tx_leaf_off[t0], b0 = cp ? 0 : b->leaf_off[l0];
-  TxWork& w = d.tx;
+  TxWork& w = S.tx;
   hipStream_t s = d.stream, sc = d.s_idcopy ? d.s_idcopy : d.stream;
   const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
   const uint8_t* bytes_base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(w.leaf_bytes.p) - b0);
@@ -577,7 +604,7 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
       uint8_t* cst = w.comp_status.as<uint8_t>() + (ls0 - l0);
       e = e ? e : launch_kryo_shape(it, w.payload.as<uint8_t>(), cp->c->payload_len, n, cp->group[j],
                                     d.kryo_fixed.as<uint8_t>(), slots, slots + n, d.kryo_sizes.as<uint64_t>(), cst, s,
-                                    true);
+                                    true, (uint32_t)set_idx);
       e = e ? e : launch_kryo_hash(it, w.payload.as<uint8_t>(), cp->c->payload_len, n, cp->group[j],
                                    d.kryo_fixed.as<uint8_t>(), slots, d.kryo_sizes.as<uint64_t>(), cst,
                                    w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
@@ -591,7 +618,8 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
                                      cp->c->payload_len, n, cp->group[j], d.kryo_fixed.as<uint8_t>(), slots, slots + n,
                                      d.kryo_sizes.as<uint64_t>(), w.leaf_off.as<uint64_t>() + (ls0 - l0), sb,
                                      cp->slice_cap, w.comp_status.as<uint8_t>() + (ls0 - l0), d.kryo_ws.as<uint8_t>(),
-                                     CompPlan::kDirectWriters, d.kryo_temp.p, d.kryo_temp.cap, s, cp->templates_only);
+                                     CompPlan::kDirectWriters, d.kryo_temp.p, d.kryo_temp.cap, s, cp->templates_only,
+                                     (uint32_t)set_idx);
       e = e ? e : launch_sha256_leaves(sb, w.leaf_off.as<uint64_t>() + (ls0 - l0), n,
                                        w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
     } else {
@@ -623,9 +651,12 @@ hipError_t tx_ids_enqueue(Device& d, const cordahip_txid_batch* b, const std::ve
     e = e ? e : hipEventRecord(ev[j], s);
   }
   if (e == hipSuccess && j1 + 1 == bound.size()) {
-    e = hipEventRecord(d.tx_ev, s);  // the last slice: fence d.tx
-    if (cp && e == hipSuccess) {     // and the encoder's scratch (d.kryo_*)
-      e = kryo_usage_report(d, s);
+    // the last slice: the encoder's usage report, then the fences of the set's
+    // buffers (S.tx_ev: the call's drain waits on it) and of the encoder's
+    // scratch (d.kryo_*)
+    if (cp) e = kryo_usage_report(d, &S, s);
+    e = e ? e : hipEventRecord(S.tx_ev, s);
+    if (cp && e == hipSuccess) {
       if (!d.kryo_ev) e = e ? e : hipEventCreateWithFlags(&d.kryo_ev, hipEventDisableTiming);
       e = e ? e : hipEventRecord(d.kryo_ev, s);
     }
@@ -679,22 +710,36 @@ void reduce_txs(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b, uint64_t t
 // host. (r03 waited for each slice's ids on the host and copied them back as
 // messages: the GPU sat idle ~5 ms per C4 step until the first signatures were
 // packed.)
+// Consecutive calls on one device overlap (r06): a call holds one of the
+// device's two buffer sets (SetLease: ids, leaf / component buffers, the
+// signature stages) from start to finish, but the device's enqueue token
+// (tx_order_mu) -- and, for component batches, the encoder's scratch lock
+// (kryo_mu) -- only until its last signature chunk and id slice are enqueued.
+// The next call then packs and enqueues its first slices and chunks while this
+// one drains (its last chunks' ladders, the statuses, the per-tx reduce), so
+// the GPU no longer idles through each call's fill (the first slice's leaf
+// bytes and pack) and drain. Work reaches the shared streams in call order; a
+// call's drain waits on its own events, never on the streams.
 constexpr int kRedoFull = -1000;  // a templates-only component call missed: run it again with the full encoder
 
 int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx_batch* b, uint64_t* tx_of,
                           uint64_t lo, uint64_t hi, uint64_t slices, const cordahip_txcomp_batch* comps,
                           bool templates_only) {
-  std::lock_guard<std::mutex> g(d.tx_mu);  // d.tx (the ids) stays ours until every gather has run
-  // component batches also use the GPU encoder's scratch (d.kryo_*) for the whole call
+  SetLease lease(d);  // S.tx (the ids) and S.pb stay ours until every gather has run
+  TxSet& S = lease.get();
+  const int set_idx = lease.index();
+  std::unique_lock<std::mutex> tok(d.tx_order_mu);
+  // component batches also enqueue on the GPU encoder's shared scratch (d.kryo_*)
   std::unique_lock<std::mutex> gk(d.kryo_mu, std::defer_lock);
   CompPlan plan, *cp = nullptr;
+  uint64_t gen = 0;
   if (comps) {
     gk.lock();
     plan.c = comps;
     plan.templates_only = templates_only;
     cp = &plan;
   }
-  int r = tx_acquire_host(d);
+  int r = tx_acquire_host(d, S);
   if (r == CORDAHIP_SUCCESS && ensure_streams(d) != hipSuccess) r = CORDAHIP_ERR_HIP;
   if (r == CORDAHIP_SUCCESS && cp && d.kryo_ev && hipStreamWaitEvent(d.stream, d.kryo_ev, 0) != hipSuccess)
     r = CORDAHIP_ERR_HIP;  // an earlier cordahip_kryo_encode_device still using the scratch
@@ -764,12 +809,26 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
     const size_t j1 = std::min<size_t>(slices, j + 1);
     hipError_t e = hipSuccess;
     if (j1 > issued)
-      e = tx_ids_enqueue(d, &b->tx, di.tx_bound, issued, j1, ev, cev, di.ready, map_txid, map_status, cp);
+      e = tx_ids_enqueue(d, S, set_idx, &b->tx, di.tx_bound, issued, j1, ev, cev, di.ready, map_txid, map_status, cp);
     issued = std::max(issued, j1);
     return e;
   };
-  if (r == CORDAHIP_SUCCESS && tx_ids_prepare(ctx, d, &b->tx, di.tx_bound, cp) != hipSuccess)
+  // the end of this call's enqueues: the slices no signature asked for
+  // (transactions without signatures at the end), then the token and the
+  // encoder's scratch go to the next call (idempotent: called by the pipeline
+  // once its last chunk is enqueued, and after it)
+  bool handed_on = false;
+  auto hand_on = [&]() -> hipError_t {
+    if (handed_on) return hipSuccess;
+    handed_on = true;
+    const hipError_t e = issue_through(slices);
+    if (gk.owns_lock()) gk.unlock();
+    if (tok.owns_lock()) tok.unlock();
+    return e;
+  };
+  if (r == CORDAHIP_SUCCESS && tx_ids_prepare(ctx, d, S, set_idx, &b->tx, di.tx_bound, cp) != hipSuccess)
     r = CORDAHIP_ERR_OUT_OF_MEMORY;
+  if (cp) gen = d.kryo_gen;  // after a clear in prepare: this call builds the new table's shapes
   if (r == CORDAHIP_SUCCESS && issue_through(0) != hipSuccess) r = CORDAHIP_ERR_HIP;
   // each signature signs its transaction's id (SignedTransaction.kt:98): the
   // pipeline finds it through tx_of, filled chunk by chunk just ahead of its use
@@ -791,7 +850,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
   };
   std::vector<std::pair<uint64_t, uint64_t>> reduced;  // tx ranges the chunks reduced
   if (r == CORDAHIP_SUCCESS && s1 > s0) {
-    di.txid = d.tx.txid.as<uint8_t>();
+    di.txid = S.tx.txid.as<uint8_t>();
     di.t0 = lo;
     di.split_prep = cp == nullptr;
     // before a chunk's copies: the slices it needs; after them: `lookahead` more,
@@ -804,6 +863,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
       const size_t j = (size_t)(std::upper_bound(di.tx_bound.begin(), di.tx_bound.end(), tx) - di.tx_bound.begin()) - 1;
       return issue_through(j);
     };
+    di.enqueued = hand_on;
     // each finished chunk reduces the transactions whose signatures it holds
     // entirely (once their ids are on the host), overlapped with later chunks'
     // GPU work: the whole-batch pass after the drain was ~0.55 ms of a 32 ms
@@ -832,7 +892,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
     cordahip_sig_batch sb{b->tx_sig_off[b->tx.ntx], b->scheme, b->key, b->key_off, b->sig, b->sig_off, b->tx.txid,
                           nullptr, b->sig_status, nullptr, 0u};
     try {
-      r = sig_verify_range(ctx, d, &sb, mv, s0, s1);
+      r = sig_verify_range(ctx, d, S, &sb, mv, s0, s1);
     } catch (const std::bad_alloc&) {
       r = CORDAHIP_ERR_OUT_OF_MEMORY;
     } catch (...) {
@@ -840,24 +900,41 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
     }
   }
   const double tr0 = tracing() ? now_ms() : 0;
-  // slices no signature asked for (transactions without signatures at the end)
-  if (r == CORDAHIP_SUCCESS && issue_through(slices) != hipSuccess) r = CORDAHIP_ERR_HIP;
-  // every slice writes the caller's txid / tx_status: drain before returning, errors included
-  const hipError_t e1 = hipStreamSynchronize(d.s_idcopy ? d.s_idcopy : d.stream), e2 = hipStreamSynchronize(d.stream);
+  // slices no signature asked for; the token goes on (if the pipeline did not hand
+  // it on; after an error nothing more is enqueued)
+  if (r == CORDAHIP_SUCCESS) {
+    if (hand_on() != hipSuccess) r = CORDAHIP_ERR_HIP;
+  } else {
+    handed_on = true;
+    if (gk.owns_lock()) gk.unlock();
+    if (tok.owns_lock()) tok.unlock();
+  }
+  // every slice writes the caller's txid / tx_status: drain before returning,
+  // errors included. S.tx_ev follows the last slice (and the encoder's usage
+  // report) on the id stream, after every earlier slice; the id copies on
+  // s_idcopy precede their slices' kernels. After an error the streams
+  // themselves are drained.
+  hipError_t e1 = hipSuccess;
+  if (r == CORDAHIP_SUCCESS) e1 = hipEventSynchronize(S.tx_ev);
+  if (r != CORDAHIP_SUCCESS || e1 != hipSuccess) {
+    (void)hipStreamSynchronize(d.s_idcopy ? d.s_idcopy : d.stream);
+    (void)hipStreamSynchronize(d.stream);
+  }
   const double tr1 = tracing() ? now_ms() : 0;
-  if (r == CORDAHIP_SUCCESS && (e1 != hipSuccess || e2 != hipSuccess)) r = CORDAHIP_ERR_HIP;
+  if (r == CORDAHIP_SUCCESS && e1 != hipSuccess) r = CORDAHIP_ERR_HIP;
   if (r != CORDAHIP_SUCCESS) return r;
   if (cp) {
-    // the encoder's misses in this call (kryo_usage_report ran on d.stream, drained above):
-    // a templates-only call with any is void; a full call without any lets the next
-    // call on this device take the templates-only chain
-    const uint32_t misses = static_cast<const volatile uint32_t*>(d.kryo_usage)[2];
-    if (tracing()) fprintf(stderr, "[cordahip] dev %d component call: %u encoder misses\n", d.id, misses);
+    // the encoder's misses in this call (this set's counter, reported after its last
+    // slice, drained above): a templates-only call with any is void; a full call
+    // without any lets the next call on this device take the templates-only chain
+    const uint32_t misses = static_cast<const volatile uint32_t*>(S.kryo_usage)[2 + set_idx];
+    if (tracing()) fprintf(stderr, "[cordahip] dev %d set %d component call: %u encoder misses\n", d.id, set_idx, misses);
+    std::lock_guard<std::mutex> g(d.kryo_mu);
     if (cp->templates_only && misses) {
       d.kryo_templates_ok = false;
       return kRedoFull;
     }
-    d.kryo_templates_ok = misses == 0;
+    if (d.kryo_gen == gen) d.kryo_templates_ok = misses == 0;
   }
   // the transactions no chunk reduced: chunk-edge ones, those without signatures
   std::sort(reduced.begin(), reduced.end());
@@ -1115,8 +1192,9 @@ int stream_verify_impl(cordahip_ctx* ctx, const cordahip_stream_batch* b) {
 // FilteredTransaction.verify for txs [t0, t1) on one device: K3 hashes the
 // filtered leaves, K6 evaluates each partial tree and compares.
 int filtered_tx_shard(Device& d, const cordahip_filtered_tx_batch* b, uint64_t t0, uint64_t t1) {
-  std::lock_guard<std::mutex> g(d.tx_mu);
-  if (int rc = tx_acquire_host(d)) return rc;
+  SetLease lease(d);
+  TxSet& S = lease.get();
+  if (int rc = tx_acquire_host(d, S)) return rc;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
   const uint64_t b0 = nleaves ? b->leaf_off[l0] : 0, b1 = nleaves ? b->leaf_off[l1] : 0;
@@ -1127,7 +1205,7 @@ int filtered_tx_shard(Device& d, const cordahip_filtered_tx_batch* b, uint64_t t
     toff[i] = b->tx_leaf_off[t0 + i] - l0;
     koff[i] = b->tx_tok_off[t0 + i] - k0;
   }
-  TxWork& w = d.tx;
+  TxWork& w = S.tx;
   if (w.leaf_bytes.ensure(std::max<uint64_t>(b1 - b0, 16)) || w.leaf_off.ensure((nleaves + 1) * 8) ||
       w.tx_leaf_off.ensure((ntx + 1) * 8) || w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) ||
       w.tok.ensure(std::max<uint64_t>(ntok, 1)) || w.tok_hash.ensure(std::max<uint64_t>(ntok, 1) * 32) ||
@@ -1152,8 +1230,9 @@ int filtered_tx_shard(Device& d, const cordahip_filtered_tx_batch* b, uint64_t t
                                 w.tok_hash.as<uint8_t>(), w.tx_tok_off.as<uint64_t>(), w.root.as<uint8_t>(), ntx,
                                 w.stack.as<uint32_t>(), w.tx_status.as<uint8_t>(), s);
   e = e ? e : hipMemcpyAsync(b->tx_status + t0, w.tx_status.p, ntx, hipMemcpyDeviceToHost, s);
-  e = e ? e : hipEventRecord(d.tx_ev, s);
-  e = e ? e : hipStreamSynchronize(s);
+  e = e ? e : hipEventRecord(S.tx_ev, s);
+  e = e ? e : hipEventSynchronize(S.tx_ev);
+  if (e != hipSuccess) (void)hipStreamSynchronize(s);
   return hip_err(e);
 }
 
@@ -1179,14 +1258,25 @@ void free_device(Device& d) {
     for (hipEvent_t ev : {st.copied, st.done})
       if (ev) (void)hipEventDestroy(ev);
   }
-  for (BatchStage& st : d.pb) {
-    for (auto& b : st.h) b.release();
-    for (auto& b : st.d) b.release();
-    for (auto& b : st.hidx) b.release();
-    for (auto& b : st.didx) b.release();
-    st.dverdict.release();
-    for (hipEvent_t ev : {st.copied, st.ed_done, st.ec_done})
-      if (ev) (void)hipEventDestroy(ev);
+  for (TxSet& S : d.set) {
+    for (BatchStage& st : S.pb) {
+      for (auto& b : st.h) b.release();
+      for (auto& b : st.d) b.release();
+      for (auto& b : st.hidx) b.release();
+      for (auto& b : st.didx) b.release();
+      st.dverdict.release();
+      for (hipEvent_t ev : {st.copied, st.ed_done, st.ec_done})
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    TxWork& w = S.tx;
+    for (DevBuf* b : {&w.leaf_bytes, &w.leaf_off, &w.tx_leaf_off, &w.hashes, &w.txid, &w.tx_status, &w.tx_sig_off,
+                      &w.msgs, &w.comp_items, &w.payload, &w.comp_status, &w.tok, &w.tok_hash, &w.tx_tok_off, &w.root,
+                      &w.stack})
+      b->release();
+    if (S.kryo_usage) (void)hipHostFree(S.kryo_usage);
+    S.kryo_usage = S.kryo_usage_dev = nullptr;
+    if (S.tx_ev) (void)hipEventDestroy(S.tx_ev);
+    S.tx_ev = nullptr;
   }
   for (auto& st : d.sstage) {
     for (DevBuf* b : {&st.ed_keys, &st.ed_sigs, &st.ed_msgs, &st.ed_status, &st.ec_scheme, &st.ec_keys,
@@ -1197,17 +1287,13 @@ void free_device(Device& d) {
   }
   for (hipStream_t ss : {d.s_copy, d.s_ed, d.s_ec, d.s_idcopy, d.s_ed2})
     if (ss) (void)hipStreamDestroy(ss);
-  for (DevBuf* b : {&d.tx.leaf_bytes, &d.tx.leaf_off, &d.tx.tx_leaf_off, &d.tx.hashes, &d.tx.txid, &d.tx.tx_status,
-                    &d.tx.tx_sig_off, &d.tx.msgs, &d.tx.tok, &d.tx.tok_hash, &d.tx.tx_tok_off, &d.tx.root,
-                    &d.tx.stack})
-    b->release();
   for (DevBuf* b : {&d.ec.counters, &d.ec.perm, &d.ec.ws, &d.kryo_sizes, &d.kryo_temp, &d.kryo_ws, &d.kryo_fixed,
                     &d.kryo_items})
     b->release();
   for (auto& w : d.ed_ws) w.release();
   if (d.kryo_usage) (void)hipHostFree(d.kryo_usage);
   d.kryo_usage = d.kryo_usage_dev = nullptr;
-  for (hipEvent_t ev : {d.ec.ev, d.ed_ev[0], d.ed_ev[1], d.tx_ev, d.kryo_ev})
+  for (hipEvent_t ev : {d.ec.ev, d.ed_ev[0], d.ed_ev[1], d.kryo_ev})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& tc : d.ring)
     for (hipEvent_t ev : {tc.a, tc.b})
@@ -1288,11 +1374,13 @@ static int init_impl(uint32_t device_mask, cordahip_ctx** out) {
     Device& dev = *ctx->devs.back();
     dev.id = d;
     dev.uid = g_device_uid.fetch_add(1);
-    if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&dev.tx_ev, hipEventDisableTiming) != hipSuccess) {
+    if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking) != hipSuccess) {
       rc = CORDAHIP_ERR_HIP;
       break;
     }
+    for (TxSet& S : dev.set)
+      if (hipEventCreateWithFlags(&S.tx_ev, hipEventDisableTiming) != hipSuccess) rc = CORDAHIP_ERR_HIP;
+    if (rc != CORDAHIP_SUCCESS) break;
     for (auto& tc : dev.ring)
       if (hipEventCreate(&tc.a) != hipSuccess || hipEventCreate(&tc.b) != hipSuccess) rc = CORDAHIP_ERR_HIP;
     if (rc != CORDAHIP_SUCCESS) break;
@@ -1309,7 +1397,7 @@ static int init_impl(uint32_t device_mask, cordahip_ctx** out) {
     }
     if (launch_ed25519_btable(dev.btab, dev.stream) != hipSuccess ||
         launch_ecdsa_gtables(dev.gtab_k1, dev.gtab_r1, dev.stream) != hipSuccess ||
-        hipEventRecord(dev.tx_ev, dev.stream) != hipSuccess || hipStreamSynchronize(dev.stream) != hipSuccess)
+        hipStreamSynchronize(dev.stream) != hipSuccess)
       rc = CORDAHIP_ERR_HIP;
   }
   if (rc == CORDAHIP_SUCCESS && ctx->devs.empty()) rc = CORDAHIP_ERR_NO_DEVICE;
@@ -1568,19 +1656,22 @@ int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, cons
   if (!d || (ntx && (!d_leaf_off || !d_tx_leaf_off || !d_tx_sig_off || !d_txid || !d_tx_status || !d_first_bad)) ||
       (nsig && (!d_keys || !d_sigs || !d_sig_status)))
     return CORDAHIP_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> g(d->tx_mu);
+  // a buffer set for the enqueue; its event then fences the set's hashes / msgs
+  // until these kernels finish (the next holder waits on it)
+  SetLease lease(*d);
+  TxSet& S = lease.get();
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
-  TxWork& w = d->tx;
+  TxWork& w = S.tx;
   if (w.hashes.cap < std::max<uint64_t>(nleaves, 1) * 32 || w.msgs.cap < std::max<uint64_t>(nsig, 1) * 32) {
     // growing frees the old buffers: the previous user's kernels must be done
-    if (hipEventSynchronize(d->tx_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (hipEventSynchronize(S.tx_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
     if (w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) || w.msgs.ensure(std::max<uint64_t>(nsig, 1) * 32))
       return CORDAHIP_ERR_OUT_OF_MEMORY;
   }
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   TimedCall* tc = timed_begin(*d, s);
   if (!tc) return CORDAHIP_ERR_HIP;
-  hipError_t e = hipStreamWaitEvent(s, d->tx_ev, 0);  // the previous user of w.hashes / w.msgs is done
+  hipError_t e = hipStreamWaitEvent(s, S.tx_ev, 0);  // the previous user of w.hashes / w.msgs is done
   e = e ? e : launch_sha256_leaves(static_cast<const uint8_t*>(d_leaf_bytes), static_cast<const uint64_t*>(d_leaf_off),
                                    nleaves, w.hashes.as<uint32_t>(), s);
   e = e ? e : launch_merkle_root(w.hashes.as<uint32_t>(), static_cast<const uint64_t*>(d_tx_leaf_off), ntx,
@@ -1590,7 +1681,7 @@ int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, cons
   e = e ? e : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
                                 w.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status), nullptr,
                                 0u, s);
-  e = e ? e : hipEventRecord(d->tx_ev, s);  // fences w.hashes / w.msgs for the next user
+  e = e ? e : hipEventRecord(S.tx_ev, s);  // fences w.hashes / w.msgs for the next user
   e = e ? e : launch_tx_reduce(static_cast<const uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off),
                                ntx, static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);
   e = e ? e : hipEventRecord(tc->b, s);
@@ -1608,8 +1699,8 @@ int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_ite
     if (!d->kryo_ev && hipEventCreateWithFlags(&d->kryo_ev, hipEventDisableTiming) != hipSuccess)
       return CORDAHIP_ERR_HIP;
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    // the direct encoder's writers (items without a template): 2^15 threads,
-    // 7 KB of level buffers each (224 MB)
+    // the direct encoder's writers (items without a template): 2^13 threads,
+    // 7 KB of level buffers each (56 MB)
     const uint64_t dwriters = 1u << 13;
     size_t temp_bytes = 0;
     if (kryo_scan_bytes(temp_bytes, n + 1, s) != hipSuccess) return CORDAHIP_ERR_HIP;
@@ -1633,7 +1724,7 @@ int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_ite
                                slots, slots + n, d->kryo_sizes.as<uint64_t>(), static_cast<uint64_t*>(d_off),
                                static_cast<uint8_t*>(d_out), d_out ? cap : 0, static_cast<uint8_t*>(d_status),
                                d->kryo_ws.as<uint8_t>(), dwriters, d->kryo_temp.p, d->kryo_temp.cap, s);
-    e = e ? e : kryo_usage_report(*d, s);
+    e = e ? e : kryo_usage_report(*d, nullptr, s);
     e = e ? e : hipEventRecord(d->kryo_ev, s);
     e = e ? e : hipEventRecord(tc->b, s);
     return hip_err(e);

@@ -197,8 +197,8 @@ struct PieceInfo {
 // status D2H on each section's stream. Classification and packing of chunk k
 // run while the GPU verifies chunks k-1 and k-2; a stage's statuses go back to
 // the caller's lanes when the stage comes round again.
-int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, const MsgView& mv, uint64_t lo,
-                 uint64_t hi) {
+int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_batch* b, const MsgView& mv,
+                 uint64_t lo, uint64_t hi) {
   if (lo >= hi) return CORDAHIP_SUCCESS;
   std::vector<Unit> units(1);
   units[0].lo = lo;
@@ -214,9 +214,8 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     chunks = make_chunks(units, mv.chunk ? mv.chunk : chunk_lanes("CORDAHIP_HOST_CHUNK", kEdChunk));
   }
   const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
-  std::lock_guard<std::mutex> g(d.pb_mu);
   if (hipSetDevice(d.id) != hipSuccess || ensure_streams(d) != hipSuccess) return CORDAHIP_ERR_HIP;
-  for (BatchStage& st : d.pb)
+  for (BatchStage& st : set.pb)
     for (hipEvent_t* pe : {&st.copied, &st.ed_done, &st.ec_done})
       if (!*pe && hipEventCreateWithFlags(pe, hipEventDisableTiming) != hipSuccess) return CORDAHIP_ERR_HIP;
   HostPool& pool = *ctx->host;
@@ -270,7 +269,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
   int rc = CORDAHIP_SUCCESS;
   const double t_start = tracing() ? now_ms() : 0;
   for (size_t k = 0; k < chunks.size() && e == hipSuccess && rc == CORDAHIP_SUCCESS; k++) {
-    BatchStage& st = d.pb[k % kPackStages];
+    BatchStage& st = set.pb[k % kPackStages];
     const double t0 = tracing() ? now_ms() : 0;
     e = finish(st);
     if (e != hipSuccess) break;
@@ -467,7 +466,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
     // (4) launches
     // consecutive chunks alternate between s_ed / s_ed2 and the two Ed25519
     // workspace slots: chunk k + 1's kernels overlap chunk k's end-of-grid tail
-    const int slot = (int)(k & 1);
+    const int slot = (int)(d.ed_turn.fetch_add(1) & 1);  // alternating across calls too
     hipStream_t es = slot ? d.s_ed2 : d.s_ed;
     e = e ? e : hipEventRecord(st.copied, d.s_copy);
     e = e ? e : hipStreamWaitEvent(es, st.copied, 0);
@@ -527,17 +526,25 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, cons
               (unsigned long long)m, (unsigned long long)ne, (unsigned long long)nc, t0 - t_start, t1 - t0,
               t1b - t1, t2 - t1b, t3 - t2, t3b - t3, t3c - t3b, now_ms() - t3c);
   }
-  // drain every stage even after an error, so no queued work outlives the call
+  // every chunk is enqueued: the caller's hook (the signed-tx path hands its
+  // enqueue token on; the stages below are this call's own)
+  if (dev && dev->enqueued && e == hipSuccess && rc == CORDAHIP_SUCCESS) e = dev->enqueued();
+  // drain every stage: each stage's events follow its chunk's last work on every
+  // stream it used, so waiting for them (not for the shared streams, which may
+  // already carry the next call's work) drains this call. After an error the
+  // streams themselves are drained, so no queued work outlives the call.
   for (int k = 0; k < kPackStages; k++) {
-    if (e == hipSuccess && rc == CORDAHIP_SUCCESS) e = finish(d.pb[k]);
-    d.pb[k].pending = false;
+    if (e == hipSuccess && rc == CORDAHIP_SUCCESS) e = finish(set.pb[k]);
+    set.pb[k].pending = false;
   }
-  const hipError_t e1 = hipStreamSynchronize(d.s_copy), e2 = hipStreamSynchronize(d.s_ed),
-                   e2b = hipStreamSynchronize(d.s_ed2),
-                   e3 = hipStreamSynchronize(d.s_ec);
+  if (e != hipSuccess || rc != CORDAHIP_SUCCESS) {
+    for (hipStream_t x : {d.s_copy, d.s_ed, d.s_ed2, d.s_ec}) (void)hipStreamSynchronize(x);
+    for (BatchStage& st : set.pb)
+      for (hipEvent_t ev : {st.copied, st.ed_done, st.ec_done}) (void)hipEventSynchronize(ev);
+  }
   if (tracing()) fprintf(stderr, "[cordahip] dev %d: shard done at %.1f ms\n", d.id, now_ms() - t_start);
   if (rc != CORDAHIP_SUCCESS) return rc;
-  return (e || e1 || e2 || e2b || e3) ? CORDAHIP_ERR_HIP : CORDAHIP_SUCCESS;
+  return e ? CORDAHIP_ERR_HIP : CORDAHIP_SUCCESS;
 }
 
 }  // namespace
@@ -557,16 +564,20 @@ int sig_verify_msgs(cordahip_ctx* ctx, const cordahip_sig_batch* b, const MsgVie
   const uint64_t n = b->n;
   if (n == 0) return CORDAHIP_SUCCESS;
   // contiguous 64-aligned input shards, one pipeline per device
-  const int rc = for_shards(ctx->devs, n, 64,
-                            [&](Device& d, uint64_t lo, uint64_t hi) { return sig_pipeline(ctx, d, b, mv, lo, hi); });
+  const int rc = for_shards(ctx->devs, n, 64, [&](Device& d, uint64_t lo, uint64_t hi) {
+    SetLease lease(d);
+    if (hipSetDevice(d.id) != hipSuccess || hipEventSynchronize(lease.get().tx_ev) != hipSuccess)
+      return (int)CORDAHIP_ERR_HIP;
+    return sig_pipeline(ctx, d, lease.get(), b, mv, lo, hi);
+  });
   if (rc != CORDAHIP_SUCCESS) return rc;
   // verdict words: built per chunk by the pipelines (sig_pipeline's finish)
   return CORDAHIP_SUCCESS;
 }
 
-int sig_verify_range(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, const MsgView& mv, uint64_t lo,
-                     uint64_t hi) {
-  return sig_pipeline(ctx, d, b, mv, lo, hi);
+int sig_verify_range(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_batch* b, const MsgView& mv,
+                     uint64_t lo, uint64_t hi) {
+  return sig_pipeline(ctx, d, set, b, mv, lo, hi);
 }
 
 int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {

@@ -88,8 +88,10 @@ constexpr uint32_t kDsizeBlocks = 64;    // kryo_dsize: blocks of 256 (direct it
 constexpr uint32_t kLevelSyms = kryo::kLevelBytes;  // levels 1..7 (level 0 is the leaf itself)
 // counters: [0] new shapes this call, [1] direct items this call, [2] templates
 // in the arena, [3] table slots in use (the last two persist with the table),
-// [4] misses: items that needed a new template or the direct encoder since the
-// host last reset it (a templates-only chain did not write their leaves)
+// [4 + k] misses of the runtime's buffer set k: items that needed a new template
+// or the direct encoder since the host last reset it (a templates-only chain did
+// not write their leaves); one counter per set, as two calls' slices may both be
+// on the device
 enum { kCNew = 0, kCDirect = 1, kCArena = 2, kCUsed = 3, kCMiss = 4 };
 constexpr uint8_t kKryoMiss = 4;  // item status of a miss (runtime.hpp)
 
@@ -200,7 +202,8 @@ __global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_
                                                           const kryo::ShapeRec* __restrict__ rec,
                                                           uint32_t* __restrict__ item_slot, uint32_t* __restrict__ shape_list,
                                                           uint64_t* __restrict__ sizes, uint8_t* __restrict__ status,
-                                                          uint32_t* __restrict__ direct, uint32_t* __restrict__ counters) {
+                                                          uint32_t* __restrict__ direct, uint32_t* __restrict__ counters,
+                                                          uint32_t* __restrict__ misses) {
   kryo_priority();
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j == 0) sizes[n] = 0;  // the scan's last element: off[n] = the total
@@ -213,10 +216,11 @@ __global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_
     item_slot[i] = kRawSlot;
     if (it.len && !it.data) {
       st = 1;
-    } else if (templates_only && it.len >> 32) {  // kryo_hash takes 32-bit lengths: the full chain
+    } else if (templates_only && it.len >> 29) {  // kryo_hash takes leaves under 2^29 bytes (32-bit bit counts
+                                                  // and block indices): larger RAW leaves take the full chain
       st = kKryoMiss;
       item_slot[i] = kNoSlot;
-      atomicAdd(&counters[kCMiss], 1u);
+      atomicAdd(misses, 1u);
     } else {
       size = it.len;
     }
@@ -280,13 +284,20 @@ __global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_
       slot = kNoSlot;
     }
   }
-  wave_count(&counters[kCMiss], deferred || slot == kNoSlot);
+  // an item the encoder rejects before writing a byte (no payload, an unknown kind)
+  // is decided here: neither a direct item nor a miss (one such item from untrusted
+  // input would otherwise redo every templates-only call)
+  const bool reject = slot == kNoSlot && kryo::rejected_outright(it);
+  wave_count(misses, deferred || (slot == kNoSlot && !reject));
   if (deferred) {
     item_slot[i] = slot | kDefer;
     return;
   }
   item_slot[i] = slot;
-  if (slot == kNoSlot) {
+  if (reject) {
+    size = 0;
+    st = 1;
+  } else if (slot == kNoSlot) {
     if (templates_only) {
       size = 0;
       st = kKryoMiss;
@@ -819,8 +830,8 @@ __global__ void __launch_bounds__(1024) kryo_hash_kernel(ItemSrc items, uint64_t
         for (int k = 0; k < 4; k++) w[4 * q + k] = bswap32(v[k]);
       }
       if (b == nb - 1) {
-        w[14] = 0;
-        w[15] = h.len * 8;
+        w[14] = h.len >> 29;  // the 64-bit bit length (0 below the 2^29-byte guard in kryo_shape)
+        w[15] = h.len << 3;
       }
       sha256_block(st, w);
     }
@@ -867,22 +878,22 @@ hipError_t kryo_clear(uint8_t* fixed, hipStream_t s) {
 }
 // counters[kCArena .. kCMiss + 1] (device) -> usage[0..3] (host-mapped), after a call
 const uint32_t* kryo_usage_src(uint8_t* fixed) { return KryoState(fixed).counters + kCArena; }
-hipError_t kryo_reset_misses(uint8_t* fixed, hipStream_t s) {
-  return hipMemsetAsync(KryoState(fixed).counters + kCMiss, 0, 4, s);
+hipError_t kryo_reset_misses(uint8_t* fixed, uint32_t set, hipStream_t s) {
+  return hipMemsetAsync(KryoState(fixed).counters + kCMiss + (set & 1), 0, 4, s);
 }
 uint32_t kryo_clear_threshold_slots() { return kSlots / 2; }
 uint32_t kryo_clear_threshold_templates() { return kBuilders - 64; }
 
 hipError_t launch_kryo_shape(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
                              uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
-                             uint64_t* sizes, uint8_t* status, hipStream_t s, bool templates_only) {
+                             uint64_t* sizes, uint8_t* status, hipStream_t s, bool templates_only, uint32_t set) {
   if (n == 0) return hipSuccess;
   const ItemSrc items{d_items, data_base, data_len};
   const KryoState k(fixed);
   const uint32_t sb = shape_block(n, group), g = grouped(n, group) ? group : 1;
   hipLaunchKernelGGL(kryo_shape_kernel, dim3((uint32_t)((item_threads(n, group) + sb - 1) / sb)), dim3(sb), 0, s, items,
                      n, g, templates_only, k.table, k.slot_size, k.rec, item_slot, k.shape_list, sizes, status,
-                     direct, k.counters);
+                     direct, k.counters, k.counters + kCMiss + (set & 1));
   return hipGetLastError();
 }
 
@@ -890,7 +901,7 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* 
                               uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
                               uint64_t* sizes, uint64_t* off, uint8_t* out, uint64_t cap, uint8_t* status,
                               uint8_t* dws, uint64_t dwriters, void* scan_temp, size_t scan_bytes, hipStream_t s,
-                              bool templates_only) {
+                              bool templates_only, uint32_t set) {
   const ItemSrc items{d_items, data_base, data_len};
   const KryoState k(fixed);
   // kCNew, kCDirect (the templates-only chain neither claims nor lists: no reset, one
@@ -901,7 +912,7 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* 
     return e;
   }
   e = launch_kryo_shape(d_items, data_base, data_len, n, group, fixed, item_slot, direct, sizes, status, s,
-                        templates_only);
+                        templates_only, set);
   // build, tsize, dsize (and dwrite) serve new shapes and direct items; in steady
   // state they find nothing to do, yet beside the Ed25519 ladders of a component
   // batch each empty launch of build / dsize / dwrite took 0.07-0.47 ms on the

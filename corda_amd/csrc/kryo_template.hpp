@@ -281,6 +281,28 @@ KRYO_HD inline bool shape_hash_of(const cordahip_kryo_item& it, uint64_t& h) {
   h = v.value();
   return ok;
 }
+// The encoder (kryo_core.hpp encode_leaf) rejects the item before writing a
+// byte: an unknown kind, or a payload that is missing (after ItemSrc's bounds
+// check) or of a length the kind never accepts. Mirrors encode_leaf's early
+// returns; the shape pass gives such items status 1 at once instead of sending
+// them to the direct encoder (or, in the templates-only chain, counting a miss
+// that would redo the whole call).
+KRYO_HD inline bool rejected_outright(const cordahip_kryo_item& it) {
+  switch (it.kind) {
+    case CORDAHIP_KRYO_CHAR: case CORDAHIP_KRYO_SHORT: case CORDAHIP_KRYO_INT: case CORDAHIP_KRYO_LONG:
+    case CORDAHIP_KRYO_BYTE: case CORDAHIP_KRYO_BOOLEAN: case CORDAHIP_KRYO_FLOAT: case CORDAHIP_KRYO_DOUBLE:
+      return false;
+    case CORDAHIP_KRYO_RAW:
+    case CORDAHIP_KRYO_STRING: return it.len && !it.data;
+    case CORDAHIP_KRYO_ED25519_KEY: return !it.data || it.len != 32;
+    case CORDAHIP_KRYO_PUBLIC_KEY: return !it.data || it.len == 0 || it.len > 0x7fffffffull;
+    case CORDAHIP_KRYO_KOTLIN_OBJECT: return !it.data || it.len == 0;
+    case CORDAHIP_KRYO_PARTY: return !it.data || it.len < 3;
+    case CORDAHIP_KRYO_ISSUE_COMMAND: return !it.data || it.len < 2;
+    case CORDAHIP_KRYO_CASH_STATE: return !it.data;
+    default: return true;
+  }
+}
 // the item has exactly the recorded shape
 KRYO_HD inline bool shape_matches(const cordahip_kryo_item& it, const ShapeRec& rec) {
   ShapeCmp v(rec);

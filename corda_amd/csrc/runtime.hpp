@@ -48,10 +48,11 @@ size_t kryo_fixed_scratch_bytes();                     // shape table, records, 
 size_t kryo_direct_ws_bytes(uint64_t writers);         // the direct encoder's level buffers
 hipError_t kryo_scan_bytes(size_t& bytes, uint64_t n1, hipStream_t s);
 hipError_t kryo_clear(uint8_t* fixed, hipStream_t s);  // empty the shape table (and the template arena)
-// device: [templates in the arena, table slots in use, misses since kryo_reset_misses, 0]
+// device: [templates in the arena, table slots in use, misses of buffer set 0, of set 1]
+// (each set's since its kryo_reset_misses)
 const uint32_t* kryo_usage_src(uint8_t* fixed);
 constexpr size_t kKryoUsageBytes = 16;
-hipError_t kryo_reset_misses(uint8_t* fixed, hipStream_t s);
+hipError_t kryo_reset_misses(uint8_t* fixed, uint32_t set, hipStream_t s);
 uint32_t kryo_clear_threshold_slots();
 uint32_t kryo_clear_threshold_templates();
 // data_base != nullptr: items' `data` are offsets into data_len bytes at data_base.
@@ -63,11 +64,11 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* items, const uint8_t* da
                               uint64_t n, uint32_t group, uint8_t* fixed,
                               uint32_t* item_slot, uint32_t* direct, uint64_t* sizes, uint64_t* off, uint8_t* out,
                               uint64_t cap, uint8_t* status, uint8_t* dws, uint64_t dwriters, void* scan_temp,
-                              size_t scan_bytes, hipStream_t s, bool templates_only = false);
+                              size_t scan_bytes, hipStream_t s, bool templates_only = false, uint32_t set = 0);
 // the shape pass alone (sizes, item_slot, statuses; kCMiss counts misses)
 hipError_t launch_kryo_shape(const cordahip_kryo_item* items, const uint8_t* data_base, uint64_t data_len, uint64_t n,
                              uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct, uint64_t* sizes,
-                             uint8_t* status, hipStream_t s, bool templates_only);
+                             uint8_t* status, hipStream_t s, bool templates_only, uint32_t set = 0);
 // SHA-256 of every item's leaf straight from its template (after a templates-only shape
 // pass): hashes[n][8] big-endian words, zero for items with a nonzero status
 hipError_t launch_kryo_hash(const cordahip_kryo_item* items, const uint8_t* data_base, uint64_t data_len, uint64_t n,
@@ -188,6 +189,20 @@ struct TxWork {  // device buffers of the transaction paths (grow-only)
   DevBuf tok, tok_hash, tx_tok_off, root, stack;  // filtered-tx (partial Merkle tree) path
 };
 
+// One set of a device's transaction and signature-pipeline buffers. A call
+// holds its set from start to finish; tx_ev marks the completion of the last
+// work enqueued on the set's device buffers (the next holder's first wait).
+struct TxSet {
+  TxWork tx;
+  hipEvent_t tx_ev = nullptr;
+  BatchStage pb[kPackStages];  // generic CSR batches and the signed-tx signature chunks
+  // component calls: the encoder's usage counters after this set's last call,
+  // host-mapped: [templates in the arena, table slots in use, misses of set 0, of set 1]
+  uint32_t* kryo_usage = nullptr;
+  uint32_t* kryo_usage_dev = nullptr;
+};
+constexpr int kTxSets = 2;
+
 struct EcWork {  // device buffers of the ECDSA paths (grow-only)
   DevBuf counters, perm;
   DevBuf ws;                 // split-kernel workspace (kEcWsSlots records)
@@ -215,12 +230,20 @@ struct Device {
   std::mutex tmu;
   TimedCall ring[kTimingRing];
   uint64_t ring_next = 0;
-  // tx buffers: tx_mu orders the enqueues of every user (host tx paths, the
-  // device signed-tx path), tx_ev marks the last enqueued user's completion;
-  // each user's stream waits on it before touching the buffers.
-  std::mutex tx_mu;
-  TxWork tx;
-  hipEvent_t tx_ev = nullptr;
+  // Transaction / signature-pipeline buffer sets (TxSet): a call holds one set
+  // from start to finish (acquire_set / SetLease); two sets let a signed-tx call
+  // drain while the next one enqueues. tx_order_mu is the enqueue token of the
+  // signed-tx path: held from a call's start until its last chunk is enqueued,
+  // so consecutive calls' work reaches the shared streams in call order.
+  TxSet set[kTxSets];
+  std::mutex set_m;
+  std::condition_variable set_cv;
+  bool set_busy[kTxSets] = {};
+  std::mutex tx_order_mu;
+  // consecutive Ed25519 chunks of every pipeline call alternate workspace slots and
+  // streams (s_ed / s_ed2) across calls too, so call k + 1's first prep overlaps
+  // call k's last ladder
+  std::atomic<uint32_t> ed_turn{0};
   // Ed25519 split-kernel workspace, shared by every stream that verifies on
   // this device: ed_mu orders the enqueues, ed_ev makes each user's stream
   // wait for the previous user's kernels before it reuses the buffer.
@@ -243,10 +266,10 @@ struct Device {
   hipStream_t s_idcopy = nullptr;
   std::mutex stream_mu;  // serialises use of sstage (C5)
   StreamStage sstage[kStreamStages];
-  // packed host pipelines: one stage set per section, each behind its mutex
-  std::mutex ped_mu, pb_mu;
-  PackStage ped[kPackStages];   // dense Ed25519 rows (cordahip_ed25519_verify_host)
-  BatchStage pb[kPackStages];   // generic CSR batches (cordahip_sig_verify / _submit)
+  // packed dense Ed25519 rows (cordahip_ed25519_verify_host); the generic CSR
+  // batches' stages live in the TxSets
+  std::mutex ped_mu;
+  PackStage ped[kPackStages];
   // GPU Kryo encoder scratch (cordahip_kryo_encode_device): leaf sizes, the
   // scan's temporary storage, the shape table and templates, per-item shape
   // slots and the direct-encoder list, the direct writers' OutputChunked level
@@ -254,12 +277,14 @@ struct Device {
   std::mutex kryo_mu;
   DevBuf kryo_sizes, kryo_temp, kryo_ws, kryo_fixed, kryo_items;
   // the fixed part is persistent (shape table, records, templates): zeroed when
-  // allocated, cleared when a call reports it over half full (kryo_usage: a
-  // host-mapped copy of its usage counters, stored after each call)
+  // allocated, cleared when a call reports it over half full (TxSet::kryo_usage:
+  // a host-mapped copy of its usage counters, stored after each call)
   bool kryo_fresh = false;
   bool kryo_templates_ok = false;  // the last component batch had no encoder misses (cordahip.cpp)
-  uint32_t* kryo_usage = nullptr;
+  uint32_t* kryo_usage = nullptr;      // cordahip_kryo_encode_device's own report
   uint32_t* kryo_usage_dev = nullptr;
+  uint64_t kryo_gen = 0;           // table clears so far (kryo_mu): a call's end updates kryo_templates_ok
+                                   // only if no clear came after its start
   hipEvent_t kryo_ev = nullptr;
 };
 
@@ -386,6 +411,42 @@ int for_shards(std::vector<std::unique_ptr<Device>>& devs, uint64_t n, uint64_t 
   return rc;
 }
 
+// A device's buffer set for one call: the first free one (blocks while both are
+// held); `prefer` is tried first. The holder then waits on set.tx_ev before
+// touching device buffers an asynchronous device-path call may still use.
+class SetLease {
+ public:
+  explicit SetLease(Device& d, int prefer = 0) : d_(d) {
+    std::unique_lock<std::mutex> g(d.set_m);
+    for (;;) {
+      for (int k = 0; k < kTxSets; k++) {
+        const int i = (prefer + k) % kTxSets;
+        if (!d.set_busy[i]) {
+          d.set_busy[i] = true;
+          idx_ = i;
+          return;
+        }
+      }
+      d.set_cv.wait(g);
+    }
+  }
+  ~SetLease() {
+    {
+      std::lock_guard<std::mutex> g(d_.set_m);
+      d_.set_busy[idx_] = false;
+    }
+    d_.set_cv.notify_one();
+  }
+  SetLease(const SetLease&) = delete;
+  SetLease& operator=(const SetLease&) = delete;
+  int index() const { return idx_; }
+  TxSet& get() const { return d_.set[idx_]; }
+
+ private:
+  Device& d_;
+  int idx_ = 0;
+};
+
 }  // namespace rt
 }  // namespace cordahip
 
@@ -427,6 +488,9 @@ struct DeviceIds {
   // chunk has finished): the per-transaction reduce of the transactions whose
   // signatures all lie in [a, b) runs there, while later chunks verify
   std::function<hipError_t(uint64_t a, uint64_t b)> done;
+  // called once every chunk is enqueued, before the pipeline drains: the signed-tx
+  // call enqueues its remaining id slices and hands the enqueue token to the next call
+  std::function<hipError_t()> enqueued;
   hipEvent_t wait_for(uint64_t tx) const {  // the event after which transaction tx's id is on the device
     const size_t j = (size_t)(std::upper_bound(tx_bound.begin(), tx_bound.end(), tx) - tx_bound.begin());
     return ready[j ? j - 1 : 0];
@@ -450,9 +514,10 @@ struct MsgView {
 // from mv instead of b->msg / b->msg_off
 int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b);
 int sig_verify_msgs(cordahip_ctx* ctx, const cordahip_sig_batch* b, const MsgView& mv);
-// lanes [lo, hi) of b on device d only (the signed-tx path's per-device signatures)
-int sig_verify_range(cordahip_ctx* ctx, Device& d, const cordahip_sig_batch* b, const MsgView& mv, uint64_t lo,
-                     uint64_t hi);
+// lanes [lo, hi) of b on device d only, through the stages of the caller's set
+// (the signed-tx path's per-device signatures)
+int sig_verify_range(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_batch* b, const MsgView& mv,
+                     uint64_t lo, uint64_t hi);
 // dense Ed25519 rows in host memory through the packed pipeline (host_batch.cpp)
 int ed25519_dense_host(cordahip_ctx* ctx, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
                        uint32_t msg_len, uint64_t n, uint8_t* status, uint64_t* verdict);

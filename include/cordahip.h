@@ -395,7 +395,7 @@ int cordahip_kryo_encode(const cordahip_kryo_item* items, uint64_t n, uint8_t* o
  * (equal structure, kryo_template.hpp) are written from a template traced once
  * per shape. d_out NULL: sizes and offsets only (statuses 0 / 1). n < 2^31 - 1
  * per call. Device scratch (grow-only, per device): 16 B per item, ~18 MB of
- * shape table and templates, 224 MB of level buffers for the items written
+ * shape table and templates, 56 MB of level buffers for the items written
  * without a template. */
 int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_items, uint64_t n, uint32_t group,
                                 void* d_out, uint64_t cap, void* d_off, void* d_status, void* hip_stream);

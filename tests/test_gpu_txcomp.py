@@ -269,3 +269,63 @@ def test_fused_template_hashes_every_kind(engine, oracle):
         res = engine.signed_txcomp_verify(txs, sigs)
         assert [res[0][t].tobytes() for t in range(len(txs))] == ids
         assert (res[1] == 0).all() and (res[3] == 0).all()
+
+
+def test_concurrent_tickets_one_device(engine, oracle):
+    """Consecutive signed-tx calls overlap on one device (two buffer sets, the enqueue
+    token handed on once a call's last chunk is enqueued): two cordahip_txcomp_submit
+    tickets and one cordahip_tx_submit ticket outstanding at once, each with its own
+    signatures (different corruptions) and output arrays, in many signature chunks and id
+    slices, the component calls before and after their shapes are built (full chain, then
+    the templates-only chain). Every id, tx status, first_bad_sig and signature status
+    equals the leaf path's run alone; the ids equal the oracle's on a sample."""
+    rng = np.random.default_rng(56)
+    ntx = 6000
+    blob, items, _ = cash_issue_items(rng.integers(0, 256, (ntx, 32), dtype=np.uint8),
+                                      rng.integers(0, 256, (ntx, 32), dtype=np.uint8), bytes(range(32)),
+                                      rng.integers(1, 10**9, ntx), rng.integers(-2**63, 2**63 - 1, ntx))
+    it = items.reshape(-1).copy()
+    host_it = it.copy()
+    host_it["data"] += np.uint64(blob.ctypes.data)
+    hb, ho = _lib.kryo_encode_array(host_it)
+    leaves = [[hb[int(ho[5 * t + j]):int(ho[5 * t + j + 1])].tobytes() for j in range(5)] for t in range(ntx)]
+    ids_l, _ = engine.tx_ids(leaves)
+    assert [ids_l[t].tobytes() for t in range(0, ntx, 1499)] == [_oracle_id(oracle, leaves[t])
+                                                                 for t in range(0, ntx, 1499)]
+    base = [[(ED,) + _sign(oracle, hashlib.sha256(b"cc%d-%d" % (t, q)).digest(), ids_l[t].tobytes())
+             for q in range(1 + t % 3)] for t in range(ntx)]
+
+    def corrupt(period, phase):
+        out = []
+        for t, per in enumerate(base):
+            per = list(per)
+            if t % period == phase:
+                q = t % len(per)
+                per[q] = (ED, per[q][1], per[q][2][:9] + bytes([per[q][2][9] ^ 2]) + per[q][2][10:])
+            out.append(per)
+        return out
+
+    sig_sets = [corrupt(10, 3), corrupt(7, 2), corrupt(13, 5)]
+    want = [engine.signed_tx_verify(leaves, s) for s in sig_sets]  # the leaf path, one call at a time
+    tio = np.arange(0, 5 * ntx + 1, 5, dtype=np.uint64)
+    old = os.environ.get("CORDAHIP_TX_SIG_CHUNK")
+    os.environ["CORDAHIP_TX_SIG_CHUNK"] = "2048"  # ~6 chunks and id slices per call
+    try:
+        for rnd in range(3):  # round 0 may build shapes (full chain); later rounds: templates-only
+            tks = [engine.signed_txcomp_verify_arrays(blob, it, tio, sig_sets[0], async_=True, pinned_out=rnd % 2 == 0),
+                   engine.signed_tx_verify(leaves, sig_sets[2], async_=True),
+                   engine.signed_txcomp_verify_arrays(blob, it, tio, sig_sets[1], async_=True)]
+            got = [tk.wait() for tk in tks]
+            for g, w in zip(got, [want[0], want[2], want[1]]):
+                ids_c, st_c, fb_c, sst_c = g
+                ids_w, st_w, fb_w, sst_w = w
+                assert np.array_equal(st_c, st_w), rnd
+                assert np.array_equal(fb_c, fb_w), rnd
+                assert np.array_equal(sst_c, sst_w), rnd
+                assert np.array_equal(ids_c, ids_w), rnd
+                assert (st_c == 1).sum() > 0 and (st_c == 0).sum() > ntx // 2
+    finally:
+        if old is None:
+            del os.environ["CORDAHIP_TX_SIG_CHUNK"]
+        else:
+            os.environ["CORDAHIP_TX_SIG_CHUNK"] = old
