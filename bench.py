@@ -400,12 +400,15 @@ class C4:
                     rng.integers(-2**63, 2**63 - 1, ntx))
             del pubs0, scratch
             if self.device_encode:
-                # the components' payloads stay in HBM; every step encodes the leaves
-                # on the GPU (cordahip_kryo_encode_device) before hashing them
+                # the components' payloads stay in HBM; every step hashes their leaves on the
+                # GPU from the encoder's templates (cordahip_signed_txcomp_verify_ed25519_device:
+                # items with payload offsets); the leaves themselves are written only by the
+                # check (cordahip_kryo_encode_device: items with device pointers)
                 blob, items, self.layout = cash_issue_items(*comp)
                 self.host_blob, self.host_items = blob, items
                 self.d_blob = torch.from_numpy(blob).to(device)
                 it = items.reshape(-1).copy()
+                self.d_items_off = torch.from_numpy(it.view(np.uint8).copy()).to(device)
                 it["data"] += np.uint64(self.d_blob.data_ptr())
                 self.d_items = torch.from_numpy(it.view(np.uint8)).to(device)
                 self.n_items = it.size
@@ -479,17 +482,21 @@ class C4:
                        "leaf_bytes_per_tx": round(self.leaf_bytes.numel() / ntx, 1), "native_leaves": self.native,
                        "device_encode": self.device_encode}
         if self.device_encode:
-            self.kernel = "kryo_size + scan + kryo_write + " + C4.kernel
-            # the encoder's L2-to-fabric bytes per tx (tools/leases/gpu_r5n.sh -> tools/pmc_kryo_traffic.py)
-            self.extra_pmc = ("r05_pmc_kryo_traffic.json", ntx)
+            self.kernel = ("cordahip_signed_txcomp_verify_ed25519_device: kryo_shape + kryo_hash (leaf hashes from the "
+                           "templates) + merkle_root + ed25519 prep/ladder + tx_reduce")
+            # the id chain's L2-to-fabric bytes per tx (its own PMC passes, tools/pmc_kryo_traffic.py)
+            self.extra_pmc = ("r06_pmc_c4_device_chain.json", ntx)
             self.config["component_bytes_per_tx"] = round(self.d_blob.numel() / ntx, 1)
         if not self.native:
             self.config["leaf_lens"] = list(C4_LEAF_LENS)
 
     def step(self):
         if self.device_encode:
-            self.eng.kryo_encode_device(self.d_items, self.n_items, self.leaf_bytes, self.leaf_off, self.kstatus,
-                                        group=len(C4_LEAF_LENS), device=0, stream=self.stream)
+            self.eng.signed_txcomp_verify_ed25519_device(
+                self.d_items_off, self.n_items, self.d_blob, self.tx_leaf_off, self.tx_sig_off, self.keys, self.sigs,
+                self.txid, self.tx_status, self.first_bad, self.sig_status, group=len(C4_LEAF_LENS), device=0,
+                stream=self.stream)
+            return
         self.eng.signed_tx_verify_ed25519_device(self.leaf_bytes, self.leaf_off, self.tx_leaf_off, self.tx_sig_off,
                                                  self.keys, self.sigs, self.txid, self.tx_status, self.first_bad,
                                                  self.sig_status, device=0, stream=self.stream)
@@ -499,9 +506,20 @@ class C4:
                + int((self.first_bad != self.exp_bad).sum()),
                "accepted_txs": int((self.tx_status == 0).sum()), "txs": self.ntx, "sigs": self.ns}
         if getattr(self, "device_encode", False):
-            # the GPU's leaves of the first 20,000 transactions against the host encoder
-            # (cordahip_kryo_encode) over the same (corrupted) components
+            # (1) every leaf written by the GPU encoder (cordahip_kryo_encode_device, untimed) and
+            # the leaf-level device path over them: all ids, statuses and first_bad_sig equal the
+            # component call's; (2) the leaves of the first 20,000 transactions against the host
+            # encoder (cordahip_kryo_encode) over the same (corrupted) components
             from corda_amd import _lib
+            t = self.torch
+            self.eng.kryo_encode_device(self.d_items, self.n_items, self.leaf_bytes, self.leaf_off, self.kstatus,
+                                        group=len(C4_LEAF_LENS), device=0, stream=self.stream)
+            lp = [t.empty_like(x) for x in (self.txid, self.tx_status, self.first_bad, self.sig_status)]
+            self.eng.signed_tx_verify_ed25519_device(self.leaf_bytes, self.leaf_off, self.tx_leaf_off, self.tx_sig_off,
+                                                     self.keys, self.sigs, *lp, device=0, stream=self.stream)
+            t.cuda.synchronize(self.device)
+            out["mismatches_vs_leaf_path"] = (int((lp[0] != self.txid).any(dim=1).sum()) + int((lp[1] != self.tx_status).sum())
+                                              + int((lp[2] != self.first_bad).sum()) + int((lp[3] != self.sig_status).sum()))
             k = min(self.ntx, 20000) * len(C4_LEAF_LENS)
             blob = self.d_blob.cpu().numpy()
             it = self.host_items.reshape(-1)[:k].copy()

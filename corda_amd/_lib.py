@@ -35,6 +35,7 @@ EXPORTS = [
     "cordahip_ecdsa_verify_device", "cordahip_stream_verify", "cordahip_filtered_tx_verify",
     "cordahip_tx_submit", "cordahip_txid_submit", "cordahip_filtered_tx_submit", "cordahip_shard_range",
     "cordahip_kryo_encode", "cordahip_kryo_encode_device", "cordahip_signed_txcomp_verify", "cordahip_txcomp_submit",
+    "cordahip_signed_txcomp_verify_ed25519_device",
 ]
 ERR_BUFFER_TOO_SMALL = -8
 # cordahip_kryo_item kinds (CORDAHIP_KRYO_*)
@@ -190,6 +191,8 @@ def lib() -> ctypes.CDLL:
         "cordahip_kryo_encode_device": (i32, [vp, i32, vp, u64, u32, vp, u64, vp, vp, vp]),
         "cordahip_signed_txcomp_verify": (i32, [vp, ctypes.POINTER(SignedTxcompBatch)]),
         "cordahip_txcomp_submit": (i32, [vp, ctypes.POINTER(SignedTxcompBatch), ctypes.POINTER(u64)]),
+        "cordahip_signed_txcomp_verify_ed25519_device": (i32, [vp, i32, vp, u64, u32, vp, u64, vp, u64, vp, vp, vp, u64,
+                                                               vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(l, name)

@@ -1682,7 +1682,7 @@ int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, cons
                                 w.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status), nullptr,
                                 0u, s);
   e = e ? e : hipEventRecord(S.tx_ev, s);  // fences w.hashes / w.msgs for the next user
-  e = e ? e : launch_tx_reduce(static_cast<const uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off),
+  e = e ? e : launch_tx_reduce(static_cast<uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off),
                                ntx, static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);
   e = e ? e : hipEventRecord(tc->b, s);
   return hip_err(e);
@@ -1726,6 +1726,77 @@ int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_ite
                                d->kryo_ws.as<uint8_t>(), dwriters, d->kryo_temp.p, d->kryo_temp.cap, s);
     e = e ? e : kryo_usage_report(*d, nullptr, s);
     e = e ? e : hipEventRecord(d->kryo_ev, s);
+    e = e ? e : hipEventRecord(tc->b, s);
+    return hip_err(e);
+  });
+}
+
+int cordahip_signed_txcomp_verify_ed25519_device(cordahip_ctx* ctx, int device, const void* d_items,
+                                                 uint64_t n_items, uint32_t group, const void* d_payload,
+                                                 uint64_t payload_len, const void* d_tx_item_off, uint64_t ntx,
+                                                 const void* d_tx_sig_off, const void* d_keys, const void* d_sigs,
+                                                 uint64_t nsig, void* d_txid, void* d_tx_status, void* d_first_bad,
+                                                 void* d_sig_status, void* hip_stream) {
+  Device* d = dev_at(ctx, device);
+  if (!d || (ntx && (!d_tx_item_off || !d_tx_sig_off || !d_txid || !d_tx_status || !d_first_bad)) ||
+      (n_items && !d_items) || (payload_len && !d_payload) || (nsig && (!d_keys || !d_sigs || !d_sig_status)))
+    return CORDAHIP_ERR_INVALID_ARG;
+  if (n_items >= (1ull << 31) - 1) return CORDAHIP_ERR_INVALID_ARG;  // the encoder's item slots and lists are 32-bit
+  if ((reinterpret_cast<uintptr_t>(d_keys) | reinterpret_cast<uintptr_t>(d_sigs)) & 15) return CORDAHIP_ERR_INVALID_ARG;
+  return guarded([&]() -> int {
+    // a buffer set for the enqueue (its hashes, messages and component statuses, fenced
+    // by its event until these kernels finish) and the encoder's scratch (kryo_mu, kryo_ev)
+    SetLease lease(*d);
+    TxSet& S = lease.get();
+    std::lock_guard<std::mutex> gk(d->kryo_mu);
+    if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
+    if (!d->kryo_ev && hipEventCreateWithFlags(&d->kryo_ev, hipEventDisableTiming) != hipSuccess) return CORDAHIP_ERR_HIP;
+    TxWork& w = S.tx;
+    const uint64_t dwriters = CompPlan::kDirectWriters;
+    if (w.hashes.cap < std::max<uint64_t>(n_items, 1) * 32 || w.msgs.cap < std::max<uint64_t>(nsig, 1) * 32 ||
+        w.comp_status.cap < std::max<uint64_t>(n_items, 1)) {
+      // growing frees the old buffers: the set's previous user must be done
+      if (hipEventSynchronize(S.tx_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
+      if (w.hashes.ensure(std::max<uint64_t>(n_items, 1) * 32) || w.msgs.ensure(std::max<uint64_t>(nsig, 1) * 32) ||
+          w.comp_status.ensure(std::max<uint64_t>(n_items, 1)))
+        return CORDAHIP_ERR_OUT_OF_MEMORY;
+    }
+    if (d->kryo_sizes.cap < (n_items + 1) * 8 || d->kryo_items.cap < n_items * 8 + 8 ||
+        d->kryo_ws.cap < kryo_direct_ws_bytes(dwriters) || d->kryo_fixed.cap < kryo_fixed_scratch_bytes()) {
+      if (hipEventSynchronize(d->kryo_ev) != hipSuccess) return CORDAHIP_ERR_HIP;
+      if (d->kryo_sizes.ensure((n_items + 1) * 8) || d->kryo_items.ensure(n_items * 8 + 8) ||
+          d->kryo_ws.ensure(kryo_direct_ws_bytes(dwriters)) || kryo_fixed_ensure(*d))
+        return CORDAHIP_ERR_OUT_OF_MEMORY;
+    }
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    TimedCall* tc = timed_begin(*d, s);
+    if (!tc) return CORDAHIP_ERR_HIP;
+    uint32_t* slots = d->kryo_items.as<uint32_t>();
+    hipError_t e = hipStreamWaitEvent(s, S.tx_ev, 0);  // the previous users of the set's buffers
+    e = e ? e : hipStreamWaitEvent(s, d->kryo_ev, 0);  // and of the encoder's scratch are done
+    e = e ? e : kryo_state_ready(*d, s);
+    // leaf hashes from the templates (misses impossible: new shapes are built, the rest
+    // hashed by the direct encoder), then the ids, with a rejected component making its
+    // transaction CORDAHIP_TX_BAD_COMPONENT
+    e = e ? e
+          : launch_kryo_hash_chain(static_cast<const cordahip_kryo_item*>(d_items),
+                                   static_cast<const uint8_t*>(d_payload), payload_len, n_items, group,
+                                   d->kryo_fixed.as<uint8_t>(), slots, slots + n_items, d->kryo_sizes.as<uint64_t>(),
+                                   w.comp_status.as<uint8_t>(), w.hashes.as<uint32_t>(), d->kryo_ws.as<uint8_t>(),
+                                   dwriters, s);
+    e = e ? e : kryo_usage_report(*d, nullptr, s);
+    e = e ? e : hipEventRecord(d->kryo_ev, s);
+    e = e ? e : launch_merkle_root(w.hashes.as<uint32_t>(), static_cast<const uint64_t*>(d_tx_item_off), ntx,
+                                   static_cast<uint8_t*>(d_txid), static_cast<uint8_t*>(d_tx_status), s,
+                                   w.comp_status.as<uint8_t>());
+    e = e ? e : launch_gather_txid(static_cast<const uint8_t*>(d_txid), static_cast<const uint64_t*>(d_tx_sig_off), ntx,
+                                   w.msgs.as<uint8_t>(), s);
+    e = e ? e : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
+                                  w.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status), nullptr,
+                                  0u, s);
+    e = e ? e : hipEventRecord(S.tx_ev, s);  // fences the set's buffers for the next user
+    e = e ? e : launch_tx_reduce(static_cast<uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off), ntx,
+                                 static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);
     e = e ? e : hipEventRecord(tc->b, s);
     return hip_err(e);
   });

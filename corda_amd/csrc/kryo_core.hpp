@@ -110,9 +110,22 @@ constexpr uint32_t kSymTypeMask = 3u << 30;
 constexpr uint32_t kSymOr80 = 1u << 29;
 constexpr uint32_t kMaxPayloadOff = 1u << 21;  // payload offsets a symbol can name (bits 8..28)
 
-template <bool Trace>
+// Level-0 byte sink (KoutT's Sink): NoSink for the leaf in memory (or counting);
+// kryo_device.hip's hashing sink takes the leaf's bytes as they are written and
+// compresses them into a SHA-256 state (the direct encoder's leaves then need no
+// buffer). A sink keeps at least the last byte written until the next one
+// arrives: mark() sets bit 7 of it (an ASCII string's end mark).
+struct NoSink {
+  static constexpr bool kActive = false;
+  KRYO_HD void put(uint8_t) {}
+  KRYO_HD void write(const uint8_t*, uint64_t) {}
+  KRYO_HD void mark() {}
+};
+
+template <bool Trace, class Sink = NoSink>
 struct KoutT {
   using Sym = typename std::conditional<Trace, uint32_t, uint8_t>::type;
+  Sink* sink = nullptr;  // level 0 into this sink instead of `out` (out must be nullptr, buf set)
   Sym* out;          // level 0 (the leaf); nullptr: counting
   uint64_t pos = 0;  // level-0 bytes so far (also past cap)
   uint64_t cap;      // writes at or beyond cap are dropped (pos still counts them)
@@ -162,7 +175,8 @@ struct KoutT {
     if (!failed && depth > 0) depth--;
   }
   KRYO_HD void put0(uint8_t b) {
-    if (out && pos < cap) out[pos] = b;
+    if constexpr (Sink::kActive) sink->put(b);
+    else if (out && pos < cap) out[pos] = b;
     pos++;
   }
   KRYO_HD void put(uint32_t k, uint8_t b) {  // raw append (the caller has made room)
@@ -175,14 +189,17 @@ struct KoutT {
   }
   KRYO_HD void mark_last(uint32_t k) {  // the last byte written carries the end mark (ASCII strings)
     if (k == 0) {
-      if (out && pos - 1 < cap) mark(out[pos - 1]);
+      if constexpr (Sink::kActive) sink->mark();
+      else if (out && pos - 1 < cap) mark(out[pos - 1]);
     } else if (buf) {
       mark(at(k, len[k] - 1));
     }
   }
   KRYO_HD void copy(uint32_t k, const uint8_t* p, uint32_t n) {  // n bytes that fit
     if (k == 0) {
-      if (out) {
+      if constexpr (Sink::kActive) {
+        sink->write(p, n);
+      } else if (out) {
         bool done = false;
         if constexpr (!Trace) {
           if (pos + n <= cap) {
@@ -207,7 +224,13 @@ struct KoutT {
     }
   }
   KRYO_HD void put_syms0(const Sym* p, uint32_t n) {  // a flushed level-1 chunk into the leaf
-    if (out) {
+    if constexpr (Sink::kActive) {
+      if constexpr (Trace) {
+        for (uint32_t i = 0; i < n; i++) sink->put((uint8_t)p[i]);
+      } else {
+        sink->write(p, n);
+      }
+    } else if (out) {
       if (pos + n <= cap) {
         __builtin_memcpy(out + pos, p, (size_t)n * sizeof(Sym));
       } else {

@@ -197,6 +197,7 @@ __device__ inline uint32_t probe_slot(unsigned long long* table, uint64_t h, uin
 // item without a built template of its shape is a miss (kKryoMiss, size 0,
 // item_slot kNoSlot: kryo_twrite does not write it).
 __global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_t n, uint32_t group, bool templates_only,
+                                                          bool hash_chain,
                                                           unsigned long long* __restrict__ table,
                                                           const int32_t* __restrict__ slot_size,
                                                           const kryo::ShapeRec* __restrict__ rec,
@@ -216,11 +217,15 @@ __global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_
     item_slot[i] = kRawSlot;
     if (it.len && !it.data) {
       st = 1;
-    } else if (templates_only && it.len >> 29) {  // kryo_hash takes leaves under 2^29 bytes (32-bit bit counts
-                                                  // and block indices): larger RAW leaves take the full chain
-      st = kKryoMiss;
+    } else if (hash_chain && it.len >> 29) {  // kryo_hash takes leaves under 2^29 bytes (32-bit bit counts
+                                              // and block indices): larger RAW leaves take the full chain
       item_slot[i] = kNoSlot;
-      atomicAdd(misses, 1u);
+      if (templates_only) {
+        st = kKryoMiss;
+        atomicAdd(misses, 1u);
+      } else {
+        direct_item(direct, counters, i);  // the device hash chain: hashed by kryo_dhash
+      }
     } else {
       size = it.len;
     }
@@ -697,6 +702,93 @@ __global__ void __launch_bounds__(256) kryo_dwrite_kernel(ItemSrc items, const u
   }
 }
 
+// ---- 6b. direct hashes --------------------------------------------------------------
+// The device hash chain (cordahip_signed_txcomp_verify_ed25519_device) needs the
+// direct items' leaves only as SHA-256 input: the direct encoder runs with a
+// level-0 sink that compresses the bytes as they come (no leaf buffer, no size
+// pass, no scan). A byte at a time through a per-thread block: slow per byte,
+// but the direct list is empty in steady state (new shapes get templates).
+struct ShaSink {
+  static constexpr bool kActive = true;
+  uint32_t st[8];
+  uint32_t w[16];
+  uint32_t n = 0;  // bytes in the current block; a full block is compressed when the next byte arrives
+  __device__ ShaSink() {
+    sha256_init(st);
+    for (int k = 0; k < 16; k++) w[k] = 0;
+  }
+  __device__ void compress() {
+    uint32_t t[16];
+    for (int k = 0; k < 16; k++) t[k] = w[k], w[k] = 0;
+    sha256_block(st, t);
+    n = 0;
+  }
+  __device__ void put(uint8_t b) {
+    if (n == 64) compress();
+    w[n >> 2] |= (uint32_t)b << (24 - 8 * (n & 3));
+    n++;
+  }
+  // n bytes: whole blocks straight from p while more than a block remains behind
+  // them (the last byte stays buffered for mark()), the rest through the block
+  __device__ void write(const uint8_t* p, uint64_t len) {
+    while (len) {
+      if (n == 64) compress();
+      if (n == 0 && len > 64) {
+        uint32_t t[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+          t[k] = ((uint32_t)p[4 * k] << 24) | ((uint32_t)p[4 * k + 1] << 16) | ((uint32_t)p[4 * k + 2] << 8) | p[4 * k + 3];
+        sha256_block(st, t);
+        p += 64;
+        len -= 64;
+        continue;
+      }
+      const uint64_t take = len < 64 - n ? len : 64 - n;
+      for (uint64_t i = 0; i < take; i++, n++) w[n >> 2] |= (uint32_t)p[i] << (24 - 8 * (n & 3));
+      p += take;
+      len -= take;
+    }
+  }
+  __device__ void mark() { w[(n - 1) >> 2] |= 0x80u << (24 - 8 * ((n - 1) & 3)); }
+  __device__ void finish(uint64_t total) {  // FIPS 180-4 padding after `total` bytes
+    if (n == 64) compress();
+    w[n >> 2] |= 0x80u << (24 - 8 * (n & 3));
+    if (n >= 56) {
+      n = 64;
+      compress();
+    }
+    w[14] = (uint32_t)(total >> 29);
+    w[15] = (uint32_t)(total << 3);
+    compress();
+  }
+};
+
+__global__ void __launch_bounds__(256) kryo_dhash_kernel(ItemSrc items, const uint32_t* __restrict__ direct,
+                                                         const uint32_t* __restrict__ counters,
+                                                         uint8_t* __restrict__ status, uint32_t* __restrict__ hashes,
+                                                         uint8_t* __restrict__ ws) {
+  const uint32_t nd = counters[kCDirect];
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint8_t* levels = ws + t * (uint64_t)kLevelSyms;  // levels 1..7 of this thread's OutputChunked buffers
+  for (uint64_t j = t; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t i = direct[j];
+    ShaSink sink;
+    kryo::KoutT<false, ShaSink> o(nullptr, 0, levels);
+    o.sink = &sink;
+    const cordahip_kryo_item it = items[i];
+    const bool ok = kryo::encode_leaf(o, it);
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ok) {
+      sink.finish(o.pos);
+      for (int k = 0; k < 8; k++) h[k] = sink.st[k];
+    }
+    status[i] = ok ? 0 : 1;
+    uint4* out = reinterpret_cast<uint4*>(hashes + (uint64_t)i * 8);
+    out[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    out[1] = make_uint4(h[4], h[5], h[6], h[7]);
+  }
+}
+
 // ---- 7. leaf hashes straight from the templates (the templates-only chain) ---------
 // The component-level signed-tx slices need the leaves only as SHA-256 input:
 // one lane per leaf assembles each 64-byte message block from its template in
@@ -884,17 +976,26 @@ hipError_t kryo_reset_misses(uint8_t* fixed, uint32_t set, hipStream_t s) {
 uint32_t kryo_clear_threshold_slots() { return kSlots / 2; }
 uint32_t kryo_clear_threshold_templates() { return kBuilders - 64; }
 
-hipError_t launch_kryo_shape(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
-                             uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
-                             uint64_t* sizes, uint8_t* status, hipStream_t s, bool templates_only, uint32_t set) {
+static hipError_t shape_launch(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
+                               uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
+                               uint64_t* sizes, uint8_t* status, hipStream_t s, bool templates_only, bool hash_chain,
+                               uint32_t set) {
   if (n == 0) return hipSuccess;
   const ItemSrc items{d_items, data_base, data_len};
   const KryoState k(fixed);
   const uint32_t sb = shape_block(n, group), g = grouped(n, group) ? group : 1;
   hipLaunchKernelGGL(kryo_shape_kernel, dim3((uint32_t)((item_threads(n, group) + sb - 1) / sb)), dim3(sb), 0, s, items,
-                     n, g, templates_only, k.table, k.slot_size, k.rec, item_slot, k.shape_list, sizes, status,
-                     direct, k.counters, k.counters + kCMiss + (set & 1));
+                     n, g, templates_only, hash_chain, k.table, k.slot_size, k.rec, item_slot, k.shape_list, sizes,
+                     status, direct, k.counters, k.counters + kCMiss + (set < 2 ? set : 2));  // [6]: the device hash chain's (unread)
   return hipGetLastError();
+}
+
+hipError_t launch_kryo_shape(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
+                             uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
+                             uint64_t* sizes, uint8_t* status, hipStream_t s, bool templates_only, uint32_t set) {
+  // the shape pass of the templates-only chain feeds kryo_hash: RAW leaves over its limit are misses
+  return shape_launch(d_items, data_base, data_len, n, group, fixed, item_slot, direct, sizes, status, s,
+                      templates_only, templates_only, set);
 }
 
 hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
@@ -911,8 +1012,8 @@ hipError_t launch_kryo_encode(const cordahip_kryo_item* d_items, const uint8_t* 
     e = e ? e : hipMemsetAsync(off, 0, 8, s);
     return e;
   }
-  e = launch_kryo_shape(d_items, data_base, data_len, n, group, fixed, item_slot, direct, sizes, status, s,
-                        templates_only, set);
+  e = shape_launch(d_items, data_base, data_len, n, group, fixed, item_slot, direct, sizes, status, s,
+                   templates_only, templates_only, set);
   // build, tsize, dsize (and dwrite) serve new shapes and direct items; in steady
   // state they find nothing to do, yet beside the Ed25519 ladders of a component
   // batch each empty launch of build / dsize / dwrite took 0.07-0.47 ms on the
@@ -949,6 +1050,37 @@ hipError_t launch_kryo_hash(const cordahip_kryo_item* d_items, const uint8_t* da
   const uint32_t sb = shape_block(n, group), g = grouped(n, group) ? group : 1;
   hipLaunchKernelGGL(kryo_hash_kernel, dim3((uint32_t)((item_threads(n, group) + sb - 1) / sb)), dim3(sb), 0, s, items,
                      n, g, item_slot, k.slot_map, k.arena, sizes, status, hashes);
+  return hipGetLastError();
+}
+
+// The device hash chain: every item's leaf hash without a leaf in memory and
+// without misses. The shape pass claims new shapes (as the full chain does),
+// kryo_build traces their templates, kryo_tsize resolves the items of shapes
+// built in this launch set; kryo_hash hashes every template and RAW item from
+// its template or bytes, and kryo_dhash runs the direct encoder into a SHA-256
+// sink for the rest (collisions, leaves beyond a template, a full arena, RAW
+// leaves of 2^29 bytes or more). Steady state: build / tsize / dhash find
+// nothing to do. dwriters: the dhash threads (ws holds kLevelSyms bytes each).
+hipError_t launch_kryo_hash_chain(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
+                                  uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
+                                  uint64_t* sizes, uint8_t* status, uint32_t* hashes, uint8_t* dws, uint64_t dwriters,
+                                  hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const ItemSrc items{d_items, data_base, data_len};
+  const KryoState k(fixed);
+  hipError_t e = hipMemsetAsync(k.counters, 0, 8, s);  // kCNew, kCDirect
+  e = e ? e : shape_launch(d_items, data_base, data_len, n, group, fixed, item_slot, direct, sizes, status, s, false,
+                           true, 2);
+  if (e) return e;
+  hipLaunchKernelGGL(kryo_build_kernel, dim3(kBuildWaves), dim3(64), 0, s, items, k.table, k.shape_list, k.counters,
+                     k.rec, k.slot_size, k.slot_map, k.arena);
+  hipLaunchKernelGGL(kryo_tsize_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, items, n, item_slot,
+                     k.slot_size, k.rec, sizes, status, direct, k.counters);
+  e = hipGetLastError();
+  e = e ? e : launch_kryo_hash(d_items, data_base, data_len, n, group, fixed, item_slot, sizes, status, hashes, s);
+  if (e) return e;
+  hipLaunchKernelGGL(kryo_dhash_kernel, dim3((uint32_t)std::max<uint64_t>(1, dwriters / 256)), dim3(256), 0, s, items,
+                     direct, k.counters, status, hashes, dws);
   return hipGetLastError();
 }
 

@@ -74,8 +74,15 @@ hipError_t launch_kryo_shape(const cordahip_kryo_item* items, const uint8_t* dat
 hipError_t launch_kryo_hash(const cordahip_kryo_item* items, const uint8_t* data_base, uint64_t data_len, uint64_t n,
                             uint32_t group, uint8_t* fixed, const uint32_t* item_slot, const uint64_t* sizes,
                             const uint8_t* status, uint32_t* hashes, hipStream_t s);
+// the device hash chain (no misses, no leaf bytes): shapes -> build -> tsize ->
+// kryo_hash -> kryo_dhash (the direct encoder into a SHA-256 sink); hashes[n][8]
+// big-endian words, zero for an item the encoder rejects (status 1)
+hipError_t launch_kryo_hash_chain(const cordahip_kryo_item* items, const uint8_t* data_base, uint64_t data_len,
+                                  uint64_t n, uint32_t group, uint8_t* fixed, uint32_t* item_slot, uint32_t* direct,
+                                  uint64_t* sizes, uint8_t* status, uint32_t* hashes, uint8_t* dws, uint64_t dwriters,
+                                  hipStream_t s);
 hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64_t n, uint8_t* rows, hipStream_t s);
-hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
+hipError_t launch_tx_reduce(uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
                             uint8_t* tx_status, hipStream_t s);
 hipError_t launch_pmt_verify(const uint32_t* leaf_hashes, const uint64_t* tx_leaf_off, const uint8_t* tok,
                              const uint8_t* tok_hash, const uint64_t* tx_tok_off, const uint8_t* root, uint64_t ntx,

@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(256) store_to_host_kernel(const uint8_t* __res
 
 // K5: checkSignaturesAreValid order — the first non-OK signature (list order)
 // decides the tx outcome; -1 when every signature verified.
-__global__ void __launch_bounds__(256) tx_reduce_kernel(const uint8_t* __restrict__ sig_status,
+__global__ void __launch_bounds__(256) tx_reduce_kernel(uint8_t* __restrict__ sig_status,
                                                        const uint64_t* __restrict__ tx_sig_off, uint64_t ntx,
                                                        int64_t* __restrict__ first_bad, uint8_t* __restrict__ tx_status) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -255,7 +255,10 @@ __global__ void __launch_bounds__(256) tx_reduce_kernel(const uint8_t* __restric
     tx_status[t] = kTxNoSignatures;
     return;
   }
-  if (tx_status[t] != kStatusOk) return;  // no leaves: the id itself could not be computed
+  if (tx_status[t] != kStatusOk) {  // the id itself could not be computed (no leaves, a bad component):
+    for (uint64_t s = lo; s < hi; s++) sig_status[s] = tx_status[t];  // no signature was checked (host reduce_txs)
+    return;
+  }
   int64_t fb = -1;
   uint8_t st = kStatusOk;
   for (uint64_t s = lo; s < hi; s++) {
@@ -415,7 +418,7 @@ hipError_t launch_gather_rows32(const uint8_t* txid, const uint32_t* idx, uint64
   hipLaunchKernelGGL(gather_rows32_kernel, dim3((uint32_t)((2 * n + 255) / 256)), dim3(256), 0, s, txid, idx, n, rows);
   return hipGetLastError();
 }
-hipError_t launch_tx_reduce(const uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
+hipError_t launch_tx_reduce(uint8_t* sig_status, const uint64_t* tx_sig_off, uint64_t ntx, int64_t* first_bad,
                             uint8_t* tx_status, hipStream_t s) {
   if (!ntx) return hipSuccess;
   hipLaunchKernelGGL(tx_reduce_kernel, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, s, sig_status,

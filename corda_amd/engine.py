@@ -224,6 +224,20 @@ class Engine:
             sigs.data_ptr(), keys.shape[0], txid.data_ptr(), tx_status.data_ptr(), first_bad.data_ptr(),
             sig_status.data_ptr(), s), "cordahip_signed_tx_verify_ed25519_device")
 
+    def signed_txcomp_verify_ed25519_device(self, items, n_items: int, payload, tx_item_off, tx_sig_off, keys, sigs,
+                                            txid, tx_status, first_bad, sig_status, group: int = 1, device: int = 0,
+                                            stream=None):
+        """cordahip_signed_txcomp_verify_ed25519_device: items (device tensor of n_items
+        cordahip_kryo_item records whose `data` are offsets into payload), payload (uint8 device
+        tensor), tx_item_off / tx_sig_off (int64 [ntx + 1]), keys [nsig, 32], sigs [nsig, 64];
+        outputs as in signed_tx_verify_ed25519_device."""
+        s = stream.cuda_stream if stream is not None else 0
+        check(lib().cordahip_signed_txcomp_verify_ed25519_device(
+            self._ctx, device, items.data_ptr(), n_items, group, payload.data_ptr() if payload.numel() else None,
+            payload.numel(), tx_item_off.data_ptr(), tx_item_off.shape[0] - 1, tx_sig_off.data_ptr(),
+            keys.data_ptr(), sigs.data_ptr(), keys.shape[0], txid.data_ptr(), tx_status.data_ptr(),
+            first_bad.data_ptr(), sig_status.data_ptr(), s), "cordahip_signed_txcomp_verify_ed25519_device")
+
     def kryo_encode_device(self, items, n: int, out, off, status, group: int = 1, device: int = 0, stream=None):
         """cordahip_kryo_encode_device: leaf preimages of n components on the GPU. items: a
         device tensor holding n cordahip_kryo_item records (_lib.KRYO_ITEM_DTYPE) whose data

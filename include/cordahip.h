@@ -447,6 +447,29 @@ typedef struct {
 int cordahip_signed_txcomp_verify(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* batch);
 int cordahip_txcomp_submit(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* batch, uint64_t* ticket);
 
+/* Device-resident component-level variant (all Ed25519, 32-byte keys, 64-byte
+ * sigs; every array in HBM on `device`, items[i].data OFFSETS into d_payload as
+ * in cordahip_txcomp_batch): the components' leaf hashes straight from the
+ * encoder's per-shape templates (no leaf bytes; new shapes are traced in the
+ * same launch set, items without a template go through the direct encoder into
+ * a SHA-256 sink, so there is no miss and no second pass) -> K4 Merkle roots ->
+ * txid gather -> K1 verify -> K5 per-tx reduce, all on hip_stream. The ids of
+ * cordahip_signed_txcomp_verify / cordahip_signed_tx_verify over the same
+ * components' leaves; a rejected component makes its transaction
+ * CORDAHIP_TX_BAD_COMPONENT and its signatures carry that status (as a failed
+ * id does in every signed-tx path). group: as in cordahip_kryo_encode_device.
+ * d_tx_item_off / d_tx_sig_off [ntx+1] (uint64) index d_items / the signatures
+ * from 0; device memory is the caller's contract (not readable from the host).
+ * n_items < 2^31 - 1. Replaces the same reference calls as
+ * cordahip_txcomp_submit (SignedTransaction.kt:95-100, WireTransaction.kt:48,
+ * MerkleTransaction.kt:16-18). */
+int cordahip_signed_txcomp_verify_ed25519_device(cordahip_ctx* ctx, int device, const void* d_items,
+                                                 uint64_t n_items, uint32_t group, const void* d_payload,
+                                                 uint64_t payload_len, const void* d_tx_item_off, uint64_t ntx,
+                                                 const void* d_tx_sig_off, const void* d_keys, const void* d_sigs,
+                                                 uint64_t nsig, void* d_txid, void* d_tx_status, void* d_first_bad,
+                                                 void* d_sig_status, void* hip_stream);
+
 /* Device time (ms) of the calling thread's most recent *_device call on
  * `device`, from HIP events recorded around its launches on the stream it ran
  * on (waits for them); -1 if the thread made no such call. Each call gets its

@@ -329,3 +329,147 @@ def test_concurrent_tickets_one_device(engine, oracle):
             del os.environ["CORDAHIP_TX_SIG_CHUNK"]
         else:
             os.environ["CORDAHIP_TX_SIG_CHUNK"] = old
+
+
+def _device_comp_call(engine, blob, items, tio, sigs, group=1):
+    """cordahip_signed_txcomp_verify_ed25519_device over host arrays (copied to the GPU);
+    sigs[t] = [(ED, key, sig), ...]. Returns (ids, tx_status, first_bad, sig_status) as numpy."""
+    import torch
+    dev = torch.device("cuda:0")
+    n = len(tio) - 1
+    flat = [x for per in sigs for x in per]
+    so = np.zeros(n + 1, np.int64)
+    so[1:] = np.cumsum([len(per) for per in sigs])
+    d_items = torch.from_numpy(np.ascontiguousarray(items).view(np.uint8).copy()).to(dev)
+    d_blob = torch.from_numpy(np.ascontiguousarray(blob, dtype=np.uint8).copy()).to(dev) if len(blob) else \
+        torch.zeros(16, dtype=torch.uint8, device=dev)[:0]
+    d_tio = torch.from_numpy(np.asarray(tio, np.int64)).to(dev)
+    d_so = torch.from_numpy(so).to(dev)
+    k = torch.from_numpy(np.frombuffer(b"".join(x[1] for x in flat) or bytes(32), np.uint8).reshape(-1, 32).copy()).to(dev)
+    s = torch.from_numpy(np.frombuffer(b"".join(x[2] for x in flat) or bytes(64), np.uint8).reshape(-1, 64).copy()).to(dev)
+    k, s = k[:len(flat)], s[:len(flat)]
+    txid = torch.zeros((max(n, 1), 32), dtype=torch.uint8, device=dev)
+    st = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
+    fb = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
+    sst = torch.zeros(max(len(flat), 1), dtype=torch.uint8, device=dev)
+    engine.signed_txcomp_verify_ed25519_device(d_items, len(items), d_blob, d_tio, d_so, k, s, txid, st, fb, sst,
+                                               group=group)
+    torch.cuda.synchronize()
+    return txid.cpu().numpy()[:n], st.cpu().numpy()[:n], fb.cpu().numpy()[:n], sst.cpu().numpy()[:len(flat)]
+
+
+def _same(a, b, ctx=""):
+    ids_a, st_a, fb_a, sst_a = a
+    ids_b, st_b, fb_b, sst_b = b
+    assert np.array_equal(st_a, st_b), ctx
+    assert np.array_equal(fb_a, fb_b), ctx
+    assert np.array_equal(sst_a, sst_b), ctx
+    assert np.array_equal(ids_a[st_b == 0], ids_b[st_b == 0]), ctx
+
+
+def test_device_component_call_every_kind(engine, oracle):
+    """The device-resident component call (leaf hashes from the templates, new shapes traced
+    in the same launch set, the rest through the direct encoder's SHA-256 sink) on random
+    transactions of every kind -- invalid components, a transaction without components and
+    ones without signatures, 70,000-character strings (no template: direct) -- called
+    repeatedly (shapes built by the first call, hits afterwards): every output equals the
+    host component path's, and the ids equal the oracle's over the restatement's leaves."""
+    rng = random.Random(57)
+    ntx = 300
+    spec, comps = _random_txs(rng, ntx)
+    comps[3], spec[3] = [], []
+    for t in (11, 150):
+        comps[t] = comps[t] + [("String", "d" * 70_000, 0)]
+        spec[t] = spec[t] + [("String", "d" * 70_000, 0)]
+    comps[40] = comps[40] + [("ed25519_key", b"k" * 31, 45)]  # rejected: BAD_COMPONENT
+    leaves = [[K.leaf(k, v, c) for k, v, c in tx] for tx in spec]
+    ids = [_oracle_id(oracle, lv) if lv and t != 40 else None for t, lv in enumerate(leaves)]
+    sigs = _signers(oracle, rng, ids, ntx)
+    host = engine.signed_txcomp_verify(comps, sigs)
+    flat = [c for tx in comps for c in tx]
+    blob, items, has = _lib.kryo_pack(flat)
+    items = items.copy()
+    items["data"] = np.where(has, items["data"], 0)
+    tio = np.zeros(ntx + 1, np.uint64)
+    tio[1:] = np.cumsum([len(tx) for tx in comps])
+    for rnd in range(3):
+        got = _device_comp_call(engine, blob, items, tio, sigs)
+        _same(got, host, rnd)
+        for t in range(ntx):
+            if ids[t] is not None and sigs[t]:
+                assert got[0][t].tobytes() == ids[t], (rnd, t)
+        assert got[1][40] == _lib.TX_BAD_COMPONENT or not sigs[40]
+
+
+def test_device_component_call_cash_corpus(engine, oracle):
+    """The bench's cash-issue components through the device call (group = 5), corrupted
+    signatures and components included, against the leaf path over the host encoder's leaves
+    and the oracle's ids on a sample; a second corpus of other shapes between two calls."""
+    rng = np.random.default_rng(58)
+    ntx = 20000
+    ik = rng.integers(0, 256, (ntx, 32), dtype=np.uint8)
+    blob, items, layout = cash_issue_items(ik, rng.integers(0, 256, (ntx, 32), dtype=np.uint8), bytes(range(32)),
+                                           rng.integers(1, 10**9, ntx), rng.integers(-2**63, 2**63 - 1, ntx))
+    blob = blob.copy()
+    for t in range(5, ntx, 1000):  # a flipped owner-key byte: another id, the signatures fail
+        blob[layout["owner_key"] + t * layout["cash_stride"]] ^= 1
+    it = items.reshape(-1).copy()
+    host_it = it.copy()
+    host_it["data"] += np.uint64(blob.ctypes.data)
+    hb, ho = _lib.kryo_encode_array(host_it)
+    leaves = [[hb[int(ho[5 * t + j]):int(ho[5 * t + j + 1])].tobytes() for j in range(5)] for t in range(ntx)]
+    ids_l, _ = engine.tx_ids(leaves)
+    assert [ids_l[t].tobytes() for t in range(0, ntx, 1999)] == [_oracle_id(oracle, leaves[t])
+                                                                 for t in range(0, ntx, 1999)]
+    sig_id = ids_l.copy()
+    for t in range(5, ntx, 1000):
+        sig_id[t] ^= 0xff  # signed over the id before the corruption (any other id)
+    sigs = []
+    for t in range(ntx):
+        per = []
+        for q in range(1 + t % 3):
+            pub, sg = _sign(oracle, hashlib.sha256(b"dc%d-%d" % (t, q)).digest(), sig_id[t].tobytes())
+            if t % 17 == 4 and q == 0:
+                sg = sg[:20] + bytes([sg[20] ^ 8]) + sg[21:]
+            per.append((ED, pub, sg))
+        sigs.append(per)
+    want = engine.signed_tx_verify(leaves, sigs)
+    tio = np.arange(0, 5 * ntx + 1, 5, dtype=np.uint64)
+    got = _device_comp_call(engine, blob, it, tio, sigs, group=5)
+    _same(got, want)
+    assert (want[1] == 1).sum() == len(set(range(5, ntx, 1000)) | set(range(4, ntx, 17)))
+    other = [[("String", "x" * (100 + t), 0), ("long", t, 0)] for t in range(50)]
+    ob, oi, oh = _lib.kryo_pack([c for tx in other for c in tx])
+    oi = oi.copy()
+    oi["data"] = np.where(oh, oi["data"], 0)
+    oleaves = [[K.leaf(k, v, c) for k, v, c in tx] for tx in other]
+    oids = [_oracle_id(oracle, lv) for lv in oleaves]
+    osigs = [[(ED,) + _sign(oracle, b"\x21" * 32, oids[t])] for t in range(50)]
+    og = _device_comp_call(engine, ob, oi, np.arange(0, 101, 2, dtype=np.uint64), osigs)
+    assert [og[0][t].tobytes() for t in range(50)] == oids and (og[1] == 0).all()
+    got = _device_comp_call(engine, blob, it, tio, sigs, group=5)
+    _same(got, want)
+
+
+def test_raw_leaf_over_2_29_bytes(engine, oracle):
+    """A RAW component of 2^29 + 3 bytes (512 MiB): kryo_hash takes leaves under 2^29 bytes,
+    so the templates-only chain counts it a miss (the call is redone with the full chain) and
+    the device chain hashes it through the direct encoder's SHA-256 sink (64-bit bit length).
+    Its transaction's id against hashlib (one leaf: the root is the leaf hash)."""
+    big = np.frombuffer(np.random.default_rng(59).bytes((1 << 29) + 3), np.uint8)
+    leaf_hash = hashlib.sha256(big.tobytes()).digest()
+    items = np.zeros(1, _lib.KRYO_ITEM_DTYPE)
+    items[0]["kind"], items[0]["len"], items[0]["data"] = 0, big.size, 0
+    tio = np.array([0, 1], np.uint64)
+    sigs = [[(ED,) + _sign(oracle, b"\x31" * 32, leaf_hash)]]
+    # small component batches first, so the device's component calls run the templates-only chain
+    small = [[("int", 7, 0), ("long", 9, 0)]] * 4
+    sm_ids = [_oracle_id(oracle, [K.leaf(k, v, c) for k, v, c in tx]) for tx in small]
+    for _ in range(3):
+        engine.signed_txcomp_verify(small, [[(ED,) + _sign(oracle, b"\x32" * 32, i)] for i in sm_ids])
+    print("templates-only chain warm; the 512 MiB leaf through the host call", flush=True)
+    host = engine.signed_txcomp_verify_arrays(big, items, tio, sigs)
+    assert host[0][0].tobytes() == leaf_hash and host[1][0] == 0 and host[3][0] == 0
+    print("host call ok; the device call", flush=True)
+    dev = _device_comp_call(engine, big, items, tio, sigs)
+    assert dev[0][0].tobytes() == leaf_hash and dev[1][0] == 0 and dev[3][0] == 0
