@@ -1275,8 +1275,10 @@ void free_device(Device& d) {
       b->release();
     if (S.kryo_usage) (void)hipHostFree(S.kryo_usage);
     S.kryo_usage = S.kryo_usage_dev = nullptr;
-    if (S.tx_ev) (void)hipEventDestroy(S.tx_ev);
-    S.tx_ev = nullptr;
+    for (hipEvent_t* pe : {&S.tx_ev, &S.fork, &S.ids}) {
+      if (*pe) (void)hipEventDestroy(*pe);
+      *pe = nullptr;
+    }
   }
   for (auto& st : d.sstage) {
     for (DevBuf* b : {&st.ed_keys, &st.ed_sigs, &st.ed_msgs, &st.ed_status, &st.ec_scheme, &st.ec_keys,
@@ -1379,7 +1381,8 @@ static int init_impl(uint32_t device_mask, cordahip_ctx** out) {
       break;
     }
     for (TxSet& S : dev.set)
-      if (hipEventCreateWithFlags(&S.tx_ev, hipEventDisableTiming) != hipSuccess) rc = CORDAHIP_ERR_HIP;
+      for (hipEvent_t* pe : {&S.tx_ev, &S.fork, &S.ids})
+        if (hipEventCreateWithFlags(pe, hipEventDisableTiming) != hipSuccess) rc = CORDAHIP_ERR_HIP;
     if (rc != CORDAHIP_SUCCESS) break;
     for (auto& tc : dev.ring)
       if (hipEventCreate(&tc.a) != hipSuccess || hipEventCreate(&tc.b) != hipSuccess) rc = CORDAHIP_ERR_HIP;
@@ -1668,19 +1671,33 @@ int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, cons
     if (w.hashes.ensure(std::max<uint64_t>(nleaves, 1) * 32) || w.msgs.ensure(std::max<uint64_t>(nsig, 1) * 32))
       return CORDAHIP_ERR_OUT_OF_MEMORY;
   }
+  if (ensure_streams(*d) != hipSuccess) return CORDAHIP_ERR_HIP;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  // CORDAHIP_DEVICE_SPLIT=1: the id kernels fork onto the device's id stream beside the
+  // key half of the Ed25519 prep on s (off by default: slower, see the component call)
+  static const bool split = getenv("CORDAHIP_DEVICE_SPLIT") && getenv("CORDAHIP_DEVICE_SPLIT")[0] == '1';
+  hipStream_t x = split ? d->s_idcopy : s;
   TimedCall* tc = timed_begin(*d, s);
   if (!tc) return CORDAHIP_ERR_HIP;
   hipError_t e = hipStreamWaitEvent(s, S.tx_ev, 0);  // the previous user of w.hashes / w.msgs is done
+  if (split) {
+    e = e ? e : hipEventRecord(S.fork, s);
+    e = e ? e : hipStreamWaitEvent(x, S.fork, 0);
+  }
   e = e ? e : launch_sha256_leaves(static_cast<const uint8_t*>(d_leaf_bytes), static_cast<const uint64_t*>(d_leaf_off),
-                                   nleaves, w.hashes.as<uint32_t>(), s);
+                                   nleaves, w.hashes.as<uint32_t>(), x);
   e = e ? e : launch_merkle_root(w.hashes.as<uint32_t>(), static_cast<const uint64_t*>(d_tx_leaf_off), ntx,
-                                 static_cast<uint8_t*>(d_txid), static_cast<uint8_t*>(d_tx_status), s);
-  e = e ? e : launch_gather_txid(static_cast<const uint8_t*>(d_txid), static_cast<const uint64_t*>(d_tx_sig_off), ntx,
-                                 w.msgs.as<uint8_t>(), s);
+                                 static_cast<uint8_t*>(d_txid), static_cast<uint8_t*>(d_tx_status), x);
+  if (split) e = e ? e : hipEventRecord(S.ids, x);
+  const std::function<hipError_t()> join = [&]() -> hipError_t {  // the ids, then the signatures' messages
+    hipError_t r = split ? hipStreamWaitEvent(s, S.ids, 0) : hipSuccess;
+    return r ? r : launch_gather_txid(static_cast<const uint8_t*>(d_txid), static_cast<const uint64_t*>(d_tx_sig_off),
+                                      ntx, w.msgs.as<uint8_t>(), s);
+  };
+  if (nsig == 0) e = e ? e : join();
   e = e ? e : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
                                 w.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status), nullptr,
-                                0u, s);
+                                0u, s, 0, nsig ? &join : nullptr);
   e = e ? e : hipEventRecord(S.tx_ev, s);  // fences w.hashes / w.msgs for the next user
   e = e ? e : launch_tx_reduce(static_cast<uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off),
                                ntx, static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);
@@ -1768,13 +1785,25 @@ int cordahip_signed_txcomp_verify_ed25519_device(cordahip_ctx* ctx, int device, 
           d->kryo_ws.ensure(kryo_direct_ws_bytes(dwriters)) || kryo_fixed_ensure(*d))
         return CORDAHIP_ERR_OUT_OF_MEMORY;
     }
+    if (ensure_streams(*d) != hipSuccess) return CORDAHIP_ERR_HIP;
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    // CORDAHIP_DEVICE_SPLIT=1: the id chain forks onto the device's id stream and runs
+    // beside the key half of the Ed25519 prep (key and R decoding: no dependence on the
+    // ids) on s, which joins it before the message half. Off: the split prep's two
+    // launches cost more than the overlap gains (c4 --device-encode 87.3-87.4 against
+    // 89.1-89.2 M sig/s, c4 95.6-95.9 against 96.1-96.5; profiles/r06_device_split_ab/)
+    static const bool split = getenv("CORDAHIP_DEVICE_SPLIT") && getenv("CORDAHIP_DEVICE_SPLIT")[0] == '1';
+    hipStream_t x = split ? d->s_idcopy : s;
     TimedCall* tc = timed_begin(*d, s);
     if (!tc) return CORDAHIP_ERR_HIP;
     uint32_t* slots = d->kryo_items.as<uint32_t>();
     hipError_t e = hipStreamWaitEvent(s, S.tx_ev, 0);  // the previous users of the set's buffers
     e = e ? e : hipStreamWaitEvent(s, d->kryo_ev, 0);  // and of the encoder's scratch are done
-    e = e ? e : kryo_state_ready(*d, s);
+    if (split) {
+      e = e ? e : hipEventRecord(S.fork, s);
+      e = e ? e : hipStreamWaitEvent(x, S.fork, 0);
+    }
+    e = e ? e : kryo_state_ready(*d, x);
     // leaf hashes from the templates (misses impossible: new shapes are built, the rest
     // hashed by the direct encoder), then the ids, with a rejected component making its
     // transaction CORDAHIP_TX_BAD_COMPONENT
@@ -1783,17 +1812,22 @@ int cordahip_signed_txcomp_verify_ed25519_device(cordahip_ctx* ctx, int device, 
                                    static_cast<const uint8_t*>(d_payload), payload_len, n_items, group,
                                    d->kryo_fixed.as<uint8_t>(), slots, slots + n_items, d->kryo_sizes.as<uint64_t>(),
                                    w.comp_status.as<uint8_t>(), w.hashes.as<uint32_t>(), d->kryo_ws.as<uint8_t>(),
-                                   dwriters, s);
-    e = e ? e : kryo_usage_report(*d, nullptr, s);
-    e = e ? e : hipEventRecord(d->kryo_ev, s);
+                                   dwriters, x);
+    e = e ? e : kryo_usage_report(*d, nullptr, x);
+    e = e ? e : hipEventRecord(d->kryo_ev, x);
     e = e ? e : launch_merkle_root(w.hashes.as<uint32_t>(), static_cast<const uint64_t*>(d_tx_item_off), ntx,
-                                   static_cast<uint8_t*>(d_txid), static_cast<uint8_t*>(d_tx_status), s,
+                                   static_cast<uint8_t*>(d_txid), static_cast<uint8_t*>(d_tx_status), x,
                                    w.comp_status.as<uint8_t>());
-    e = e ? e : launch_gather_txid(static_cast<const uint8_t*>(d_txid), static_cast<const uint64_t*>(d_tx_sig_off), ntx,
-                                   w.msgs.as<uint8_t>(), s);
+    if (split) e = e ? e : hipEventRecord(S.ids, x);
+    const std::function<hipError_t()> join = [&]() -> hipError_t {  // the ids, then the signatures' messages
+      hipError_t r = split ? hipStreamWaitEvent(s, S.ids, 0) : hipSuccess;
+      return r ? r : launch_gather_txid(static_cast<const uint8_t*>(d_txid), static_cast<const uint64_t*>(d_tx_sig_off),
+                                        ntx, w.msgs.as<uint8_t>(), s);
+    };
+    if (nsig == 0) e = e ? e : join();
     e = e ? e : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
                                   w.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status), nullptr,
-                                  0u, s);
+                                  0u, s, 0, nsig ? &join : nullptr);
     e = e ? e : hipEventRecord(S.tx_ev, s);  // fences the set's buffers for the next user
     e = e ? e : launch_tx_reduce(static_cast<uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off), ntx,
                                  static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);

@@ -838,11 +838,27 @@ __device__ inline void leaf_piece(const HashSrc& h, uint32_t p, uint64_t desc, u
       }
       return;  // the copy and the descriptor are zero past the leaf
     }
-    const uint32_t* syms = reinterpret_cast<const uint32_t*>(h.tmpl);
+    // byte by byte from the symbols: the piece's 16 symbols in four 16-byte loads (the
+    // same address in every lane of the wave), then every payload byte's load issued
+    // before any is used (r05 walked them one dependent load pair at a time)
+    const uint4* sp = reinterpret_cast<const uint4*>(h.tmpl + 4 * (size_t)lo);
+    const uint4 q0 = sp[0], q1 = sp[1], q2 = sp[2], q3 = sp[3];
+    const uint32_t sy[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                             q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+    uint32_t pb[16];
+#pragma unroll
+    for (uint32_t t = 0; t < 16; t++)
+      pb[t] = (t <= last && (sy[t] & kryo::kSymTypeMask) == kryo::kSymPayload)
+                  ? h.data[(sy[t] >> 8) & (kryo::kMaxPayloadOff - 1)] : 0u;
 #pragma unroll
     for (int i = 0; i < 4; i++) v[i] = 0;
-    for (uint32_t t = 0; t <= last; t++)
-      v[t >> 2] |= (uint32_t)kryo::sym_byte(syms[lo + t], h.data, h.value) << (8 * (t & 3));
+#pragma unroll
+    for (uint32_t t = 0; t < 16; t++) {
+      const uint32_t x = sy[t], ty = x & kryo::kSymTypeMask;
+      uint32_t b = ty == kryo::kSymPayload ? (pb[t] | ((x & kryo::kSymOr80) ? 0x80u : 0u))
+                   : ty == kryo::kSymConst ? (x & 0xffu) : (uint32_t)kryo::sym_byte(x, nullptr, h.value);
+      v[t >> 2] |= (t <= last ? b : 0u) << (8 * (t & 3));
+    }
     return;
   }
   if (last < 15) {  // RAW: the window holds only the leaf's bytes
@@ -854,7 +870,9 @@ __device__ inline void leaf_piece(const HashSrc& h, uint32_t p, uint64_t desc, u
   }
 }
 
-__global__ void __launch_bounds__(1024) kryo_hash_kernel(ItemSrc items, uint64_t n, uint32_t group,
+template <int kMinWaves>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kMinWaves, 8)))
+kryo_hash_kernel(ItemSrc items, uint64_t n, uint32_t group,
                                                          const uint32_t* __restrict__ item_slot,
                                                          const uint32_t* __restrict__ slot_map,
                                                          const uint32_t* __restrict__ arena,
@@ -1048,8 +1066,23 @@ hipError_t launch_kryo_hash(const cordahip_kryo_item* d_items, const uint8_t* da
   const ItemSrc items{d_items, data_base, data_len};
   const KryoState k(fixed);
   const uint32_t sb = shape_block(n, group), g = grouped(n, group) ? group : 1;
-  hipLaunchKernelGGL(kryo_hash_kernel, dim3((uint32_t)((item_threads(n, group) + sb - 1) / sb)), dim3(sb), 0, s, items,
-                     n, g, item_slot, k.slot_map, k.arena, sizes, status, hashes);
+  // waves per SIMD the register allocation must allow (CORDAHIP_KRYO_HASH_WAVES, A/B): 5
+  // (96 VGPRs, 40 B of spills) against 4 (117 VGPRs): 2.43 against 2.67 ms per 6.25 M
+  // leaves of C4 on the device chain, 6 (80 VGPRs, 112 B of spills) 2.56 (profiles/r06_kryo_hash_waves_ab/)
+  static const int waves = [] {
+    const char* v = getenv("CORDAHIP_KRYO_HASH_WAVES");
+    return v ? atoi(v) : 5;
+  }();
+  const dim3 grid((uint32_t)((item_threads(n, group) + sb - 1) / sb)), blk(sb);
+  if (waves >= 6)
+    hipLaunchKernelGGL(kryo_hash_kernel<6>, grid, blk, 0, s, items, n, g, item_slot, k.slot_map, k.arena, sizes, status,
+                       hashes);
+  else if (waves == 5)
+    hipLaunchKernelGGL(kryo_hash_kernel<5>, grid, blk, 0, s, items, n, g, item_slot, k.slot_map, k.arena, sizes, status,
+                       hashes);
+  else
+    hipLaunchKernelGGL(kryo_hash_kernel<1>, grid, blk, 0, s, items, n, g, item_slot, k.slot_map, k.arena, sizes, status,
+                       hashes);
   return hipGetLastError();
 }
 

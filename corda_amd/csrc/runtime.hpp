@@ -207,6 +207,9 @@ struct TxSet {
   // host-mapped: [templates in the arena, table slots in use, misses of set 0, of set 1]
   uint32_t* kryo_usage = nullptr;
   uint32_t* kryo_usage_dev = nullptr;
+  // the device signed-tx calls' fork / join: the id chain runs on the id stream beside
+  // the key half of the Ed25519 prep on the caller's stream
+  hipEvent_t fork = nullptr, ids = nullptr;
 };
 constexpr int kTxSets = 2;
 

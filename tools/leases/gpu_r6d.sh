@@ -1,0 +1,13 @@
+# r06: kernel summary of c4 --device-encode (the device component chain) beside c4
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r6d
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+prof() {  # name, args
+  timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/p_$1 -o $1 -- python3 $R/bench.py --no-cpu-baseline --no-clock --steps 6 --warmup 2 $2 > $O/prof_$1.log 2>&1 || { echo "prof $1 failed"; tail -20 $O/prof_$1.log; exit 1; }
+  find /tmp/p_$1 -name "*kernel_stats.csv" -exec cp {} $O/$1_kernel_stats.csv \;
+  find /tmp/p_$1 -name "*kernel_trace.csv" -exec cp {} $O/$1_kernel_trace.csv \;
+  grep -h '^{' $O/prof_$1.log > $O/$1_line.json || true
+}
+prof c4de "--workload c4 --device-encode"

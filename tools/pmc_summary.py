@@ -11,7 +11,7 @@ tot = defaultdict(lambda: defaultdict(float))
 disp = defaultdict(set)
 for path in paths:
     for r in csv.DictReader(open(path)):
-        k = r["Kernel_Name"].split("(")[0]
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
         tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add((path, r["Dispatch_Id"]))
 out = {}
