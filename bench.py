@@ -699,7 +699,8 @@ class _HostSigBatch:
         self.status = _pinned(np.zeros(n, np.uint8))
         self.verdict = _pinned(np.zeros((n + 63) // 64, np.uint64))
         p = [x.data_ptr() for x in self.t]
-        self.b = _lib.SigBatch(n, *p, self.status.data_ptr(), self.verdict.data_ptr(), 0)
+        self.b = _lib.SigBatch(n, *p, self.status.data_ptr(), self.verdict.data_ptr(), 0,
+                               self.t[1].numel(), self.t[3].numel(), self.t[5].numel())
 
     def run(self, eng):
         import ctypes
@@ -832,9 +833,9 @@ class C4H(C4):
                                            payload, self.tx_sig_off.cpu().numpy().astype(np.uint64)) + sig_arrays]
             p = [x.data_ptr() for x in self.t]
             for txid, txst, sst, fb in self.outs:
-                tb = _lib.TxcompBatch(ntx, p[0], p[1], p[2], payload.size, txid.data_ptr(), txst.data_ptr())
+                tb = _lib.TxcompBatch(ntx, p[0], p[1], p[2], payload.size, txid.data_ptr(), txst.data_ptr(), items.size)
                 self.bs.append(_lib.SignedTxcompBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], sst.data_ptr(),
-                                                      fb.data_ptr()))
+                                                      fb.data_ptr(), ns, self.t[5].numel(), self.t[7].numel()))
             self.pcie_tx_bytes = (items.nbytes + 8 * (5 * ntx + 1) + payload.size) / ntx
             what = ("the components of each tx (cordahip_txcomp_submit: %.0f B per tx of Kryo items and payload; "
                     "the GPU writes the %.0f B of leaves)" % (self.pcie_tx_bytes, self.leaf_bytes.numel() / ntx))
@@ -847,9 +848,10 @@ class C4H(C4):
                 + sig_arrays]
             p = [x.data_ptr() for x in self.t]
             for txid, txst, sst, fb in self.outs:
-                tb = _lib.TxidBatch(ntx, p[0], p[1], p[2], txid.data_ptr(), txst.data_ptr())
+                tb = _lib.TxidBatch(ntx, p[0], p[1], p[2], txid.data_ptr(), txst.data_ptr(), self.t[1].numel() - 1,
+                                    self.t[0].numel())
                 self.bs.append(_lib.SignedTxBatch(tb, p[3], p[4], p[5], p[6], p[7], p[8], sst.data_ptr(),
-                                                  fb.data_ptr()))
+                                                  fb.data_ptr(), ns, self.t[5].numel(), self.t[7].numel()))
             self.pcie_tx_bytes = (self.leaf_bytes.numel() + 8 * (self.leaf_off.numel() + ntx + 1)) / ntx
             what = ("native Kryo leaves, %.0f B per tx" % (self.leaf_bytes.numel() / ntx) if self.native
                     else "5 leaves of %s B" % list(C4_LEAF_LENS))

@@ -42,7 +42,7 @@ ERR_BUFFER_TOO_SMALL = -8
 KRYO_KINDS = {"raw": 0, "char": 1, "short": 2, "int": 3, "long": 4, "byte": 5, "boolean": 6, "float": 7,
               "double": 8, "String": 9, "ed25519_key": 10, "public_key": 11, "kotlin_object": 12, "party": 13,
               "issue_command": 14, "cash_state": 15}
-ABI_VERSION = 3
+ABI_VERSION = 4
 FLAG_IS_VALID = 1  # CORDAHIP_FLAG_IS_VALID: Crypto.isValid semantics (no emptiness checks)
 TX_NO_LEAVES, TX_NO_SIGNATURES, TX_BAD_TREE, TX_BAD_COMPONENT = 6, 7, 8, 9
 
@@ -67,6 +67,7 @@ class SigBatch(ctypes.Structure):
         ("status", ctypes.c_void_p),
         ("verdict", ctypes.c_void_p),
         ("flags", ctypes.c_uint32),
+        ("key_bytes", ctypes.c_uint64), ("sig_bytes", ctypes.c_uint64), ("msg_bytes", ctypes.c_uint64),  # ABI 4
     ]
 
 
@@ -82,6 +83,7 @@ class TxidBatch(ctypes.Structure):
         ("ntx", ctypes.c_uint64),
         ("leaf_bytes", ctypes.c_void_p), ("leaf_off", ctypes.c_void_p), ("tx_leaf_off", ctypes.c_void_p),
         ("txid", ctypes.c_void_p), ("tx_status", ctypes.c_void_p),
+        ("nleaves", ctypes.c_uint64), ("leaf_bytes_len", ctypes.c_uint64),  # ABI 4
     ]
 
 
@@ -93,6 +95,7 @@ class SignedTxBatch(ctypes.Structure):
         ("key", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
         ("sig", ctypes.c_void_p), ("sig_off", ctypes.c_void_p),
         ("sig_status", ctypes.c_void_p), ("first_bad_sig", ctypes.c_void_p),
+        ("nsig", ctypes.c_uint64), ("key_bytes", ctypes.c_uint64), ("sig_bytes", ctypes.c_uint64),  # ABI 4
     ]
 
 
@@ -102,6 +105,7 @@ class TxcompBatch(ctypes.Structure):
         ("items", ctypes.c_void_p), ("tx_item_off", ctypes.c_void_p),
         ("payload", ctypes.c_void_p), ("payload_len", ctypes.c_uint64),
         ("txid", ctypes.c_void_p), ("tx_status", ctypes.c_void_p),
+        ("n_items", ctypes.c_uint64),  # ABI 4
     ]
 
 
@@ -113,6 +117,7 @@ class SignedTxcompBatch(ctypes.Structure):
         ("key", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
         ("sig", ctypes.c_void_p), ("sig_off", ctypes.c_void_p),
         ("sig_status", ctypes.c_void_p), ("first_bad_sig", ctypes.c_void_p),
+        ("nsig", ctypes.c_uint64), ("key_bytes", ctypes.c_uint64), ("sig_bytes", ctypes.c_uint64),  # ABI 4
     ]
 
 
@@ -122,6 +127,7 @@ class FilteredTxBatch(ctypes.Structure):
         ("leaf_bytes", ctypes.c_void_p), ("leaf_off", ctypes.c_void_p), ("tx_leaf_off", ctypes.c_void_p),
         ("tok", ctypes.c_void_p), ("tok_hash", ctypes.c_void_p), ("tx_tok_off", ctypes.c_void_p),
         ("root", ctypes.c_void_p), ("tx_status", ctypes.c_void_p),
+        ("nleaves", ctypes.c_uint64), ("leaf_bytes_len", ctypes.c_uint64), ("ntok", ctypes.c_uint64),  # ABI 4
     ]
 
 

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "csr_check.hpp"
 #include "der.hpp"
 #include "kryo_core.hpp"
 #include "runtime.hpp"
@@ -358,6 +359,15 @@ namespace {
 
 std::atomic<uint64_t> g_device_uid{1};
 
+// the context's host pool as csr_check.hpp's parallel runner
+struct PoolPar {
+  HostPool& pool;
+  template <class F>
+  void operator()(uint64_t n, uint64_t grain, F&& fn) const {
+    pool.parallel_for(n, grain, std::function<void(uint64_t, uint64_t)>(fn));
+  }
+};
+
 // device uid -> (ring slot, generation) of this thread's most recent timed call
 thread_local std::unordered_map<uint64_t, std::pair<int, uint64_t>> tl_last_call;
 
@@ -435,6 +445,7 @@ int tx_ids_impl(cordahip_ctx* ctx, const cordahip_txid_batch* b) {
   if (b->ntx && (!b->leaf_off || !b->tx_leaf_off || !b->txid || !b->tx_status || !b->leaf_bytes))
     return CORDAHIP_ERR_INVALID_ARG;
   if (b->ntx == 0) return CORDAHIP_SUCCESS;
+  if (!check_txid_batch(PoolPar{*ctx->host}, b)) return CORDAHIP_ERR_INVALID_ARG;  // before any enqueue
   // contiguous tx shards: a transaction's tree stays on one device
   return for_shards(ctx->devs, b->ntx, 1,
                     [&](Device& d, uint64_t t0, uint64_t t1) { return tx_ids_shard(ctx, d, b, t0, t1); });
@@ -890,7 +901,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
     mv.dev = &di;
     // checkSignaturesAreValid -> sig.verify -> Crypto.doVerify: doVerify semantics
     cordahip_sig_batch sb{b->tx_sig_off[b->tx.ntx], b->scheme, b->key, b->key_off, b->sig, b->sig_off, b->tx.txid,
-                          nullptr, b->sig_status, nullptr, 0u};
+                          nullptr, b->sig_status, nullptr, 0u, b->key_bytes, b->sig_bytes, 0};
     try {
       r = sig_verify_range(ctx, d, S, &sb, mv, s0, s1);
     } catch (const std::bad_alloc&) {
@@ -982,6 +993,12 @@ int signed_tx_impl(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b, const c
   } else if (!b->tx.leaf_off || !b->tx.tx_leaf_off || !b->tx.txid || !b->tx.tx_status || !b->tx.leaf_bytes) {
     return CORDAHIP_ERR_INVALID_ARG;
   }
+  // the CSR levels (csr_check.hpp), whole, before any enqueue: the leaves or the
+  // items, then the signatures
+  const PoolPar par{*ctx->host};
+  if (comps ? !check_txcomp_batch(par, comps) : !check_txid_batch(par, &b->tx)) return CORDAHIP_ERR_INVALID_ARG;
+  if (!check_sig_level(par, ntx, b->tx_sig_off, b->nsig, b->key_off, b->key_bytes, b->sig_off, b->sig_bytes))
+    return CORDAHIP_ERR_INVALID_ARG;
   const uint64_t nsig = b->tx_sig_off[ntx];
   if (nsig && (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off)) return CORDAHIP_ERR_INVALID_ARG;
   const double t0 = tracing() ? now_ms() : 0;
@@ -1049,6 +1066,9 @@ int signed_txcomp_impl(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* cb
   b.sig_off = cb->sig_off;
   b.sig_status = cb->sig_status;
   b.first_bad_sig = cb->first_bad_sig;
+  b.nsig = cb->nsig;
+  b.key_bytes = cb->key_bytes;
+  b.sig_bytes = cb->sig_bytes;
   return signed_tx_impl(ctx, &b, &cb->tx);
 }
 
@@ -1242,6 +1262,7 @@ int filtered_tx_impl(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* b) {
   if (!b->leaf_off || !b->tx_leaf_off || !b->tx_tok_off || !b->root || !b->tx_status ||
       (!b->tok && b->tx_tok_off[n]) || (!b->tok_hash && b->tx_tok_off[n]))
     return CORDAHIP_ERR_INVALID_ARG;
+  if (!check_filtered_batch(PoolPar{*ctx->host}, b)) return CORDAHIP_ERR_INVALID_ARG;  // before any enqueue
   return for_shards(ctx->devs, n, 1, [&](Device& d, uint64_t t0, uint64_t t1) { return filtered_tx_shard(d, b, t0, t1); });
 }
 

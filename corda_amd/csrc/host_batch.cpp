@@ -184,6 +184,7 @@ struct PieceInfo {
   std::vector<uint32_t> ed_global;               // piece-local group -> chunk group
   uint64_t ec = 0, ec_bytes = 0;                 // ECDSA lanes and their message bytes
   bool too_long = false;
+  bool bad_csr = false;                          // a lane's CSR ranges outside the batch's buffers
 };
 
 // One device's input shard [lo, hi) of a generic batch, streamed in chunks
@@ -286,7 +287,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_ba
         PieceInfo& P = pieces[q];
         P.ed.clear();
         P.ec = P.ec_bytes = 0;
-        P.too_long = false;
+        P.too_long = P.bad_csr = false;
         // length -> group: the previous lane's group first (batches are mostly
         // one message length), a hash map once a piece has many lengths, so a
         // batch of adversarially varied lengths stays linear
@@ -295,7 +296,10 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_ba
         for (uint64_t r = q * kGrain; r < std::min(m, (q + 1) * kGrain); r++) {
           uint64_t mlen = 0;
           uint16_t c = classify(b, mv, a + r, mlen);
-          if (c == kEc) {
+          if (c == kBadCsr) {
+            P.bad_csr = true;
+            c = kDirect;  // not packed: the chunk is not enqueued
+          } else if (c == kEc) {
             P.ec++;
             P.ec_bytes += mlen;
           } else if (c == kEdBase) {
@@ -328,7 +332,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_ba
     // (2) chunk layout: groups by length, rows and message offsets per piece
     lens.clear();
     for (const PieceInfo& P : pieces) {
-      if (P.too_long) rc = CORDAHIP_ERR_INVALID_ARG;
+      if (P.too_long || P.bad_csr) rc = CORDAHIP_ERR_INVALID_ARG;
       for (const auto& kv : P.ed) lens.push_back(kv.first);
     }
     if (rc != CORDAHIP_SUCCESS) break;
@@ -585,6 +589,7 @@ int sig_verify_impl(cordahip_ctx* ctx, const cordahip_sig_batch* b) {
   if (!b->scheme || !b->key || !b->key_off || !b->sig || !b->sig_off || !b->msg || !b->msg_off || !b->status ||
       (b->flags & ~CORDAHIP_FLAG_IS_VALID))
     return CORDAHIP_ERR_INVALID_ARG;
+  // every lane's ranges are checked as its chunk is classified (pack_rows.hpp classify)
   return sig_verify_msgs(ctx, b, MsgView{b->msg, b->msg_off, nullptr});
 }
 

@@ -36,13 +36,22 @@ inline void pack_ed_row(const cordahip_sig_batch* b, const MV& mv, bool do_verif
 }
 
 // Lane classes of a generic batch: the per-lane checks that precede the
-// engines (statuses decided here are written at once).
-enum : uint16_t { kDirect = 0, kEc = 1, kEdBase = 2 };
+// engines (statuses decided here are written at once). kBadCsr: the lane's CSR
+// ranges are not inside the batch's buffers (csr_check.hpp: the batch fails with
+// CORDAHIP_ERR_INVALID_ARG before its chunk is packed).
+enum : uint16_t { kDirect = 0, kEc = 1, kEdBase = 2, kBadCsr = 0xffff };
 
 template <class MV>
 inline uint16_t classify(const cordahip_sig_batch* b, const MV& mv, uint64_t i, uint64_t& mlen) {
+  // the lane's ranges first, before any byte of it is read: non-decreasing and inside
+  // the declared buffers (key_off[i + 1] <= key_bytes, ...; messages of a signed-tx
+  // batch are its transactions' ids, checked with the transactions)
+  const uint64_t k0 = b->key_off[i], k1 = b->key_off[i + 1], s0 = b->sig_off[i], s1 = b->sig_off[i + 1];
+  mlen = 0;
+  if (k1 < k0 || k1 > b->key_bytes || s1 < s0 || s1 > b->sig_bytes) return kBadCsr;
+  if (!mv.tx_of && (mv.off[i + 1] < mv.off[i] || mv.off[i + 1] > b->msg_bytes)) return kBadCsr;
   const uint8_t sch = b->scheme[i];
-  const uint64_t kl = b->key_off[i + 1] - b->key_off[i];
+  const uint64_t kl = k1 - k0;
   mlen = mv.len(i);
   if (sch == CORDAHIP_SCHEME_ECDSA_SECP256K1_SHA256 || sch == CORDAHIP_SCHEME_ECDSA_SECP256R1_SHA256) {
     if (kl != 33 && kl != 65) {

@@ -67,7 +67,7 @@ class Engine:
         status = np.zeros(max(n, 1), dtype=np.uint8)
         verdict = np.zeros(max((n + 63) // 64, 1), dtype=np.uint64)
         b = SigBatch(n, _ptr(sch), _ptr(kb), _ptr(ko), _ptr(sb), _ptr(so), _ptr(mb), _ptr(mo),
-                     _ptr(status), _ptr(verdict), _lib.FLAG_IS_VALID if is_valid else 0)
+                     _ptr(status), _ptr(verdict), _lib.FLAG_IS_VALID if is_valid else 0, kb.size, sb.size, mb.size)
         keep = (sch, kb, ko, sb, so, mb, mo, status, verdict, b)
         if async_:
             t = ctypes.c_uint64()
@@ -121,7 +121,7 @@ class Engine:
             to[1:] = np.cumsum([len(tx) for tx in txs], dtype=np.uint64)
         txid = np.zeros((max(len(txs), 1), 32), dtype=np.uint8)
         st = np.zeros(max(len(txs), 1), dtype=np.uint8)
-        b = TxidBatch(len(txs), _ptr(lb), _ptr(lo), _ptr(to), _ptr(txid), _ptr(st))
+        b = TxidBatch(len(txs), _ptr(lb), _ptr(lo), _ptr(to), _ptr(txid), _ptr(st), len(leaves), lb.size)
         return b, (lb, lo, to, txid, st)
 
     def tx_ids(self, txs: Sequence[Sequence[bytes]], async_: bool = False):
@@ -150,7 +150,8 @@ class Engine:
         sb, sgo = self._csr([x[2] for x in flat])
         sst = np.zeros(max(len(flat), 1), dtype=np.uint8)
         fb = np.zeros(max(len(txs), 1), dtype=np.int64)
-        sbatch = SignedTxBatch(b, _ptr(so), _ptr(sch), _ptr(kb), _ptr(ko), _ptr(sb), _ptr(sgo), _ptr(sst), _ptr(fb))
+        sbatch = SignedTxBatch(b, _ptr(so), _ptr(sch), _ptr(kb), _ptr(ko), _ptr(sb), _ptr(sgo), _ptr(sst), _ptr(fb),
+                               len(flat), kb.size, sb.size)
         n = len(txs)
         res = lambda: (keep[3][:n], keep[4][:n], fb[:n], sst[:len(flat)])  # noqa: E731
         if async_:
@@ -193,7 +194,7 @@ class Engine:
             txid = np.zeros((max(n, 1), 32), dtype=np.uint8)
             st = np.zeros(max(n, 1), dtype=np.uint8)
         tb = TxcompBatch(n, _ptr(items) if len(items) else None, _ptr(tio), _ptr(payload) if payload.size else None,
-                         payload.size, _ptr(txid), _ptr(st))
+                         payload.size, _ptr(txid), _ptr(st), len(items))
         flat = [x for per in sigs for x in per]
         so = np.zeros(n + 1, dtype=np.uint64)
         if n:
@@ -204,7 +205,7 @@ class Engine:
         sst = np.zeros(max(len(flat), 1), dtype=np.uint8)
         fb = np.zeros(max(n, 1), dtype=np.int64)
         sbatch = SignedTxcompBatch(tb, _ptr(so), _ptr(sch), _ptr(kb), _ptr(ko), _ptr(sb), _ptr(sgo), _ptr(sst),
-                                   _ptr(fb))
+                                   _ptr(fb), len(flat), kb.size, sb.size)
         res = lambda: (txid[:n], st[:n], fb[:n], sst[:len(flat)])  # noqa: E731
         keep = (payload, items, tio, txid, st, so, sch, kb, ko, sb, sgo, sst, fb, tb, sbatch, pins)
         if async_:
@@ -302,7 +303,7 @@ class Engine:
         root = np.frombuffer(b"".join(f[2] for f in ftxs) or bytes(32), dtype=np.uint8).copy()
         st = np.zeros(max(len(ftxs), 1), dtype=np.uint8)
         b = FilteredTxBatch(len(ftxs), _ptr(lb), _ptr(lo), _ptr(to), _ptr(tok), _ptr(th), _ptr(ko), _ptr(root),
-                            _ptr(st))
+                            _ptr(st), len(leaves), lb.size, len(toks))
         if async_:
             t = ctypes.c_uint64()
             check(lib().cordahip_filtered_tx_submit(self._ctx, ctypes.byref(b), ctypes.byref(t)),

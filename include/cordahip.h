@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CORDAHIP_ABI_VERSION 3u
+#define CORDAHIP_ABI_VERSION 4u
 
 /* ---- per-lane statuses (status[i]) ------------------------------------- */
 #define CORDAHIP_STATUS_OK 0            /* isValid -> true;  doVerify -> true                         */
@@ -89,9 +89,17 @@ int cordahip_free_pinned(cordahip_ctx* ctx, void* host);
 
 /* ---- generic signature batch (host memory) ------------------------------ *
  * Variable-length fields are CSR: item i's key is key[key_off[i] .. key_off[i+1]).
- * Every CSR array in this header is the caller's contract, not checked: offsets
- * non-decreasing and the last one within its buffer (the JVM binding builds
- * them from its own arrays); lengths and contents are checked.
+ * Every CSR array in this header is CHECKED (ABI 4): offsets non-decreasing, the
+ * last one within the buffer length the batch declares (key_bytes, sig_bytes,
+ * msg_bytes, leaf_bytes_len, n_items, ntok), and each level's range inside the
+ * next level's declared count (a transaction's leaves < nleaves, items < n_items,
+ * signatures < nsig): the library reads no array past the entries its declared
+ * count implies ([n+1] offsets for n entries). A violation fails the batch
+ * with CORDAHIP_ERR_INVALID_ARG, never a read outside the caller's buffers:
+ * transaction-level batches are checked whole before anything is enqueued; a
+ * generic signature batch is checked lane by lane as its chunks are classified
+ * (earlier chunks may then have written their statuses; the result is the error).
+ * The context stays usable after INVALID_ARG.
  * Key encodings: Ed25519 = the 32-byte A (Kryo wire form, Kryo.kt:386); ECDSA =
  * SEC1 point (the SPKI BIT STRING payload, Crypto.kt:348-355).
  * verdict (optional): bit (i % 64) of word (i / 64) = (status[i] == OK).
@@ -114,6 +122,9 @@ typedef struct {
   uint8_t* status;         /* [n] out */
   uint64_t* verdict;       /* [(n+63)/64] out, may be NULL */
   uint32_t flags;          /* CORDAHIP_FLAG_* */
+  uint64_t key_bytes;      /* ABI 4: bytes at key; key_off[n] <= key_bytes */
+  uint64_t sig_bytes;      /* bytes at sig */
+  uint64_t msg_bytes;      /* bytes at msg */
 } cordahip_sig_batch;
 
 /* Tickets: every *_submit queues the batch on the context's worker pool and
@@ -220,6 +231,8 @@ typedef struct {
   const uint64_t* tx_leaf_off; /* [ntx+1] leaves of tx t: [tx_leaf_off[t], tx_leaf_off[t+1]) */
   uint8_t* txid;               /* [ntx*32] out: WireTransaction.id (SecureHash bytes) */
   uint8_t* tx_status;          /* [ntx] out: OK, NO_LEAVES (ids) / first failing lane status (signed tx) */
+  uint64_t nleaves;            /* ABI 4: leaves (leaf_off has nleaves+1 entries); tx_leaf_off[ntx] <= nleaves */
+  uint64_t leaf_bytes_len;     /* bytes at leaf_bytes */
 } cordahip_txid_batch;
 int cordahip_tx_ids(cordahip_ctx* ctx, const cordahip_txid_batch* batch);
 
@@ -238,6 +251,9 @@ typedef struct {
   const uint64_t* sig_off;
   uint8_t* sig_status;    /* [nsig] out */
   int64_t* first_bad_sig; /* [ntx] out */
+  uint64_t nsig;          /* ABI 4: signatures (key_off / sig_off have nsig+1 entries); tx_sig_off[ntx] <= nsig */
+  uint64_t key_bytes;     /* bytes at key */
+  uint64_t sig_bytes;     /* bytes at sig */
 } cordahip_signed_tx_batch;
 int cordahip_signed_tx_verify(cordahip_ctx* ctx, const cordahip_signed_tx_batch* batch);
 
@@ -277,6 +293,9 @@ typedef struct {
   const uint64_t* tx_tok_off;  /* [ntx+1] */
   const uint8_t* root;         /* [ntx*32] claimed Merkle roots (FilteredTransaction.rootHash) */
   uint8_t* tx_status;          /* [ntx] out */
+  uint64_t nleaves;            /* ABI 4: leaves (leaf_off has nleaves+1 entries) */
+  uint64_t leaf_bytes_len;     /* bytes at leaf_bytes */
+  uint64_t ntok;               /* tokens at tok (and 32-byte hashes at tok_hash) */
 } cordahip_filtered_tx_batch;
 int cordahip_filtered_tx_verify(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch);
 int cordahip_filtered_tx_submit(cordahip_ctx* ctx, const cordahip_filtered_tx_batch* batch, uint64_t* ticket);
@@ -432,6 +451,7 @@ typedef struct {
   uint64_t payload_len;
   uint8_t* txid;      /* [ntx*32] out */
   uint8_t* tx_status; /* [ntx] out */
+  uint64_t n_items;   /* ABI 4: records at items; tx_item_off[ntx] <= n_items */
 } cordahip_txcomp_batch;
 typedef struct {
   cordahip_txcomp_batch tx;
@@ -443,6 +463,9 @@ typedef struct {
   const uint64_t* sig_off;
   uint8_t* sig_status;    /* [nsig] out */
   int64_t* first_bad_sig; /* [ntx] out */
+  uint64_t nsig;          /* ABI 4: signatures (key_off / sig_off have nsig+1 entries) */
+  uint64_t key_bytes;     /* bytes at key */
+  uint64_t sig_bytes;     /* bytes at sig */
 } cordahip_signed_txcomp_batch;
 int cordahip_signed_txcomp_verify(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* batch);
 int cordahip_txcomp_submit(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* batch, uint64_t* ticket);

@@ -42,8 +42,8 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_abi_version_and_errors(lib):
     from corda_amd import _lib
-    assert lib.cordahip_abi_version() == _lib.ABI_VERSION == 3
-    assert "#define CORDAHIP_ABI_VERSION 3u" in open(HEADER).read()
+    assert lib.cordahip_abi_version() == _lib.ABI_VERSION == 4
+    assert "#define CORDAHIP_ABI_VERSION 4u" in open(HEADER).read()
     assert lib.cordahip_strerror(0) == b"success"
     assert lib.cordahip_strerror(-7) == b"not implemented on the GPU path"
     assert lib.cordahip_strerror(12345) == b"unknown error"
@@ -75,8 +75,10 @@ def test_sig_batch_layout_matches_header():
     import ctypes
     from corda_amd import _lib
     assert [f[0] for f in _lib.SigBatch._fields_] == ["n", "scheme", "key", "key_off", "sig", "sig_off", "msg",
-                                                      "msg_off", "status", "verdict", "flags"]
-    assert ctypes.sizeof(_lib.SigBatch) == 11 * 8  # 10 8-byte fields + u32 flags padded to 8
+                                                      "msg_off", "status", "verdict", "flags", "key_bytes",
+                                                      "sig_bytes", "msg_bytes"]
+    # 10 8-byte fields + u32 flags padded to 8 + the three ABI-4 buffer lengths
+    assert ctypes.sizeof(_lib.SigBatch) == 14 * 8
     src = open(HEADER).read()
     assert "#define CORDAHIP_FLAG_IS_VALID 1u" in src and _lib.FLAG_IS_VALID == 1
 
@@ -103,3 +105,33 @@ def test_shard_range_rule(lib):
                            for i in range(nd))
     assert _lib.shard_range(100, 4, 9, 64) == (100, 100)  # out-of-range shard: empty
     assert _lib.shard_range(100, 0, 0, 64) == (100, 100)
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """Every batch struct as ctypes lays it out == the C compiler's layout of
+    include/cordahip.h (sizeof and every field's offsetof), so a binding built
+    from the header and the Python mirror agree byte for byte."""
+    import shutil
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc absent")
+    from corda_amd import _lib
+    structs = {"cordahip_sig_batch": _lib.SigBatch, "cordahip_txid_batch": _lib.TxidBatch,
+               "cordahip_signed_tx_batch": _lib.SignedTxBatch, "cordahip_txcomp_batch": _lib.TxcompBatch,
+               "cordahip_signed_txcomp_batch": _lib.SignedTxcompBatch,
+               "cordahip_filtered_tx_batch": _lib.FilteredTxBatch, "cordahip_stream_batch": _lib.StreamBatch,
+               "cordahip_kryo_item": _lib.KryoItem}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "cordahip.h"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f in cls._fields_:
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, f[0], cname, f[0]))
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = str(tmp_path / "layout")
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-o", exe, str(src)])
+    got = dict(l.split() for l in subprocess.check_output([exe], text=True).splitlines())
+    for cname, cls in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f in cls._fields_:
+            assert int(got["%s.%s" % (cname, f[0])]) == getattr(cls, f[0]).offset, (cname, f[0])

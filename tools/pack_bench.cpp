@@ -67,7 +67,8 @@ void make(Batch& B, uint64_t n, bool ecdsa) {
   B.status.assign(n, 0);
   B.verdict.assign((n + 63) / 64, 0);
   B.b = cordahip_sig_batch{n, B.scheme.data(), B.key.data(), B.key_off.data(), B.sig.data(), B.sig_off.data(),
-                           B.msg.data(), B.msg_off.data(), B.status.data(), B.verdict.data(), 0u};
+                           B.msg.data(), B.msg_off.data(), B.status.data(), B.verdict.data(), 0u,
+                           (uint64_t)B.key.size(), (uint64_t)B.sig.size(), (uint64_t)B.msg.size()};
 }
 
 // lanes [lo, hi) through classify, pack, scatter, verdict words (the per-lane host work of a chunk)
