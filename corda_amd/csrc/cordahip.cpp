@@ -13,6 +13,7 @@
 // the caller as CORDAHIP_ERR_HIP. The generic CSR signature batch lives in
 // host_batch.cpp; the shared runtime types in runtime.hpp.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <sched.h>
 
 #include <algorithm>
@@ -34,9 +35,36 @@ namespace cordahip {
 namespace rt {
 
 // ---- host fork-join pool -----------------------------------------------------
-HostPool::HostPool(int nthreads) {
-  for (int i = 1; i < nthreads; i++) threads_.emplace_back([this] { worker(); });
+HostPool::HostPool(int nthreads, const std::vector<int>& cpus) {
+  for (int i = 1; i < nthreads; i++) {
+    threads_.emplace_back([this] { worker(); });
+    if (!cpus.empty()) {  // the device's node: its rows are packed next to its GPU
+      cpu_set_t cs;
+      CPU_ZERO(&cs);
+      for (int c : cpus)
+        if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &cs);
+      (void)pthread_setaffinity_np(threads_.back().native_handle(), sizeof(cs), &cs);
+    }
+  }
 }
+
+NodeBind::NodeBind(const Device& d) {
+  if (d.place.cpus.empty()) return;
+  cpu_set_t old, cs;
+  if (pthread_getaffinity_np(pthread_self(), sizeof(old), &old) != 0) return;
+  CPU_ZERO(&cs);
+  for (int c : d.place.cpus)
+    if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &cs);
+  if (CPU_EQUAL(&cs, &old) || pthread_setaffinity_np(pthread_self(), sizeof(cs), &cs) != 0) return;
+  saved_.assign(reinterpret_cast<unsigned char*>(&old), reinterpret_cast<unsigned char*>(&old) + sizeof(old));
+  bound_ = true;
+}
+
+NodeBind::~NodeBind() {
+  if (bound_) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpu_set_t), reinterpret_cast<cpu_set_t*>(saved_.data()));
+}
+
+HostPool& pool_of(cordahip_ctx* ctx, Device& d) { return d.pool ? *d.pool : *ctx->host; }
 
 HostPool::~HostPool() {
   {
@@ -412,6 +440,7 @@ int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uin
   (void)ctx;
   SetLease lease(d);
   TxSet& S = lease.get();
+  const NodeBind nb(d);
   if (int rc = tx_acquire_host(d, S)) return rc;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1];
@@ -497,7 +526,7 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, TxSet& S, int set_idx, c
     cp->pay_end.assign(ns, 0);
     cp->group.assign(ns, 1);
     std::vector<uint64_t> cap(ns, 0);
-    ctx->host->parallel_for(ns, 1, [&](uint64_t x, uint64_t y) {
+    pool_of(ctx, d).parallel_for(ns, 1, [&](uint64_t x, uint64_t y) {
       for (uint64_t j = x; j < y; j++) {
         const uint64_t ts0 = bound[j], ts1 = bound[j + 1];
         const uint64_t g = ts1 > ts0 ? c->tx_item_off[ts0 + 1] - c->tx_item_off[ts0] : 1;
@@ -679,9 +708,9 @@ hipError_t tx_ids_enqueue(Device& d, TxSet& S, int set_idx, const cordahip_txid_
 // signature statuses (SignedTransaction.verifySignaturesExcept -> the first
 // signature that fails, SignedTransaction.kt:95-100): first_bad_sig, and the
 // tx status becomes that signature's status.
-void reduce_txs(cordahip_ctx* ctx, const cordahip_signed_tx_batch* b, uint64_t t0, uint64_t t1) {
+void reduce_txs(HostPool& pool, const cordahip_signed_tx_batch* b, uint64_t t0, uint64_t t1) {
   if (t0 >= t1) return;
-  ctx->host->parallel_for(t1 - t0, 4096, [&](uint64_t x, uint64_t y) {
+  pool.parallel_for(t1 - t0, 4096, [&](uint64_t x, uint64_t y) {
     for (uint64_t t = t0 + x; t < t0 + y; t++) {
       const uint64_t lo = b->tx_sig_off[t], hi = b->tx_sig_off[t + 1];
       b->first_bad_sig[t] = -1;
@@ -739,6 +768,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
   SetLease lease(d);  // S.tx (the ids) and S.pb stay ours until every gather has run
   TxSet& S = lease.get();
   const int set_idx = lease.index();
+  const NodeBind nb(d);  // this thread packs and first-touches on the GPU's NUMA node
   std::unique_lock<std::mutex> tok(d.tx_order_mu);
   // component batches also enqueue on the GPU encoder's shared scratch (d.kryo_*)
   std::unique_lock<std::mutex> gk(d.kryo_mu, std::defer_lock);
@@ -853,7 +883,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
     const uint64_t ta = (uint64_t)(std::upper_bound(so + lo, so + hi + 1, filled) - so) - 1;
     const uint64_t tb = (uint64_t)(std::upper_bound(so + lo, so + hi + 1, s_end - 1) - so);
     const uint64_t f0 = filled;
-    ctx->host->parallel_for(tb - ta, 4096, [&](uint64_t x, uint64_t y) {
+    pool_of(ctx, d).parallel_for(tb - ta, 4096, [&](uint64_t x, uint64_t y) {
       for (uint64_t t = ta + x; t < ta + y; t++)
         for (uint64_t q = std::max(so[t], f0); q < std::min(so[t + 1], s_end); q++) tx_of[q] = t;
     });
@@ -891,7 +921,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
         if (hipError_t x = blocked("ids on the host", [&] { return hipEventSynchronize(ev[j]); })) return x;
       }
       const double tr = tracing() ? now_ms() : 0;
-      reduce_txs(ctx, b, t0, t1);
+      reduce_txs(pool_of(ctx, d), b, t0, t1);
       if (tracing() && now_ms() - tr > 1.0) fprintf(stderr, "[cordahip] reduce of %llu txs %.2f ms\n",
                                                     (unsigned long long)(t1 - t0), now_ms() - tr);
       reduced.push_back({t0, t1});
@@ -951,10 +981,10 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
   std::sort(reduced.begin(), reduced.end());
   uint64_t t = lo;
   for (const auto& rg : reduced) {
-    reduce_txs(ctx, b, t, rg.first);
+    reduce_txs(pool_of(ctx, d), b, t, rg.first);
     t = std::max(t, rg.second);
   }
-  reduce_txs(ctx, b, t, hi);
+  reduce_txs(pool_of(ctx, d), b, t, hi);
   if (tracing())
     fprintf(stderr, "[cordahip] dev %d signed tx tail: id streams drained %.2f ms, edge reduce %.2f ms\n", d.id,
             tr1 - tr0, now_ms() - tr1);
@@ -1083,6 +1113,7 @@ int signed_txcomp_impl(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* cb
 // latency-bound) run beside its Ed25519 ladder on their own stream.
 int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_t e1, uint64_t c0, uint64_t c1) {
   std::lock_guard<std::mutex> g(d.stream_mu);
+  const NodeBind nb(d);
   if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
   const uint64_t ne = e1 - e0, nc = c1 - c0;
   uint64_t chunk = kStreamChunk;  // CORDAHIP_STREAM_CHUNK: smaller chunks for tests of the pipeline itself
@@ -1214,6 +1245,7 @@ int stream_verify_impl(cordahip_ctx* ctx, const cordahip_stream_batch* b) {
 int filtered_tx_shard(Device& d, const cordahip_filtered_tx_batch* b, uint64_t t0, uint64_t t1) {
   SetLease lease(d);
   TxSet& S = lease.get();
+  const NodeBind nb(d);
   if (int rc = tx_acquire_host(d, S)) return rc;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
@@ -1430,16 +1462,44 @@ static int init_impl(uint32_t device_mask, cordahip_ctx** out) {
     return rc;
   }
   ctx->pool = std::make_unique<WorkerPool>((int)std::max<size_t>(2, 2 * ctx->devs.size()));
-  // host packing threads: CORDAHIP_HOST_THREADS, else the CPUs this process may
-  // use, at most 16 per device (the pipelines are PCIe/kernel bound beyond that)
-  int ht = 0;
-  if (const char* v = getenv("CORDAHIP_HOST_THREADS")) ht = atoi(v);
-  if (ht <= 0) {
+  // host threads. Per device (numa_place.hpp): a pool bound to CPUs of the GPU's
+  // NUMA node -- the devices of one node split its CPUs -- of CORDAHIP_HOST_THREADS
+  // threads at most (default 16: the pipelines are PCIe / kernel bound beyond that,
+  // tools/pack_bench.cpp); CORDAHIP_NUMA=0 leaves them unbound. Context-wide: a
+  // pool for the batch-level passes (CSR checks, verdict words) of at most 16.
+  int cap = 16;
+  if (const char* v = getenv("CORDAHIP_HOST_THREADS")) cap = std::max(1, std::min(256, atoi(v)));
+  std::vector<int> allowed;
+  {
     cpu_set_t cs;
-    const int ncpu = sched_getaffinity(0, sizeof(cs), &cs) == 0 ? CPU_COUNT(&cs) : (int)std::thread::hardware_concurrency();
-    ht = std::max(1, std::min(ncpu, 16 * (int)ctx->devs.size()));
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0)
+      for (int c = 0; c < CPU_SETSIZE; c++)
+        if (CPU_ISSET(c, &cs)) allowed.push_back(c);
   }
-  ctx->host = std::make_unique<HostPool>(std::min(ht, 256));
+  if (allowed.empty())
+    for (int c = 0; c < (int)std::max(1u, std::thread::hardware_concurrency()); c++) allowed.push_back(c);
+  std::vector<std::string> pci(ctx->devs.size());
+  const bool numa = !(getenv("CORDAHIP_NUMA") && getenv("CORDAHIP_NUMA")[0] == '0');
+  for (size_t i = 0; i < ctx->devs.size() && numa; i++) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, ctx->devs[i]->id) == hipSuccess) {
+      pci[i] = bus;
+      for (char& ch : pci[i]) ch = (char)tolower((unsigned char)ch);
+    }
+  }
+  const char* root = getenv("CORDAHIP_SYSFS_ROOT");  // tests: a fake tree
+  const std::vector<NumaPlace> plan = numa_plan(root ? root : "/sys", pci, allowed, cap);
+  for (size_t i = 0; i < ctx->devs.size(); i++) {
+    Device& d = *ctx->devs[i];
+    d.place = plan[i];
+    if (!numa) d.place.cpus.clear();
+    d.pool = std::make_unique<HostPool>(d.place.threads, d.place.cpus);
+    if (tracing())
+      fprintf(stderr, "[cordahip] dev %d (%s): NUMA node %d, %zu CPUs, %d host threads%s%s\n", d.id, pci[i].c_str(),
+              d.place.node, d.place.cpus.size(), d.place.threads, d.place.why.empty() ? "" : ": ",
+              d.place.why.c_str());
+  }
+  ctx->host = std::make_unique<HostPool>(std::max(1, std::min<int>((int)allowed.size(), 16)));
   *out = ctx.release();
   return CORDAHIP_SUCCESS;
 }

@@ -121,9 +121,10 @@ int ed_pipeline(cordahip_ctx* ctx, Device& d, const std::vector<Unit>& units, co
   const std::vector<Chunk> chunks = make_chunks(units, chunk_lanes("CORDAHIP_HOST_CHUNK", kEdChunk));
   if (chunks.empty()) return CORDAHIP_SUCCESS;
   std::lock_guard<std::mutex> g(d.ped_mu);
+  const NodeBind nb(d);  // packing and the pinned stages' first touch on the GPU's NUMA node
   if (hipSetDevice(d.id) != hipSuccess || ensure_streams(d) != hipSuccess || ensure_events(d.ped) != hipSuccess)
     return CORDAHIP_ERR_HIP;
-  HostPool& pool = *ctx->host;
+  HostPool& pool = pool_of(ctx, d);
   auto finish = [&](PackStage& st) -> hipError_t {  // wait for a stage's chunk, scatter its statuses
     if (!st.pending) return hipSuccess;
     st.pending = false;
@@ -215,11 +216,12 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_ba
     chunks = make_chunks(units, mv.chunk ? mv.chunk : chunk_lanes("CORDAHIP_HOST_CHUNK", kEdChunk));
   }
   const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
+  const NodeBind nb(d);  // packing and the pinned stages' first touch on the GPU's NUMA node
   if (hipSetDevice(d.id) != hipSuccess || ensure_streams(d) != hipSuccess) return CORDAHIP_ERR_HIP;
   for (BatchStage& st : set.pb)
     for (hipEvent_t* pe : {&st.copied, &st.ed_done, &st.ec_done})
       if (!*pe && hipEventCreateWithFlags(pe, hipEventDisableTiming) != hipSuccess) return CORDAHIP_ERR_HIP;
-  HostPool& pool = *ctx->host;
+  HostPool& pool = pool_of(ctx, d);
   // Chunks whose rows are the lanes in order (one message length, Ed25519 only:
   // the common JVM batch) skip the host scatter: a kernel stores the statuses
   // straight into the caller's status array and the wave-ballot verdict words

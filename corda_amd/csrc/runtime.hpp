@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/cordahip.h"
+#include "numa_place.hpp"
 
 namespace cordahip {
 hipError_t launch_ed25519_btable(uint32_t* tab, hipStream_t s);
@@ -228,9 +229,17 @@ struct TimedCall {
   uint64_t gen = 0;
 };
 
+class HostPool;
+
 struct Device {
   int id = 0;
   uint64_t uid = 0;  // process-unique: keys the per-thread timing slot
+  // host threads next to this GPU (numa_place.hpp): the packing / scattering /
+  // reduce pool of its pipelines, bound to CPUs of its NUMA node; the thread that
+  // runs a pipeline binds itself there for the call (NodeBind), so the pinned
+  // stages it allocates are first-touched on that node too
+  NumaPlace place;
+  std::unique_ptr<HostPool> pool;
   uint32_t* btab = nullptr;
   uint32_t* gtab_k1 = nullptr;  // [k]G tables, k = 0..128, secp256k1 / P-256
   uint32_t* gtab_r1 = nullptr;
@@ -303,7 +312,8 @@ struct Device {
 // so concurrent callers (one pipeline per device and section) all progress.
 class HostPool {
  public:
-  explicit HostPool(int nthreads);
+  // cpus non-empty: every worker thread is bound to them (a device's NUMA node)
+  explicit HostPool(int nthreads, const std::vector<int>& cpus = {});
   ~HostPool();
   int threads() const { return (int)threads_.size() + 1; }
   void parallel_for(uint64_t n, uint64_t grain, const std::function<void(uint64_t, uint64_t)>& fn);
@@ -324,6 +334,23 @@ class HostPool {
   std::vector<std::thread> threads_;
   bool stop_ = false;
 };
+
+// The calling thread bound to a device's CPUs for a scope (its previous affinity
+// restored after): pipelines pack rows and first-touch pinned stages on the GPU's
+// NUMA node. No-op when the device has no placement.
+class NodeBind {
+ public:
+  explicit NodeBind(const Device& d);
+  ~NodeBind();
+  NodeBind(const NodeBind&) = delete;
+  NodeBind& operator=(const NodeBind&) = delete;
+
+ private:
+  bool bound_ = false;
+  std::vector<unsigned char> saved_;  // cpu_set_t bytes
+};
+// the pool a device's host work runs on
+HostPool& pool_of(cordahip_ctx* ctx, Device& d);
 
 // ---- ticket pool -------------------------------------------------------------
 struct JobState {

@@ -25,3 +25,18 @@ def test_pack_bench_runs_and_scales(tmp_path):
     # packing is memcpy-bound: a thread packs millions of lanes per second, far more
     # than one GPU verifies per thread of the GPU's host
     assert by[("ed25519", 1)]["lanes_per_s"] > 5e6 and by[("ecdsa", 1)]["lanes_per_s"] > 3e6
+
+
+def test_pack_bench_pools_mode(tmp_path):
+    """one bound pool per simulated device (the library's per-device NUMA pools):
+    every pool packs its own shard at once; the aggregate is reported"""
+    exe = str(tmp_path / "pack_bench")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-o", exe,
+                           os.path.join(ROOT, "tools", "pack_bench.cpp")])
+    pools = 2
+    out = subprocess.run([exe, str(1 << 18), str(2 * pools), str(pools)], capture_output=True, text=True, check=True,
+                         timeout=120)
+    rows = [json.loads(x) for x in out.stdout.splitlines()]
+    assert {r["scheme"] for r in rows} == {"ed25519", "ecdsa"}
+    for r in rows:
+        assert r["pools"] == pools and r["threads_per_pool"] == 2 and r["lanes_per_s"] > 1e6

@@ -16,9 +16,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <pthread.h>
+#include <sched.h>
+
 #include <thread>
 #include <vector>
 
+#include "../corda_amd/csrc/numa_place.hpp"
 #include "../corda_amd/csrc/pack_rows.hpp"
 
 using namespace cordahip::rt;
@@ -107,9 +111,97 @@ void work(const Batch& B, bool ecdsa, uint64_t lo, uint64_t hi, std::vector<uint
 
 }  // namespace
 
+// POOLS > 0: one pool per simulated device, as the library runs them (numa_place.hpp):
+// the allowed CPUs grouped by NUMA node, the pools spread over the nodes and each
+// bound to a disjoint slice of its node's CPUs; every pool first-touches its own
+// batch (a device's shard) from a bound thread, then all pools pack at once. Prints
+// the aggregate and the slowest pool's lanes/s per scheme.
+int pools_mode(uint64_t n, int threads, int pools) {
+  std::vector<int> allowed;
+  {
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0)
+      for (int c = 0; c < CPU_SETSIZE; c++)
+        if (CPU_ISSET(c, &cs)) allowed.push_back(c);
+  }
+  std::vector<std::vector<int>> by_node;  // allowed CPUs of each node that has any
+  for (int node = 0; node < 64; node++) {
+    std::string t;
+    if (!cordahip::rt::read_text("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist", t)) continue;
+    std::vector<int> c = cordahip::rt::parse_cpulist(t), mine;
+    std::set_intersection(c.begin(), c.end(), allowed.begin(), allowed.end(), std::back_inserter(mine));
+    if (!mine.empty()) by_node.push_back(mine);
+  }
+  if (by_node.empty()) by_node.push_back(allowed);
+  std::vector<std::vector<int>> slice(pools);
+  for (int k = 0; k < pools; k++) {  // pool k on node k * nodes / pools, the node's pools split its CPUs
+    const int nn = (int)by_node.size(), node = k * nn / pools;
+    int first = 0, count = 0;
+    for (int j = 0; j < pools; j++)
+      if (j * nn / pools == node) {
+        if (j < k) first++;
+        count++;
+      }
+    const auto& c = by_node[node];
+    size_t lo = c.size() * first / count, hi = c.size() * (first + 1) / count;
+    if (hi <= lo) {  // more pools than CPUs on the node: one CPU each, shared
+      hi = std::min(c.size(), lo + 1);
+      lo = hi - 1;
+    }
+    slice[k].assign(c.begin() + (long)lo, c.begin() + (long)hi);
+  }
+  const int per = std::max(1, threads / pools);
+  auto bind = [](const std::vector<int>& cpus) {
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    for (int c : cpus) CPU_SET(c, &cs);
+    (void)pthread_setaffinity_np(pthread_self(), sizeof(cs), &cs);
+  };
+  for (int ec = 0; ec < 2; ec++) {
+    std::vector<Batch> B(pools);
+    {
+      std::vector<std::thread> th;
+      for (int k = 0; k < pools; k++) th.emplace_back([&, k] { bind(slice[k]); make(B[k], n, ec); });
+      for (auto& x : th) x.join();
+    }
+    double best_all = 1e30, worst_pool = 0;
+    for (int rep = 0; rep < 3; rep++) {
+      std::vector<double> took(pools);
+      const auto t0 = std::chrono::steady_clock::now();
+      std::vector<std::thread> th;
+      for (int k = 0; k < pools; k++)
+        for (int q = 0; q < per; q++)
+          th.emplace_back([&, k, q] {
+            bind(slice[k]);
+            std::vector<uint8_t> rows;
+            std::vector<uint64_t> mo;
+            std::vector<uint16_t> cls;
+            const uint64_t step = (n / per + 63) / 64 * 64, lo = std::min<uint64_t>(n, q * step),
+                           hi = std::min<uint64_t>(n, lo + step);
+            work(B[k], ec, lo, hi, rows, mo, cls);
+          });
+      for (auto& x : th) x.join();
+      const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (dt < best_all) best_all = dt;
+      worst_pool = dt;
+    }
+    std::string cpus;
+    for (int k = 0; k < pools; k++) cpus += std::string(k ? "; " : "") + std::to_string(slice[k].size());
+    printf("{\"scheme\": \"%s\", \"pools\": %d, \"threads_per_pool\": %d, \"lanes_per_pool\": %llu, "
+           "\"numa_nodes\": %zu, \"cpus_per_pool\": \"%s\", \"s\": %.4f, \"lanes_per_s\": %.4g, "
+           "\"lanes_per_s_per_pool\": %.4g}\n",
+           ec ? "ecdsa" : "ed25519", pools, per, (unsigned long long)n, by_node.size(), cpus.c_str(), best_all,
+           pools * n / best_all, n / best_all);
+    (void)worst_pool;
+    fflush(stdout);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : (1ull << 22);
   const int maxt = argc > 2 ? atoi(argv[2]) : (int)std::thread::hardware_concurrency();
+  if (argc > 3 && atoi(argv[3]) > 0) return pools_mode(n, maxt, atoi(argv[3]));
   for (int ec = 0; ec < 2; ec++) {
     Batch B;
     make(B, n, ec);
