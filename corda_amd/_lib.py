@@ -35,7 +35,7 @@ EXPORTS = [
     "cordahip_ecdsa_verify_device", "cordahip_stream_verify", "cordahip_filtered_tx_verify",
     "cordahip_tx_submit", "cordahip_txid_submit", "cordahip_filtered_tx_submit", "cordahip_shard_range",
     "cordahip_kryo_encode", "cordahip_kryo_encode_device", "cordahip_signed_txcomp_verify", "cordahip_txcomp_submit",
-    "cordahip_signed_txcomp_verify_ed25519_device",
+    "cordahip_signed_txcomp_verify_ed25519_device", "cordahip_device_mem", "cordahip_trim",
 ]
 ERR_BUFFER_TOO_SMALL = -8
 # cordahip_kryo_item kinds (CORDAHIP_KRYO_*)
@@ -199,6 +199,8 @@ def lib() -> ctypes.CDLL:
         "cordahip_txcomp_submit": (i32, [vp, ctypes.POINTER(SignedTxcompBatch), ctypes.POINTER(u64)]),
         "cordahip_signed_txcomp_verify_ed25519_device": (i32, [vp, i32, vp, u64, u32, vp, u64, vp, u64, vp, vp, vp, u64,
                                                                vp, vp, vp, vp, vp]),
+        "cordahip_device_mem": (i32, [vp, i32, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "cordahip_trim": (i32, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(l, name)

@@ -66,6 +66,11 @@ NodeBind::~NodeBind() {
 
 HostPool& pool_of(cordahip_ctx* ctx, Device& d) { return d.pool ? *d.pool : *ctx->host; }
 
+MemAcct& mem_acct(int dev) {
+  static MemAcct acct[kMaxHipDevices];
+  return acct[dev >= 0 && dev < kMaxHipDevices ? dev : 0];
+}
+
 HostPool::~HostPool() {
   {
     std::lock_guard<std::mutex> g(m_);
@@ -306,7 +311,7 @@ hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* ke
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
                              unsigned long long* verdict, uint32_t flags, hipStream_t s) {
   EcWork& w = d.ec;
-  static const uint64_t ws_slots = env_lanes("CORDAHIP_ECDSA_WS_SLOTS", kEcWsSlots);
+  const uint64_t ws_slots = d.ec_ws_slots;  // the budget's ECDSA share (cordahip_init)
   const uint64_t slots = std::min<uint64_t>(ws_slots, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
   if (w.ws.cap < slots * ecdsa_ws_slot_bytes() || w.perm.cap < std::max<uint64_t>(n, 1) * 4) {
     hipError_t e = w.ev ? hipEventSynchronize(w.ev) : hipSuccess;  // a smaller buffer may still be in use
@@ -334,13 +339,11 @@ hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs
   std::lock_guard<std::mutex> g(d.ed_mu[slot]);
   DevBuf& ws = d.ed_ws[slot];
   hipEvent_t& ev = d.ed_ev[slot];
-  static const uint64_t ws_lanes = env_lanes("CORDAHIP_ED25519_WS_LANES", kEdWsLanes);
-  // Slot 1 only serves the alternating chunks of the pipelines (host batches,
-  // streams, signed-tx chunks): it is capped at half of slot 0, so the two
-  // together stay within 1.5 x CORDAHIP_ED25519_WS_LANES x 3,200 B (81 GB at
-  // the default). The launch loops over whatever the
-  // workspace holds, so a smaller one only costs extra launch pairs.
-  const uint64_t cap_lanes = slot ? std::max<uint64_t>(64, ws_lanes / 2 / 64 * 64) : ws_lanes;
+  // the budget's Ed25519 shares (cordahip_init, device_budget): slot 1 only serves the
+  // alternating chunks of the pipelines (host batches, streams, signed-tx chunks) and
+  // holds at most half of slot 0. The launch loops over whatever the workspace holds,
+  // so a smaller one only costs extra launch pairs.
+  const uint64_t cap_lanes = d.ed_ws_lanes[slot ? 1 : 0];
   const uint64_t lanes = std::min<uint64_t>(cap_lanes, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
   const uint64_t lane_bytes = ed25519_ws_lane_bytes();
   if (ws.cap < lanes * lane_bytes) {
@@ -366,6 +369,79 @@ hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs
                                 ws.cap / ed25519_ws_lane_bytes() / 64 * 64, flags, s, before_msgs);
   e = e ? e : hipEventRecord(ev, s);
   return e;
+}
+
+// CORDAHIP_DEVICE_MEM_BUDGET (bytes, K/M/G suffixes; default 128 GiB, at most 90%
+// of the device): the workspaces it sizes -- Ed25519 slot 0 45% of it, slot 1 20%
+// (and half of slot 0 at most), ECDSA 15% -- each also capped by its r05 maximum
+// (2^24 lanes / slots, CORDAHIP_ED25519_WS_LANES / CORDAHIP_ECDSA_WS_SLOTS). The
+// default therefore keeps C2's single 2^24-lane launch pair (53.7 GB) and the
+// r05 peak: 53.7 + 26.8 + 18.8 GB of workspaces. The other buffers follow the
+// batches (the id and signature stages, component slices, C5's stages) and are
+// not split. A smaller budget costs extra launch pairs, never a failed batch.
+uint64_t parse_bytes(const char* v, uint64_t dflt) {
+  if (!v || !*v) return dflt;
+  char* end = nullptr;
+  const double x = strtod(v, &end);
+  if (end == v || x <= 0) return dflt;
+  const char u = end ? (char)toupper((unsigned char)*end) : 0;
+  const double m = u == 'K' ? 1024.0 : u == 'M' ? 1048576.0 : u == 'G' ? 1073741824.0 : 1.0;
+  return (uint64_t)(x * m);
+}
+
+void device_budget(Device& d) {  // device current
+  uint64_t b = parse_bytes(getenv("CORDAHIP_DEVICE_MEM_BUDGET"), 128ull << 30);
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot) b = std::min<uint64_t>(b, (uint64_t)tot / 10 * 9);
+  d.mem_budget = b;
+  auto lanes = [](uint64_t bytes, uint64_t per) { return std::max<uint64_t>(64, bytes / per / 64 * 64); };
+  const uint64_t lb = ed25519_ws_lane_bytes(), sb = ecdsa_ws_slot_bytes();
+  d.ed_ws_lanes[0] = std::min(env_lanes("CORDAHIP_ED25519_WS_LANES", kEdWsLanes), lanes(b / 100 * 45, lb));
+  d.ed_ws_lanes[1] = std::min(std::max<uint64_t>(64, d.ed_ws_lanes[0] / 2 / 64 * 64), lanes(b / 5, lb));
+  d.ec_ws_slots = std::min(env_lanes("CORDAHIP_ECDSA_WS_SLOTS", kEcWsSlots), lanes(b / 100 * 15, sb));
+}
+
+// Free an idle device's grow-only buffers (the idle release, cordahip_trim): both
+// buffer sets and every lock that guards a buffer, in an order every path keeps
+// (sets, then kryo_mu, stream_mu, ped_mu, ed_mu, ec_mu); the events that fence
+// device-path users (kernels on caller streams) synchronised first. The fixed
+// tables and the encoder's shape table stay (derived data, 18 MB).
+void trim_device(Device& d) {
+  SetLease l0(d, 0, true), l1(d, 1, true);
+  std::lock_guard<std::mutex> gk(d.kryo_mu), gs(d.stream_mu), gp(d.ped_mu), ge0(d.ed_mu[0]), ge1(d.ed_mu[1]),
+      gc(d.ec_mu);
+  if (hipSetDevice(d.id) != hipSuccess) return;
+  for (hipEvent_t ev : {d.ed_ev[0], d.ed_ev[1], d.ec.ev, d.kryo_ev, d.set[0].tx_ev, d.set[1].tx_ev})
+    if (ev) (void)hipEventSynchronize(ev);
+  for (auto& w : d.ed_ws) w.release();
+  d.ec.ws.release();
+  d.ec.perm.release();
+  for (TxSet& S : d.set) {
+    TxWork& w = S.tx;
+    for (DevBuf* b : {&w.leaf_bytes, &w.leaf_off, &w.tx_leaf_off, &w.hashes, &w.txid, &w.tx_status, &w.tx_sig_off,
+                      &w.msgs, &w.comp_items, &w.payload, &w.comp_status, &w.tok, &w.tok_hash, &w.tx_tok_off, &w.root,
+                      &w.stack})
+      b->release();
+    for (BatchStage& st : S.pb) {
+      for (hipEvent_t ev : {st.copied, st.ed_done, st.ec_done})
+        if (ev) (void)hipEventSynchronize(ev);
+      for (auto& b : st.h) b.release();
+      for (auto& b : st.d) b.release();
+      for (auto& b : st.hidx) b.release();
+      for (auto& b : st.didx) b.release();
+      st.dverdict.release();
+    }
+  }
+  for (auto& st : d.sstage)
+    for (DevBuf* b : {&st.ed_keys, &st.ed_sigs, &st.ed_msgs, &st.ed_status, &st.ec_scheme, &st.ec_keys,
+                      &st.ec_key_len, &st.ec_sigs, &st.ec_sig_len, &st.ec_msgs, &st.ec_status})
+      b->release();
+  for (PackStage& st : d.ped) {
+    for (auto& b : st.h) b.release();
+    for (auto& b : st.d) b.release();
+  }
+  for (DevBuf* b : {&d.kryo_sizes, &d.kryo_temp, &d.kryo_ws, &d.kryo_items}) b->release();
+  if (tracing()) fprintf(stderr, "[cordahip] dev %d: idle buffers released\n", d.id);
 }
 
 // the in-process partition rule (cordahip_shard_range)
@@ -441,6 +517,7 @@ int tx_ids_shard(cordahip_ctx* ctx, Device& d, const cordahip_txid_batch* b, uin
   SetLease lease(d);
   TxSet& S = lease.get();
   const NodeBind nb(d);
+  const Activity act(d);
   if (int rc = tx_acquire_host(d, S)) return rc;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1];
@@ -769,6 +846,7 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
   TxSet& S = lease.get();
   const int set_idx = lease.index();
   const NodeBind nb(d);  // this thread packs and first-touches on the GPU's NUMA node
+  const Activity act(d);
   std::unique_lock<std::mutex> tok(d.tx_order_mu);
   // component batches also enqueue on the GPU encoder's shared scratch (d.kryo_*)
   std::unique_lock<std::mutex> gk(d.kryo_mu, std::defer_lock);
@@ -1114,6 +1192,7 @@ int signed_txcomp_impl(cordahip_ctx* ctx, const cordahip_signed_txcomp_batch* cb
 int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_t e1, uint64_t c0, uint64_t c1) {
   std::lock_guard<std::mutex> g(d.stream_mu);
   const NodeBind nb(d);
+  const Activity act(d);
   if (hipSetDevice(d.id) != hipSuccess) return CORDAHIP_ERR_HIP;
   const uint64_t ne = e1 - e0, nc = c1 - c0;
   uint64_t chunk = kStreamChunk;  // CORDAHIP_STREAM_CHUNK: smaller chunks for tests of the pipeline itself
@@ -1246,6 +1325,7 @@ int filtered_tx_shard(Device& d, const cordahip_filtered_tx_batch* b, uint64_t t
   SetLease lease(d);
   TxSet& S = lease.get();
   const NodeBind nb(d);
+  const Activity act(d);
   if (int rc = tx_acquire_host(d, S)) return rc;
   const uint64_t ntx = t1 - t0;
   const uint64_t l0 = b->tx_leaf_off[t0], l1 = b->tx_leaf_off[t1], nleaves = l1 - l0;
@@ -1353,6 +1433,7 @@ void free_device(Device& d) {
   for (auto& tc : d.ring)
     for (hipEvent_t ev : {tc.a, tc.b})
       if (ev) (void)hipEventDestroy(ev);
+  if (d.btab && d.gtab_k1 && d.gtab_r1) mem_acct(d.id).sub(ed25519_btable_bytes() + 2 * ecdsa_gtable_bytes());
   if (d.gtab_k1) (void)hipFree(d.gtab_k1);
   if (d.gtab_r1) (void)hipFree(d.gtab_r1);
   if (d.btab) (void)hipFree(d.btab);
@@ -1446,6 +1527,8 @@ static int init_impl(uint32_t device_mask, cordahip_ctx** out) {
       rc = CORDAHIP_ERR_OUT_OF_MEMORY;
       break;
     }
+    mem_acct(d).add(ed25519_btable_bytes() + 2 * ecdsa_gtable_bytes());
+    device_budget(dev);
     static const bool id_prio = !(getenv("CORDAHIP_ID_PRIO") && getenv("CORDAHIP_ID_PRIO")[0] == '0');
     if (!id_prio && (tx_set_id_priority(0) != hipSuccess || kryo_set_priority(0) != hipSuccess)) {
       rc = CORDAHIP_ERR_HIP;
@@ -1500,12 +1583,45 @@ static int init_impl(uint32_t device_mask, cordahip_ctx** out) {
               d.place.why.c_str());
   }
   ctx->host = std::make_unique<HostPool>(std::max(1, std::min<int>((int)allowed.size(), 16)));
+  // the idle release: a device with no call for CORDAHIP_IDLE_RELEASE_MS (default 30 s;
+  // 0: never) gives its grow-only buffers back (trim_device)
+  const char* iv = getenv("CORDAHIP_IDLE_RELEASE_MS");
+  const int64_t idle_ms = iv ? strtoll(iv, nullptr, 10) : 30000;
+  if (idle_ms > 0) {
+    cordahip_ctx* c = ctx.get();
+    c->reaper = std::thread([c, idle_ms] {
+      std::vector<int64_t> trimmed_at(c->devs.size(), 0);  // the last call's end when last trimmed
+      std::unique_lock<std::mutex> g(c->reaper_mu);
+      while (!c->reaper_stop) {
+        c->reaper_cv.wait_for(g, std::chrono::milliseconds(std::min<int64_t>(250, idle_ms)));
+        if (c->reaper_stop) break;
+        for (size_t i = 0; i < c->devs.size(); i++) {
+          Device& d = *c->devs[i];
+          const int64_t last = d.last_use_ms.load();
+          if (d.active.load() > 0 || last == 0 || last == trimmed_at[i] || (int64_t)now_ms() - last < idle_ms)
+            continue;
+          g.unlock();
+          trim_device(d);
+          g.lock();
+          trimmed_at[i] = last;
+        }
+      }
+    });
+  }
   *out = ctx.release();
   return CORDAHIP_SUCCESS;
 }
 
 void cordahip_shutdown(cordahip_ctx* ctx) {
   if (!ctx) return;
+  if (ctx->reaper.joinable()) {
+    {
+      std::lock_guard<std::mutex> g(ctx->reaper_mu);
+      ctx->reaper_stop = true;
+    }
+    ctx->reaper_cv.notify_all();
+    ctx->reaper.join();
+  }
   ctx->pool.reset();  // runs every queued job to completion, joins the workers
   ctx->host.reset();
   {
@@ -1517,6 +1633,24 @@ void cordahip_shutdown(cordahip_ctx* ctx) {
 }
 
 int cordahip_device_count(const cordahip_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int cordahip_device_mem(cordahip_ctx* ctx, int device, uint64_t* in_use, uint64_t* peak, uint64_t* budget) {
+  Device* d = dev_at(ctx, device);
+  if (!d) return CORDAHIP_ERR_INVALID_ARG;
+  const MemAcct& m = mem_acct(d->id);
+  if (in_use) *in_use = m.in_use.load();
+  if (peak) *peak = m.peak.load();
+  if (budget) *budget = d->mem_budget;
+  return CORDAHIP_SUCCESS;
+}
+
+int cordahip_trim(cordahip_ctx* ctx) {
+  if (!ctx) return CORDAHIP_ERR_INVALID_ARG;
+  return guarded([&] {
+    for (auto& d : ctx->devs) trim_device(*d);
+    return (int)CORDAHIP_SUCCESS;
+  });
+}
 
 int cordahip_alloc_pinned(cordahip_ctx* ctx, size_t bytes, void** host) {
   if (!ctx || !host) return CORDAHIP_ERR_INVALID_ARG;
@@ -1627,6 +1761,7 @@ int cordahip_ed25519_verify_device(cordahip_ctx* ctx, int device, const void* d_
   if ((reinterpret_cast<uintptr_t>(d_keys) | reinterpret_cast<uintptr_t>(d_sigs)) & 15)
     return CORDAHIP_ERR_INVALID_ARG;
   if (msg_len == 32 && (reinterpret_cast<uintptr_t>(d_msgs) & 15)) return CORDAHIP_ERR_INVALID_ARG;
+  const Activity act(*d);
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);  // NULL = the device's null stream
   TimedCall* tc = timed_begin(*d, s);
@@ -1644,6 +1779,7 @@ int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_sc
   Device* d = dev_at(ctx, device);
   if (!d || (n && (!d_scheme || !d_keys || !d_key_len || !d_sigs || !d_sig_len || !d_status || (msg_len && !d_msgs))))
     return CORDAHIP_ERR_INVALID_ARG;
+  const Activity act(*d);
   std::lock_guard<std::mutex> g(d->ec_mu);
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
@@ -1742,6 +1878,7 @@ int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, cons
     return CORDAHIP_ERR_INVALID_ARG;
   // a buffer set for the enqueue; its event then fences the set's hashes / msgs
   // until these kernels finish (the next holder waits on it)
+  const Activity act(*d);
   SetLease lease(*d);
   TxSet& S = lease.get();
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
@@ -1792,6 +1929,7 @@ int cordahip_kryo_encode_device(cordahip_ctx* ctx, int device, const void* d_ite
   if (!d || !d_off || (n && (!d_items || !d_status))) return CORDAHIP_ERR_INVALID_ARG;
   if (n >= (1ull << 31) - 1) return CORDAHIP_ERR_INVALID_ARG;  // the scan counts items in an int
   return guarded([&]() -> int {
+    const Activity act(*d);
     std::lock_guard<std::mutex> g(d->kryo_mu);
     if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
     if (!d->kryo_ev && hipEventCreateWithFlags(&d->kryo_ev, hipEventDisableTiming) != hipSuccess)
@@ -1844,6 +1982,7 @@ int cordahip_signed_txcomp_verify_ed25519_device(cordahip_ctx* ctx, int device, 
   return guarded([&]() -> int {
     // a buffer set for the enqueue (its hashes, messages and component statuses, fenced
     // by its event until these kernels finish) and the encoder's scratch (kryo_mu, kryo_ev)
+    const Activity act(*d);
     SetLease lease(*d);
     TxSet& S = lease.get();
     std::lock_guard<std::mutex> gk(d->kryo_mu);

@@ -122,6 +122,7 @@ int ed_pipeline(cordahip_ctx* ctx, Device& d, const std::vector<Unit>& units, co
   if (chunks.empty()) return CORDAHIP_SUCCESS;
   std::lock_guard<std::mutex> g(d.ped_mu);
   const NodeBind nb(d);  // packing and the pinned stages' first touch on the GPU's NUMA node
+  const Activity act(d);
   if (hipSetDevice(d.id) != hipSuccess || ensure_streams(d) != hipSuccess || ensure_events(d.ped) != hipSuccess)
     return CORDAHIP_ERR_HIP;
   HostPool& pool = pool_of(ctx, d);
@@ -217,6 +218,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_ba
   }
   const bool do_verify = !(b->flags & CORDAHIP_FLAG_IS_VALID);
   const NodeBind nb(d);  // packing and the pinned stages' first touch on the GPU's NUMA node
+  const Activity act(d);
   if (hipSetDevice(d.id) != hipSuccess || ensure_streams(d) != hipSuccess) return CORDAHIP_ERR_HIP;
   for (BatchStage& st : set.pb)
     for (hipEvent_t* pe : {&st.copied, &st.ed_done, &st.ec_done})

@@ -103,21 +103,47 @@ hipError_t launch_ecdsa_sign(const uint8_t* scheme, const uint8_t* seeds, const 
 
 namespace rt {
 
-// grow-only device buffer
+// The library's device memory per HIP device (every DevBuf, the fixed tables):
+// bytes in use and their peak, for cordahip_device_mem and the budget
+// (CORDAHIP_DEVICE_MEM_BUDGET) that sizes the workspaces.
+constexpr int kMaxHipDevices = 64;
+struct MemAcct {
+  std::atomic<uint64_t> in_use{0}, peak{0};
+  void add(uint64_t b) {
+    const uint64_t now = in_use.fetch_add(b) + b;
+    uint64_t p = peak.load();
+    while (now > p && !peak.compare_exchange_weak(p, now)) {
+    }
+  }
+  void sub(uint64_t b) { in_use.fetch_sub(b); }
+};
+MemAcct& mem_acct(int dev);
+
+// grow-only device buffer (accounted on the device it was allocated on)
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  int dev = -1;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
+    release();
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) d = 0;
     hipError_t e = hipMalloc(&p, bytes);
-    if (e == hipSuccess) cap = bytes;
+    if (e == hipSuccess) {
+      cap = bytes;
+      dev = d;
+      mem_acct(dev).add(bytes);
+    } else {
+      p = nullptr;
+    }
     return e;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      (void)hipFree(p);
+      mem_acct(dev).sub(cap);
+    }
     p = nullptr;
     cap = 0;
   }
@@ -240,6 +266,14 @@ struct Device {
   // stages it allocates are first-touched on that node too
   NumaPlace place;
   std::unique_ptr<HostPool> pool;
+  // device memory (CORDAHIP_DEVICE_MEM_BUDGET, cordahip_init): the workspace sizes
+  // the budget allows -- Ed25519 slots 0 / 1 (lanes), ECDSA (slots) -- and the
+  // activity the idle release reads (calls in progress, the last one's end)
+  uint64_t mem_budget = 0;
+  uint64_t ed_ws_lanes[2] = {0, 0};
+  uint64_t ec_ws_slots = 0;
+  std::atomic<int> active{0};
+  std::atomic<int64_t> last_use_ms{0};
   uint32_t* btab = nullptr;
   uint32_t* gtab_k1 = nullptr;  // [k]G tables, k = 0..128, secp256k1 / P-256
   uint32_t* gtab_r1 = nullptr;
@@ -352,6 +386,7 @@ class NodeBind {
 // the pool a device's host work runs on
 HostPool& pool_of(cordahip_ctx* ctx, Device& d);
 
+
 // ---- ticket pool -------------------------------------------------------------
 struct JobState {
   std::mutex m;
@@ -385,6 +420,22 @@ inline bool tracing() {
   static const bool on = getenv("CORDAHIP_TRACE") != nullptr;
   return on;
 }
+
+// a call in progress on a device (the idle release waits for none)
+class Activity {
+ public:
+  explicit Activity(Device& d) : d_(d) { d_.active.fetch_add(1); }
+  ~Activity() {
+    d_.last_use_ms.store((int64_t)now_ms());
+    d_.active.fetch_sub(1);
+  }
+  Activity(const Activity&) = delete;
+  Activity& operator=(const Activity&) = delete;
+
+ private:
+  Device& d_;
+};
+
 // The device address of pinned host memory p (nullptr when p is pageable or
 // unknown to HIP): kernels store results there directly, since a D2H
 // hipMemcpyAsync queued behind busy compute streams can hold the enqueuing
@@ -453,10 +504,11 @@ int for_shards(std::vector<std::unique_ptr<Device>>& devs, uint64_t n, uint64_t 
 // touching device buffers an asynchronous device-path call may still use.
 class SetLease {
  public:
-  explicit SetLease(Device& d, int prefer = 0) : d_(d) {
+  // exact: set `prefer` itself (the idle release takes both)
+  explicit SetLease(Device& d, int prefer = 0, bool exact = false) : d_(d) {
     std::unique_lock<std::mutex> g(d.set_m);
     for (;;) {
-      for (int k = 0; k < kTxSets; k++) {
+      for (int k = 0; k < (exact ? 1 : kTxSets); k++) {
         const int i = (prefer + k) % kTxSets;
         if (!d.set_busy[i]) {
           d.set_busy[i] = true;
@@ -500,6 +552,12 @@ struct cordahip_ctx {
   static constexpr size_t kTxOfCache = 4;
   std::mutex txof_mu;
   std::vector<std::pair<std::unique_ptr<uint64_t[]>, uint64_t>> txof_free;
+  // the idle release (CORDAHIP_IDLE_RELEASE_MS): a thread that frees an idle
+  // device's grow-only buffers (cordahip.cpp trim_device)
+  std::thread reaper;
+  std::mutex reaper_mu;
+  std::condition_variable reaper_cv;
+  bool reaper_stop = false;
 };
 
 namespace cordahip {

@@ -239,6 +239,17 @@ class Engine:
             keys.data_ptr(), sigs.data_ptr(), keys.shape[0], txid.data_ptr(), tx_status.data_ptr(),
             first_bad.data_ptr(), sig_status.data_ptr(), s), "cordahip_signed_txcomp_verify_ed25519_device")
 
+    def device_mem(self, device: int = 0):
+        """cordahip_device_mem: (bytes the library holds on the device's GPU, their peak, the budget)"""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().cordahip_device_mem(self._ctx, device, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+              "cordahip_device_mem")
+        return a.value, b.value, c.value
+
+    def trim(self):
+        """cordahip_trim: release every device's grow-only buffers now"""
+        check(lib().cordahip_trim(self._ctx), "cordahip_trim")
+
     def kryo_encode_device(self, items, n: int, out, off, status, group: int = 1, device: int = 0, stream=None):
         """cordahip_kryo_encode_device: leaf preimages of n components on the GPU. items: a
         device tensor holding n cordahip_kryo_item records (_lib.KRYO_ITEM_DTYPE) whose data

@@ -84,6 +84,19 @@ int cordahip_init(uint32_t device_mask, cordahip_ctx** out);
 void cordahip_shutdown(cordahip_ctx* ctx);
 int cordahip_device_count(const cordahip_ctx* ctx);
 
+/* Device memory (ABI 4). cordahip_device_mem: the bytes the library holds on
+ * `device`'s GPU now and at most so far (workspaces, stages, fixed tables), and
+ * its budget. The budget (CORDAHIP_DEVICE_MEM_BUDGET at cordahip_init, bytes
+ * with an optional K/M/G suffix; default 128 GiB, at most 90% of the device)
+ * sizes the verification workspaces -- Ed25519 45% (+20% for the pipelines'
+ * second slot), ECDSA 15%; a smaller budget only costs extra launches. The
+ * batch-proportional buffers (stages, id buffers) follow the batches. Buffers
+ * are grow-only while a device is busy; after CORDAHIP_IDLE_RELEASE_MS (default
+ * 30000; 0: never) without a call they are released, as cordahip_trim does now
+ * (it waits for the calls in progress). INTEGRATION.md §6. */
+int cordahip_device_mem(cordahip_ctx* ctx, int device, uint64_t* in_use, uint64_t* peak, uint64_t* budget);
+int cordahip_trim(cordahip_ctx* ctx);
+
 int cordahip_alloc_pinned(cordahip_ctx* ctx, size_t bytes, void** host);
 int cordahip_free_pinned(cordahip_ctx* ctx, void* host);
 
