@@ -36,3 +36,42 @@ int oracle_tx_id(const uint8_t* leaf_bytes, const uint64_t* leaf_off, size_t nle
   free(h);
   return rc;
 }
+
+/* oracle_tx_id over many transactions (the agreement sweeps' id checker):
+ * tx t's leaves are [tx_leaf_off[t], tx_leaf_off[t+1]) of the leaf CSR;
+ * status[t] = 0, or 6 (CORDAHIP_TX_NO_LEAVES) for a transaction without
+ * leaves (MerkleTreeException, MerkleTree.kt:49-50), its id left zero. */
+#include <pthread.h>
+
+typedef struct {
+  size_t lo, hi;
+  const uint8_t* leaf_bytes;
+  const uint64_t* leaf_off;
+  const uint64_t* tx_leaf_off;
+  uint8_t* ids;
+  uint8_t* status;
+} txid_job_t;
+
+static void* txid_worker(void* p) {
+  txid_job_t* j = (txid_job_t*)p;
+  for (size_t t = j->lo; t < j->hi; t++) {
+    const uint64_t a = j->tx_leaf_off[t], b = j->tx_leaf_off[t + 1];
+    memset(j->ids + 32 * t, 0, 32);
+    const int rc = oracle_tx_id(j->leaf_bytes, j->leaf_off + a, (size_t)(b - a), j->ids + 32 * t);
+    j->status[t] = rc == 0 ? 0 : 6;
+  }
+  return NULL;
+}
+
+void oracle_tx_id_batch(size_t ntx, const uint8_t* leaf_bytes, const uint64_t* leaf_off, const uint64_t* tx_leaf_off,
+                        uint8_t* ids, uint8_t* status, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  txid_job_t jobs[256];
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (txid_job_t){ntx * t / nthreads, ntx * (t + 1) / nthreads, leaf_bytes, leaf_off, tx_leaf_off, ids, status};
+    pthread_create(&th[t], NULL, txid_worker, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}

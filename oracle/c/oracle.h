@@ -70,6 +70,10 @@ void oracle_ecdsa_verify_batch(size_t n, const uint8_t* scheme, const uint8_t* k
 
 /* WireTransaction.id from the serialised components (leaf preimages, CSR). */
 int oracle_tx_id(const uint8_t* leaf_bytes, const uint64_t* leaf_off, size_t nleaves, uint8_t id[32]);
+/* oracle_tx_id for each of ntx transactions (tx_leaf_off [ntx+1] into the leaf CSR),
+ * on nthreads threads; status[t] 0, or 6 for no leaves */
+void oracle_tx_id_batch(size_t ntx, const uint8_t* leaf_bytes, const uint64_t* leaf_off, const uint64_t* tx_leaf_off,
+                        uint8_t* ids, uint8_t* status, int nthreads);
 
 #ifdef __cplusplus
 }

@@ -42,6 +42,7 @@ def load_oracle():
     lib.oracle_ed25519_is_valid.argtypes = [cp, sz, cp, sz, cp, sz]
     lib.oracle_ecdsa_verify_batch.argtypes = [sz] + [ctypes.c_void_p] * 8 + [ctypes.c_int]
     lib.oracle_tx_id.argtypes = [ctypes.c_void_p, ctypes.c_void_p, sz, ctypes.c_char_p]
+    lib.oracle_tx_id_batch.argtypes = [sz] + [ctypes.c_void_p] * 5 + [ctypes.c_int]
     return lib
 
 

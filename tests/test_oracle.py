@@ -247,3 +247,30 @@ def test_ecdsa_oracles_match_reference_certificates(oracle, cert_vectors):
             assert v["status"] == 0 and len(m) > 300  # multi-block SHA-256 messages (TBSCertificate)
     assert schemes == {2, 3}
     assert sum(v["cat"] == "reference_cert" for v in cert_vectors) >= 6
+
+
+def test_tx_id_batch_equals_per_tx(oracle):
+    """oracle_tx_id_batch (the agreement sweeps' id checker) == oracle_tx_id per
+    transaction, threaded, including transactions without leaves (status 6)"""
+    import ctypes
+    import random
+    import numpy as np
+    rng = random.Random(71)
+    txs = [[bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 90))) for _ in range(rng.randrange(0, 9))]
+           for _ in range(300)]
+    leaves = [x for tx in txs for x in tx]
+    blob = np.frombuffer(b"".join(leaves) or b"\0", np.uint8).copy()
+    lo = np.zeros(len(leaves) + 1, np.uint64)
+    lo[1:] = np.cumsum([len(x) for x in leaves])
+    tlo = np.zeros(len(txs) + 1, np.uint64)
+    tlo[1:] = np.cumsum([len(tx) for tx in txs])
+    ids = np.zeros((len(txs), 32), np.uint8)
+    st = np.zeros(len(txs), np.uint8)
+    oracle.oracle_tx_id_batch(len(txs), blob.ctypes.data, lo.ctypes.data, tlo.ctypes.data, ids.ctypes.data,
+                              st.ctypes.data, 4)
+    for t, tx in enumerate(txs):
+        one = ctypes.create_string_buffer(32)
+        rc = oracle.oracle_tx_id(blob.ctypes.data, lo[int(tlo[t]):].ctypes.data, len(tx), one)
+        assert st[t] == (0 if rc == 0 else 6)
+        if rc == 0:
+            assert ids[t].tobytes() == one.raw
