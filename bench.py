@@ -158,7 +158,7 @@ class C2:
     # reduction -> per-lane workspace) + ladder, one launch pair for the whole
     # 2^24-lane batch (the workspace holds 2^24 lanes, cordahip.cpp kEdWsLanes)
     kernel = "ed25519_prep_half_kernel + ed25519_ladder_half_kernel"
-    pmc = "r04_pmc_ed25519_split.json"
+    pmc = "r06_pmc_c2.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -227,6 +227,7 @@ class C1(C2):
     thread and at `cores` threads, and OpenSSL 3 EVP_DigestVerify (an independent
     CPU Ed25519, raw-key decode included per call like Crypto.doVerify's key
     handling) on a sample, all on the same tuples."""
+    pmc = "r06_pmc_c1.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
 
     def __init__(self, eng, device, stream, rank, args):
         import hashlib
@@ -295,7 +296,7 @@ class C1(C2):
 # ---- C3: mixed secp256k1 / P-256 ECDSA ----------------------------------------
 class C3:
     kernel = "ecdsa_prep_kernel + ecdsa_inv_kernel + ecdsa_ladder_kernel"
-    pmc = "r03_pmc_ecdsa_verify.json"
+    pmc = "r06_pmc_c3.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -367,7 +368,7 @@ class C3:
 # ---- C4: SignedTransaction.verifySignatures on cash-issue transactions --------
 class C4:
     kernel = "sha256_leaves + merkle_root + ed25519 prep/ladder + tx_reduce"
-    pmc = "r04_pmc_c4.json"  # tools/leases/gpu_r4_pmc2.sh -> pmc_compose.py -> pmc_hbm_split.py (ladder MALL split)
+    pmc = "r06_pmc_c4.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -484,8 +485,7 @@ class C4:
         if self.device_encode:
             self.kernel = ("cordahip_signed_txcomp_verify_ed25519_device: kryo_shape + kryo_hash (leaf hashes from the "
                            "templates) + merkle_root + ed25519 prep/ladder + tx_reduce")
-            # the id chain's L2-to-fabric bytes per tx (its own PMC passes, tools/pmc_kryo_traffic.py)
-            self.extra_pmc = ("r06_pmc_c4_device_chain.json", ntx)
+            self.pmc = "r06_pmc_c4de.json"  # its own step: the id chain from components included
             self.config["component_bytes_per_tx"] = round(self.d_blob.numel() / ntx, 1)
         if not self.native:
             self.config["leaf_lens"] = list(C4_LEAF_LENS)
@@ -563,7 +563,7 @@ class C4:
 # ---- C5: verifier-module queue drain, mixed schemes, pinned host memory -------
 class C5:
     kernel = "ed25519 prep/ladder + ecdsa prep/inv/ladder, 3-stage H2D/kernel/D2H pipeline"
-    pmc = "r04_pmc_c5.json"  # tools/leases/gpu_r4_pmc2.sh -> pmc_compose.py -> pmc_hbm_split.py (device side, per lane)
+    pmc = "r06_pmc_c5.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
     host_timed = True  # the drain is synchronous and owns its streams: wall time, PCIe included
 
     def __init__(self, eng, device, stream, rank, args):
@@ -715,6 +715,7 @@ class C2H(C2):
     the whole call: lane classification, host packing into pinned staging, PCIe
     both ways, the kernels, status scatter and verdict words."""
     kernel = "cordahip_sig_verify (host CSR batch): pack + H2D + ed25519 prep/ladder + D2H, pipelined"
+    pmc = "r06_pmc_c2h.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
     host_timed = True
 
     def __init__(self, eng, device, stream, rank, args):
@@ -759,6 +760,7 @@ class C3H(C3):
     """C3's corpus (mixed secp256k1 / P-256, DER signatures of 8-73 bytes, 33- or
     65-byte keys) through cordahip_sig_verify as a pinned host CSR batch."""
     kernel = "cordahip_sig_verify (host CSR batch): pack + H2D + ecdsa partition/prep/inv/ladders + D2H, pipelined"
+    pmc = "r06_pmc_c3h.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
     host_timed = True
 
     def __init__(self, eng, device, stream, rank, args):
@@ -796,6 +798,7 @@ class C4H(C4):
     signatures, CSR keys/sigs with scheme bytes). Timed: tx ids (leaf SHA-256 +
     Merkle) then every signature over its tx's id, PCIe both ways included."""
     kernel = "cordahip_tx_submit (host CSR): tx ids (sha256_leaves + merkle_root) then cordahip_sig_verify lanes"
+    pmc = "r06_pmc_c4h.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
     host_timed = True
 
     def __init__(self, eng, device, stream, rank, args):
@@ -839,8 +842,10 @@ class C4H(C4):
             self.pcie_tx_bytes = (items.nbytes + 8 * (5 * ntx + 1) + payload.size) / ntx
             what = ("the components of each tx (cordahip_txcomp_submit: %.0f B per tx of Kryo items and payload; "
                     "the GPU writes the %.0f B of leaves)" % (self.pcie_tx_bytes, self.leaf_bytes.numel() / ntx))
-            self.kernel = ("cordahip_txcomp_submit (host CSR): kryo encode + sha256_leaves + merkle_root per id slice, "
-                           "then cordahip_sig_verify lanes")
+            self.kernel = ("cordahip_txcomp_submit (host CSR): per id slice kryo_shape + kryo_hash (the leaves' "
+                           "SHA-256 from the encoder's templates; the full encoder + sha256_leaves when a shape is "
+                           "new) + merkle_root, then the signature chunks")
+            self.pmc = "r06_pmc_c4hc.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
         else:
             self.t = [_pinned(x) for x in (
                 self.leaf_bytes.cpu().numpy(), self.leaf_off.cpu().numpy().astype(np.uint64),
