@@ -579,14 +579,26 @@ uint64_t comp_payload_bytes(const cordahip_kryo_item& it) {
 }
 
 // Component-level batches (cordahip_txcomp_batch): per id slice, how far the
-// payload prefix must reach, the leaf buffer it needs, and its items per tx.
+// payload must reach, the leaf buffer it needs, and its items per tx.
+// The payload crosses PCIe as two windows: the low one [0, low_end) -- the
+// payloads below `split`, in practice those every transaction shares (the
+// notary Party, TransactionType), written first -- once with the first slice,
+// and the high one [high_min, pay_end[j]) growing slice by slice. Any split
+// covers every item (an item lies below it or not); taking it at the shard's
+// first transaction's last payload makes the high window start at this shard's
+// own payloads, so a device of a multi-device context no longer copies the
+// earlier shards' payloads (r05 copied [0, pay_end) on every device).
 struct CompPlan {
   const cordahip_txcomp_batch* c = nullptr;
-  std::vector<uint64_t> pay_end;  // payload bytes slices 0..j reference (running max)
+  std::vector<uint64_t> pay_end;  // high-window bytes slices 0..j reference (running max)
   std::vector<uint32_t> group;    // items per transaction when uniform in the slice (the encoder's hint), else 1
   uint64_t slice_cap = 16;        // leaf bytes of the largest slice's bound (two slice buffers alternate)
   uint64_t max_items = 0;
-  uint64_t copied = 0;            // payload prefix enqueued so far
+  uint64_t split = 0;             // items at offsets below it are the low window's
+  uint64_t low_end = 0;           // the low window [0, low_end)
+  uint64_t high_min = UINT64_MAX; // the high window's first byte
+  uint64_t copied = 0;            // high window enqueued up to here (from high_min)
+  bool low_copied = false;
   bool templates_only = false;    // the steady-state encoder chain (misses redo the call)
   static constexpr uint64_t kDirectWriters = 1u << 13;  // the direct encoder's writers (rarely any work)
 };
@@ -602,44 +614,71 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, TxSet& S, int set_idx, c
     const size_t ns = bound.size() - 1;
     cp->pay_end.assign(ns, 0);
     cp->group.assign(ns, 1);
-    std::vector<uint64_t> cap(ns, 0);
+    std::vector<uint64_t> cap(ns, 0), low(ns, 0), hmin(ns, UINT64_MAX);
+    auto fits = [&](const cordahip_kryo_item& it, uint64_t& off, uint64_t& nb) {
+      off = (uint64_t)(uintptr_t)it.data;
+      nb = comp_payload_bytes(it);
+      return off <= c->payload_len && nb <= c->payload_len - off;
+    };
+    cp->split = 0;  // the shard's first transaction's last payload (its own, past the shared ones)
+    for (uint64_t i = c->tx_item_off[t0]; i < c->tx_item_off[t0 + 1]; i++) {
+      uint64_t off, nb;
+      if (fits(c->items[i], off, nb) && nb) cp->split = std::max(cp->split, off);
+    }
     pool_of(ctx, d).parallel_for(ns, 1, [&](uint64_t x, uint64_t y) {
       for (uint64_t j = x; j < y; j++) {
         const uint64_t ts0 = bound[j], ts1 = bound[j + 1];
         const uint64_t g = ts1 > ts0 ? c->tx_item_off[ts0 + 1] - c->tx_item_off[ts0] : 1;
         bool uniform = g > 0;
-        uint64_t end = 0, bd = 0;
+        uint64_t end = 0, bd = 0, lo_end = 0, hi_min = UINT64_MAX;
         for (uint64_t t = ts0; t < ts1; t++) {
           uniform = uniform && c->tx_item_off[t + 1] - c->tx_item_off[t] == g;
           for (uint64_t i = c->tx_item_off[t]; i < c->tx_item_off[t + 1]; i++) {
             const cordahip_kryo_item& it = c->items[i];
-            const uint64_t off = (uint64_t)(uintptr_t)it.data, nb = comp_payload_bytes(it);
+            uint64_t off, nb;
+            const bool ok = fits(it, off, nb);
             if (it.kind != CORDAHIP_KRYO_RAW && nb == 0) {
               bd += comp_leaf_bound(0);
               continue;
             }
-            const bool fits = off <= c->payload_len && nb <= c->payload_len - off;
-            if (fits) end = std::max(end, off + nb);
-            bd += comp_leaf_bound(fits ? nb : 0);
+            if (ok) {
+              if (off < cp->split) {
+                lo_end = std::max(lo_end, off + nb);
+              } else {
+                hi_min = std::min(hi_min, off);
+                end = std::max(end, off + nb);
+              }
+            }
+            bd += comp_leaf_bound(ok ? nb : 0);
           }
         }
         cp->pay_end[j] = end;
+        low[j] = lo_end;
+        hmin[j] = hi_min;
         cp->group[j] = uniform && g <= 64 ? (uint32_t)g : 1;
         cap[j] = bd;
       }
     });
+    cp->low_end = 0;
+    cp->high_min = UINT64_MAX;
+    for (size_t j = 0; j < ns; j++) {
+      cp->low_end = std::max(cp->low_end, low[j]);
+      cp->high_min = std::min(cp->high_min, hmin[j]);
+    }
+    if (cp->high_min == UINT64_MAX) cp->high_min = 0;
     for (size_t j = 0; j < ns; j++) {
       if (j) cp->pay_end[j] = std::max(cp->pay_end[j], cp->pay_end[j - 1]);
       cp->slice_cap = std::max(cp->slice_cap, cap[j]);
       cp->max_items = std::max(cp->max_items, b->tx_leaf_off[bound[j + 1]] - b->tx_leaf_off[bound[j]]);
     }
-    cp->copied = 0;
+    cp->copied = cp->high_min;
+    cp->low_copied = false;
     // the templates-only chain hashes the leaves from their templates: no leaf buffers
     // (the full chain's two slice buffers are bounded at 4 KB + 4 B per payload byte per
     // component: ~1.4 GB each for C4's 2^17-signature slices)
     cp->templates_only = cp->templates_only && d.kryo_templates_ok;
     if (w.comp_items.ensure(std::max<uint64_t>(nleaves, 1) * sizeof(cordahip_kryo_item)) ||
-        w.payload.ensure(std::max<uint64_t>(ns ? cp->pay_end.back() : 0, 16)) ||
+        w.payload.ensure(std::max<uint64_t>(std::max(ns ? cp->pay_end.back() : 0, cp->low_end), 16)) ||
         w.comp_status.ensure(std::max<uint64_t>(nleaves, 1)))
       return hipErrorOutOfMemory;
     // the encoder's scratch (d.kryo_*, kryo_mu held by the caller) for the largest slice
@@ -701,7 +740,12 @@ hipError_t tx_ids_enqueue(Device& d, TxSet& S, int set_idx, const cordahip_txid_
       if (ls1 > ls0)
         e = hipMemcpyAsync(w.comp_items.as<cordahip_kryo_item>() + (ls0 - l0), c->items + ls0,
                            (ls1 - ls0) * sizeof(cordahip_kryo_item), h2d, sc);
-      if (e == hipSuccess && cp->pay_end[j] > cp->copied) {
+      if (e == hipSuccess && !cp->low_copied) {  // the low window, once (the shared payloads)
+        cp->low_copied = true;
+        if (cp->low_end)
+          e = hipMemcpyAsync(w.payload.as<uint8_t>(), c->payload, cp->low_end, h2d, sc);
+      }
+      if (e == hipSuccess && cp->pay_end[j] > cp->copied) {  // the high window grows with the slices
         e = blocked("payload H2D", [&] {
           return hipMemcpyAsync(w.payload.as<uint8_t>() + cp->copied, c->payload + cp->copied,
                                 cp->pay_end[j] - cp->copied, h2d, sc);
@@ -971,7 +1015,10 @@ int signed_tx_device_once(cordahip_ctx* ctx, Device& d, const cordahip_signed_tx
   if (r == CORDAHIP_SUCCESS && s1 > s0) {
     di.txid = S.tx.txid.as<uint8_t>();
     di.t0 = lo;
-    di.split_prep = cp == nullptr;
+    // CORDAHIP_TX_SPLIT_PREP (A/B): 0 fused prep everywhere, 1 split for component batches
+    // too; default split for leaf batches only (r05, profiles/r05_prep_split_ab/)
+    static const int split_env = getenv("CORDAHIP_TX_SPLIT_PREP") ? atoi(getenv("CORDAHIP_TX_SPLIT_PREP")) : -1;
+    di.split_prep = split_env < 0 ? cp == nullptr : split_env > 0;
     // before a chunk's copies: the slices it needs; after them: `lookahead` more,
     // so PCIe carries leaf bytes while the GPU verifies the chunk
     di.advance = [&](uint64_t sig_end, bool after) {
