@@ -158,7 +158,7 @@ class C2:
     # reduction -> per-lane workspace) + ladder, one launch pair for the whole
     # 2^24-lane batch (the workspace holds 2^24 lanes, cordahip.cpp kEdWsLanes)
     kernel = "ed25519_prep_half_kernel + ed25519_ladder_half_kernel"
-    pmc = "r06_pmc_c2.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
+    pmc = "r06_pmc_c2.json"  # tools/gpu_pmc_step.sh -> tools/pmc_step.py: one timed step of this workload
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -227,7 +227,7 @@ class C1(C2):
     thread and at `cores` threads, and OpenSSL 3 EVP_DigestVerify (an independent
     CPU Ed25519, raw-key decode included per call like Crypto.doVerify's key
     handling) on a sample, all on the same tuples."""
-    pmc = "r06_pmc_c1.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
+    pmc = "r06_pmc_c1.json"  # tools/gpu_pmc_step.sh -> tools/pmc_step.py: one timed step of this workload
 
     def __init__(self, eng, device, stream, rank, args):
         import hashlib
@@ -296,7 +296,7 @@ class C1(C2):
 # ---- C3: mixed secp256k1 / P-256 ECDSA ----------------------------------------
 class C3:
     kernel = "ecdsa_prep_kernel + ecdsa_inv_kernel + ecdsa_ladder_kernel"
-    pmc = "r06_pmc_c3.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
+    pmc = "r06_pmc_c3.json"  # tools/gpu_pmc_step.sh -> tools/pmc_step.py: one timed step of this workload
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -368,7 +368,7 @@ class C3:
 # ---- C4: SignedTransaction.verifySignatures on cash-issue transactions --------
 class C4:
     kernel = "sha256_leaves + merkle_root + ed25519 prep/ladder + tx_reduce"
-    pmc = "r06_pmc_c4.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
+    pmc = "r06_pmc_c4.json"  # tools/gpu_pmc_step.sh -> tools/pmc_step.py: one timed step of this workload
 
     def __init__(self, eng, device, stream, rank, args):
         import torch
@@ -563,7 +563,7 @@ class C4:
 # ---- C5: verifier-module queue drain, mixed schemes, pinned host memory -------
 class C5:
     kernel = "ed25519 prep/ladder + ecdsa prep/inv/ladder, 3-stage H2D/kernel/D2H pipeline"
-    pmc = "r06_pmc_c5.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
+    pmc = "r06_pmc_c5.json"  # tools/gpu_pmc_step.sh -> tools/pmc_step.py: one timed step of this workload
     host_timed = True  # the drain is synchronous and owns its streams: wall time, PCIe included
 
     def __init__(self, eng, device, stream, rank, args):
@@ -715,7 +715,7 @@ class C2H(C2):
     the whole call: lane classification, host packing into pinned staging, PCIe
     both ways, the kernels, status scatter and verdict words."""
     kernel = "cordahip_sig_verify (host CSR batch): pack + H2D + ed25519 prep/ladder + D2H, pipelined"
-    pmc = "r06_pmc_c2h.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
+    pmc = "r06_pmc_c2h.json"  # tools/gpu_pmc_step.sh -> tools/pmc_step.py: one timed step of this workload
     host_timed = True
 
     def __init__(self, eng, device, stream, rank, args):
@@ -760,7 +760,7 @@ class C3H(C3):
     """C3's corpus (mixed secp256k1 / P-256, DER signatures of 8-73 bytes, 33- or
     65-byte keys) through cordahip_sig_verify as a pinned host CSR batch."""
     kernel = "cordahip_sig_verify (host CSR batch): pack + H2D + ecdsa partition/prep/inv/ladders + D2H, pipelined"
-    pmc = "r06_pmc_c3h.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
+    pmc = "r06_pmc_c3h.json"  # tools/gpu_pmc_step.sh -> tools/pmc_step.py: one timed step of this workload
     host_timed = True
 
     def __init__(self, eng, device, stream, rank, args):
@@ -798,7 +798,7 @@ class C4H(C4):
     signatures, CSR keys/sigs with scheme bytes). Timed: tx ids (leaf SHA-256 +
     Merkle) then every signature over its tx's id, PCIe both ways included."""
     kernel = "cordahip_tx_submit (host CSR): tx ids (sha256_leaves + merkle_root) then cordahip_sig_verify lanes"
-    pmc = "r06_pmc_c4h.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
+    pmc = "r06_pmc_c4h.json"  # tools/gpu_pmc_step.sh -> tools/pmc_step.py: one timed step of this workload
     host_timed = True
 
     def __init__(self, eng, device, stream, rank, args):
@@ -845,7 +845,7 @@ class C4H(C4):
             self.kernel = ("cordahip_txcomp_submit (host CSR): per id slice kryo_shape + kryo_hash (the leaves' "
                            "SHA-256 from the encoder's templates; the full encoder + sha256_leaves when a shape is "
                            "new) + merkle_root, then the signature chunks")
-            self.pmc = "r06_pmc_c4hc.json"  # tools/leases/gpu_r6_pmc.sh -> tools/pmc_step.py: one timed step of this workload
+            self.pmc = "r06_pmc_c4hc.json"  # tools/gpu_pmc_step.sh -> tools/pmc_step.py: one timed step of this workload
         else:
             self.t = [_pinned(x) for x in (
                 self.leaf_bytes.cpu().numpy(), self.leaf_off.cpu().numpy().astype(np.uint64),
@@ -1268,6 +1268,12 @@ def main():
             "verdict_check": chk,
             "corpus_gen_s": t_gen,
         }
+        if eng is not None:
+            # the library's device memory after the run (cordahip_device_mem): what this workload
+            # held at its peak against the budget (CORDAHIP_DEVICE_MEM_BUDGET); torch's corpus
+            # tensors are the caller's and not counted
+            in_use, peak, budget = eng.device_mem(0)
+            out["device_mem_gb"] = {"in_use": in_use / 1e9, "peak": peak / 1e9, "budget": budget / 1e9}
         ghz = clock.get("clock_ghz") if clock else None
         mpeak = 256 * MAD_U64_LANE_OPS_PER_CU_CYCLE * (ghz or 2.4) * 1e9 / 1e12
         out["roofline"]["peak_measured"] = mpeak

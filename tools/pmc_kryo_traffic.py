@@ -35,7 +35,7 @@ def per_dispatch(path, counter):
 def main():
     p1, p2, txs, calls = sys.argv[1], sys.argv[2], float(sys.argv[3]), int(sys.argv[4])
     fetch, write = per_dispatch(p1, "FETCH_SIZE"), per_dispatch(p2, "WRITE_SIZE")
-    out = {"command": "tools/leases/gpu_r5n.sh: rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, over "
+    out = {"command": "profiles/recipes/gpu_r5n.sh: rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, over "
                       "tools/kryo_dev_bench.py --txs %d --calls %d" % (txs, calls - 1),
            "txs": txs, "kernels": {}}
     tot_f = tot_w = 0.0

@@ -5,7 +5,7 @@ second timed step's kernels -- corpus generation, the init step, the checks and
 the first call's one-time work (shape builds, workspace growth) cancel -- so
 every line's roofline fields come from a PMC of its own workload.
 
-Counters (tools/leases/gpu_r6_pmc.sh): pass A = SQ_INSTS_VALU SQ_ACTIVE_INST_VALU
+Counters (tools/gpu_pmc_step.sh): pass A = SQ_INSTS_VALU SQ_ACTIVE_INST_VALU
 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY
 SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE, pass B = FETCH_SIZE, pass C = WRITE_SIZE,
 each in its own run. Derived as tools/pmc_compose.py does (FETCH_SIZE x2, the
@@ -85,7 +85,7 @@ def main():
             tot[n] += v
     td = derive(tot, units)
     fabric = td.get("hbm_fetch_bytes_per_lane", 0) + td.get("hbm_write_bytes_per_lane", 0)
-    out = {"command": "tools/leases/gpu_r6_pmc.sh: rocprofv3 --pmc, 3 passes x (--steps 1, --steps 2) of "
+    out = {"command": "tools/gpu_pmc_step.sh: rocprofv3 --pmc, 3 passes x (--steps 1, --steps 2) of "
                       "bench.py %s --warmup 0 --no-clock --no-cpu-baseline; one step = the difference" % cmd,
            "workload": tag, "units_per_step": units, "lanes_per_pass": int(round(units)),
            "kernels": kernels, "total": {"counters": dict(tot), "derived": td},
