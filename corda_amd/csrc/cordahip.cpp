@@ -592,7 +592,8 @@ struct CompPlan {
   const cordahip_txcomp_batch* c = nullptr;
   std::vector<uint64_t> pay_end;  // high-window bytes slices 0..j reference (running max)
   std::vector<uint32_t> group;    // items per transaction when uniform in the slice (the encoder's hint), else 1
-  uint64_t slice_cap = 16;        // leaf bytes of the largest slice's bound (two slice buffers alternate)
+  uint64_t slice_cap = 16;        // leaf bytes of the largest piece's bound (the full chain's one leaf buffer)
+  std::vector<std::vector<uint64_t>> cuts;  // per slice: the transactions that start a new piece of the full chain
   uint64_t max_items = 0;
   uint64_t split = 0;             // items at offsets below it are the low window's
   uint64_t low_end = 0;           // the low window [0, low_end)
@@ -614,6 +615,12 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, TxSet& S, int set_idx, c
     const size_t ns = bound.size() - 1;
     cp->pay_end.assign(ns, 0);
     cp->group.assign(ns, 1);
+    cp->cuts.assign(ns, {});
+    // the full chain's leaf buffer: a tenth of the device budget at most (the budget's
+    // share for component slices; C4's 2^17-signature slices bound ~1.4 GB, far below
+    // the default's 13.7 GB); a slice whose bound exceeds it is encoded and hashed in
+    // pieces of whole transactions, one after another through the one buffer
+    const uint64_t piece_cap = std::max<uint64_t>(d.mem_budget / 10, 1u << 20);
     std::vector<uint64_t> cap(ns, 0), low(ns, 0), hmin(ns, UINT64_MAX);
     auto fits = [&](const cordahip_kryo_item& it, uint64_t& off, uint64_t& nb) {
       off = (uint64_t)(uintptr_t)it.data;
@@ -630,9 +637,10 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, TxSet& S, int set_idx, c
         const uint64_t ts0 = bound[j], ts1 = bound[j + 1];
         const uint64_t g = ts1 > ts0 ? c->tx_item_off[ts0 + 1] - c->tx_item_off[ts0] : 1;
         bool uniform = g > 0;
-        uint64_t end = 0, bd = 0, lo_end = 0, hi_min = UINT64_MAX;
+        uint64_t end = 0, bd = 0, lo_end = 0, hi_min = UINT64_MAX, piece_max = 0;
         for (uint64_t t = ts0; t < ts1; t++) {
           uniform = uniform && c->tx_item_off[t + 1] - c->tx_item_off[t] == g;
+          const uint64_t bd_tx = bd;
           for (uint64_t i = c->tx_item_off[t]; i < c->tx_item_off[t + 1]; i++) {
             const cordahip_kryo_item& it = c->items[i];
             uint64_t off, nb;
@@ -651,12 +659,17 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, TxSet& S, int set_idx, c
             }
             bd += comp_leaf_bound(ok ? nb : 0);
           }
+          if (bd > piece_cap && bd_tx > 0 && t > ts0) {  // t starts a new piece
+            cp->cuts[j].push_back(t);
+            piece_max = std::max(piece_max, bd_tx);
+            bd -= bd_tx;
+          }
         }
         cp->pay_end[j] = end;
         low[j] = lo_end;
         hmin[j] = hi_min;
         cp->group[j] = uniform && g <= 64 ? (uint32_t)g : 1;
-        cap[j] = bd;
+        cap[j] = std::max(piece_max, bd);
       }
     });
     cp->low_end = 0;
@@ -674,8 +687,8 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, TxSet& S, int set_idx, c
     cp->copied = cp->high_min;
     cp->low_copied = false;
     // the templates-only chain hashes the leaves from their templates: no leaf buffers
-    // (the full chain's two slice buffers are bounded at 4 KB + 4 B per payload byte per
-    // component: ~1.4 GB each for C4's 2^17-signature slices)
+    // (the full chain's leaf buffer is bounded at 4 KB + 4 B per payload byte per
+    // component of its largest piece: ~1.4 GB for C4's 2^17-signature slices)
     cp->templates_only = cp->templates_only && d.kryo_templates_ok;
     if (w.comp_items.ensure(std::max<uint64_t>(nleaves, 1) * sizeof(cordahip_kryo_item)) ||
         w.payload.ensure(std::max<uint64_t>(std::max(ns ? cp->pay_end.back() : 0, cp->low_end), 16)) ||
@@ -698,7 +711,7 @@ hipError_t tx_ids_prepare(cordahip_ctx* ctx, Device& d, TxSet& S, int set_idx, c
     if (hipError_t e = kryo_reset_misses(d.kryo_fixed.as<uint8_t>(), (uint32_t)set_idx, d.stream)) return e;
     cp->templates_only = cp->templates_only && d.kryo_templates_ok;  // kryo_state_ready may have cleared the table
     // sized after that: a cleared table runs the full chain, which writes leaves
-    leaf_buf = cp->templates_only ? 0 : 2 * cp->slice_cap;
+    leaf_buf = cp->templates_only ? 0 : cp->slice_cap;
     if (tracing())
       fprintf(stderr, "[cordahip] dev %d set %d component call: %s chain (templates %u, slots %u in use)\n", d.id,
               set_idx, cp->templates_only ? "templates-only" : "full encoder", S.kryo_usage[0], S.kryo_usage[1]);
@@ -770,19 +783,27 @@ hipError_t tx_ids_enqueue(Device& d, TxSet& S, int set_idx, const cordahip_txid_
                                    d.kryo_fixed.as<uint8_t>(), slots, d.kryo_sizes.as<uint64_t>(), cst,
                                    w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
     } else if (cp) {
-      // the slice's leaves on the GPU (the template encoder) into one of two
-      // alternating slice buffers, offsets relative to that buffer
-      uint8_t* sb = w.leaf_bytes.as<uint8_t>() + (j % 2) * cp->slice_cap;
+      // the slice's leaves on the GPU (the template encoder) into the leaf buffer,
+      // offsets relative to it, then their SHA-256; piece by piece (whole
+      // transactions) when the slice's bound exceeds the buffer. Every piece runs
+      // on s, so the next piece's writes follow the previous piece's hashing.
+      uint8_t* sb = w.leaf_bytes.as<uint8_t>();
       uint32_t* slots = d.kryo_items.as<uint32_t>();
-      const uint64_t n = ls1 - ls0;
-      e = e ? e : launch_kryo_encode(w.comp_items.as<cordahip_kryo_item>() + (ls0 - l0), w.payload.as<uint8_t>(),
-                                     cp->c->payload_len, n, cp->group[j], d.kryo_fixed.as<uint8_t>(), slots, slots + n,
-                                     d.kryo_sizes.as<uint64_t>(), w.leaf_off.as<uint64_t>() + (ls0 - l0), sb,
-                                     cp->slice_cap, w.comp_status.as<uint8_t>() + (ls0 - l0), d.kryo_ws.as<uint8_t>(),
-                                     CompPlan::kDirectWriters, d.kryo_temp.p, d.kryo_temp.cap, s, cp->templates_only,
-                                     (uint32_t)set_idx);
-      e = e ? e : launch_sha256_leaves(sb, w.leaf_off.as<uint64_t>() + (ls0 - l0), n,
-                                       w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
+      uint64_t pa = ts0;
+      for (size_t k = 0; k <= cp->cuts[j].size() && e == hipSuccess; k++) {
+        const uint64_t pb = k < cp->cuts[j].size() ? cp->cuts[j][k] : ts1;
+        const uint64_t is0 = b->tx_leaf_off[pa], n = b->tx_leaf_off[pb] - is0;
+        pa = pb;
+        if (!n) continue;
+        e = launch_kryo_encode(w.comp_items.as<cordahip_kryo_item>() + (is0 - l0), w.payload.as<uint8_t>(),
+                               cp->c->payload_len, n, cp->group[j], d.kryo_fixed.as<uint8_t>(), slots, slots + n,
+                               d.kryo_sizes.as<uint64_t>(), w.leaf_off.as<uint64_t>() + (is0 - l0), sb, cp->slice_cap,
+                               w.comp_status.as<uint8_t>() + (is0 - l0), d.kryo_ws.as<uint8_t>(),
+                               CompPlan::kDirectWriters, d.kryo_temp.p, d.kryo_temp.cap, s, cp->templates_only,
+                               (uint32_t)set_idx);
+        e = e ? e : launch_sha256_leaves(sb, w.leaf_off.as<uint64_t>() + (is0 - l0), n,
+                                         w.hashes.as<uint32_t>() + (is0 - l0) * 8, s);
+      }
     } else {
       e = e ? e : blocked("sha256_leaves launch", [&] {
         return launch_sha256_leaves(bytes_base, w.leaf_off.as<uint64_t>() + (ls0 - l0), ls1 - ls0,

@@ -133,3 +133,44 @@ def test_c4h_shape_trim_and_idle_release(small, engine, oracle):
     assert small.device_mem(0)[0] < grown
     got3 = small.signed_tx_verify(txs[:100], sigs[:100])  # and the context still verifies
     assert np.array_equal(got3[1], want[1][:100])
+
+
+def test_component_slices_in_pieces(small, engine, oracle):
+    """cordahip_txcomp_submit under the 64 MiB budget: the full encoder chain's leaf buffer
+    is capped at a tenth of the budget (6.7 MB, ~300 cash-issue transactions' bound), so
+    each id slice is encoded and hashed in pieces of whole transactions; ids, statuses and
+    first_bad_sig equal the default context's and the oracle's ids"""
+    from corda_amd import _lib
+    from corda_amd.corpus import cash_issue_items
+    rng = np.random.default_rng(61)
+    ntx = 3000
+    blob, items, _ = cash_issue_items(rng.integers(0, 256, (ntx, 32), dtype=np.uint8),
+                                      rng.integers(0, 256, (ntx, 32), dtype=np.uint8), bytes(range(32)),
+                                      rng.integers(1, 10**9, ntx), rng.integers(-2**63, 2**63 - 1, ntx))
+    it = items.reshape(-1).copy()
+    host_it = it.copy()
+    host_it["data"] += np.uint64(blob.ctypes.data)
+    hb, ho = _lib.kryo_encode_array(host_it)
+    leaves = [[hb[int(ho[5 * t + j]):int(ho[5 * t + j + 1])].tobytes() for j in range(5)] for t in range(ntx)]
+    ids_l, _ = engine.tx_ids(leaves)
+    for t in range(0, ntx, 499):  # the oracle's ids on a sample
+        want = ctypes.create_string_buffer(32)
+        lb = np.frombuffer(b"".join(leaves[t]), np.uint8).copy()
+        lo = np.zeros(6, np.uint64)
+        lo[1:] = np.cumsum([len(x) for x in leaves[t]])
+        assert oracle.oracle_tx_id(lb.ctypes.data, lo.ctypes.data, 5, want) == 0
+        assert want.raw == ids_l[t].tobytes()
+    sigs = []
+    for t in range(ntx):
+        pub, sg = _sign(oracle, hashlib.sha256(b"pc%d" % t).digest(), ids_l[t].tobytes())
+        if t % 13 == 5:
+            sg = sg[:7] + bytes([sg[7] ^ 2]) + sg[8:]
+        sigs.append([(ED, pub, sg)] * (1 + t % 3))
+    tio = np.arange(0, 5 * ntx + 1, 5, dtype=np.uint64)
+    want = engine.signed_txcomp_verify_arrays(blob, it, tio, sigs)
+    for _ in range(2):  # the first call on the small context runs the full chain
+        got = small.signed_txcomp_verify_arrays(blob, it, tio, sigs)
+        for a, b in zip(got, want):
+            assert np.array_equal(a, b)
+    assert np.array_equal(got[0][:ntx], ids_l[:ntx])
+    assert (got[1] == 1).sum() == len(range(5, ntx, 13))
