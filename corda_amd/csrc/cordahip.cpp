@@ -371,6 +371,40 @@ hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs
   return e;
 }
 
+// The Ed25519 section of a device signed-tx call (32-byte messages in HBM, on the
+// caller's stream s): chunks of CORDAHIP_DEVICE_ED_CHUNK signatures (default
+// 98,304 = 0.75 of a ladder round of 2 waves x 1,024 SIMDs x 64 lanes; 0: one
+// launch pair) alternate between s with workspace slot 0 and the device's s_ed2
+// with slot 1, the short remainder first. Every ladder wave takes about the same
+// time, so one launch over C4's 2.5 M signatures (19.07 rounds) ran 20 rounds, its
+// last with 7% of the CUs; alternating chunks let chunk k + 1's prep fill chunk k's
+// ladder tail, as the host pipelines do. Two streams hold two chunks, so a chunk
+// below half a round leaves CUs idle (2^15: C4 64.7 M sig/s). One box
+// (profiles/r06_device_ed_chunk_ab/): C4 93.4-94.5 with one launch pair, 95.1-96.4
+// at 2^17, 95.8-96.7 at 2^16, 97.0-97.7 at 98,304; C4 --device-encode 87.1-87.2,
+// 88.7-89.2, 89.3-89.4, 89.2-89.2.
+hipError_t ed_verify_device_chunks(Device& d, TxSet& S, const uint8_t* keys, const uint8_t* sigs, const uint8_t* msgs,
+                                   uint64_t n, uint8_t* status, hipStream_t s) {
+  static const uint64_t chunk = [] {
+    const char* v = getenv("CORDAHIP_DEVICE_ED_CHUNK");
+    return v ? (uint64_t)strtoull(v, nullptr, 10) / 64 * 64 : (uint64_t)98304;
+  }();
+  if (!chunk || n <= chunk || !d.s_ed2)
+    return ed_verify_enqueue(d, keys, sigs, msgs, 32, n, nullptr, status, nullptr, 0u, s, 0, nullptr);
+  hipError_t e = hipEventRecord(S.ed_fork, s);
+  e = e ? e : hipStreamWaitEvent(d.s_ed2, S.ed_fork, 0);
+  const uint64_t r = n % chunk;
+  uint64_t lo = 0;
+  for (int k = 0; lo < n && e == hipSuccess; k++) {
+    const uint64_t hi = lo + (k == 0 && r ? r : chunk);
+    e = ed_verify_enqueue(d, keys + lo * 32, sigs + lo * 64, msgs + lo * 32, 32, hi - lo, nullptr, status + lo,
+                          nullptr, 0u, k % 2 ? d.s_ed2 : s, k % 2, nullptr);
+    lo = hi;
+  }
+  e = e ? e : hipEventRecord(S.ed_join, d.s_ed2);
+  return e ? e : hipStreamWaitEvent(s, S.ed_join, 0);
+}
+
 // CORDAHIP_DEVICE_MEM_BUDGET (bytes, K/M/G suffixes; default 128 GiB, at most 90%
 // of the device): the workspaces it sizes -- Ed25519 slot 0 45% of it, slot 1 20%
 // (and half of slot 0 at most), ECDSA 15% -- each also capped by its r05 maximum
@@ -1476,7 +1510,7 @@ void free_device(Device& d) {
       b->release();
     if (S.kryo_usage) (void)hipHostFree(S.kryo_usage);
     S.kryo_usage = S.kryo_usage_dev = nullptr;
-    for (hipEvent_t* pe : {&S.tx_ev, &S.fork, &S.ids}) {
+    for (hipEvent_t* pe : {&S.tx_ev, &S.fork, &S.ids, &S.ed_fork, &S.ed_join}) {
       if (*pe) (void)hipEventDestroy(*pe);
       *pe = nullptr;
     }
@@ -1583,7 +1617,7 @@ static int init_impl(uint32_t device_mask, cordahip_ctx** out) {
       break;
     }
     for (TxSet& S : dev.set)
-      for (hipEvent_t* pe : {&S.tx_ev, &S.fork, &S.ids})
+      for (hipEvent_t* pe : {&S.tx_ev, &S.fork, &S.ids, &S.ed_fork, &S.ed_join})
         if (hipEventCreateWithFlags(pe, hipEventDisableTiming) != hipSuccess) rc = CORDAHIP_ERR_HIP;
     if (rc != CORDAHIP_SUCCESS) break;
     for (auto& tc : dev.ring)
@@ -1980,10 +2014,16 @@ int cordahip_signed_tx_verify_ed25519_device(cordahip_ctx* ctx, int device, cons
     return r ? r : launch_gather_txid(static_cast<const uint8_t*>(d_txid), static_cast<const uint64_t*>(d_tx_sig_off),
                                       ntx, w.msgs.as<uint8_t>(), s);
   };
-  if (nsig == 0) e = e ? e : join();
-  e = e ? e : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
-                                w.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status), nullptr,
-                                0u, s, 0, nsig ? &join : nullptr);
+  // unforked, the ids come first and the prep runs fused (its key and message halves
+  // as two launches cost ~0.6 ms more per 2.5 M signatures with nothing beside them)
+  if (nsig == 0 || !split) e = e ? e : join();
+  if (split)
+    e = e ? e : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
+                                  w.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status), nullptr,
+                                  0u, s, 0, nsig ? &join : nullptr);
+  else
+    e = e ? e : ed_verify_device_chunks(*d, S, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
+                                        w.msgs.as<uint8_t>(), nsig, static_cast<uint8_t*>(d_sig_status), s);
   e = e ? e : hipEventRecord(S.tx_ev, s);  // fences w.hashes / w.msgs for the next user
   e = e ? e : launch_tx_reduce(static_cast<uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off),
                                ntx, static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);
@@ -2112,10 +2152,15 @@ int cordahip_signed_txcomp_verify_ed25519_device(cordahip_ctx* ctx, int device, 
       return r ? r : launch_gather_txid(static_cast<const uint8_t*>(d_txid), static_cast<const uint64_t*>(d_tx_sig_off),
                                         ntx, w.msgs.as<uint8_t>(), s);
     };
-    if (nsig == 0) e = e ? e : join();
-    e = e ? e : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
-                                  w.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status), nullptr,
-                                  0u, s, 0, nsig ? &join : nullptr);
+    if (nsig == 0 || !split) e = e ? e : join();  // unforked: ids first, then the fused prep
+    if (split)
+      e = e ? e : ed_verify_enqueue(*d, static_cast<const uint8_t*>(d_keys), static_cast<const uint8_t*>(d_sigs),
+                                    w.msgs.as<uint8_t>(), 32, nsig, nullptr, static_cast<uint8_t*>(d_sig_status),
+                                    nullptr, 0u, s, 0, nsig ? &join : nullptr);
+    else
+      e = e ? e : ed_verify_device_chunks(*d, S, static_cast<const uint8_t*>(d_keys),
+                                          static_cast<const uint8_t*>(d_sigs), w.msgs.as<uint8_t>(), nsig,
+                                          static_cast<uint8_t*>(d_sig_status), s);
     e = e ? e : hipEventRecord(S.tx_ev, s);  // fences the set's buffers for the next user
     e = e ? e : launch_tx_reduce(static_cast<uint8_t*>(d_sig_status), static_cast<const uint64_t*>(d_tx_sig_off), ntx,
                                  static_cast<int64_t*>(d_first_bad), static_cast<uint8_t*>(d_tx_status), s);

@@ -870,8 +870,73 @@ __device__ inline void leaf_piece(const HashSrc& h, uint32_t p, uint64_t desc, u
   }
 }
 
+// The wave-uniform form of leaf_piece: every lane of the wave hashes a leaf of the
+// same template, so the template's constant copies, descriptors and symbols are read
+// through the scalar cache at one address per wave (constant address space: scalar
+// loads into SGPRs), only the payload windows are per-lane vector loads, and the
+// piece's control flow branches on scalars instead of exec masks.
+typedef const __attribute__((address_space(4))) uint8_t* TmplPtr;
+__device__ inline void leaf_piece_uniform(TmplPtr T, uint32_t len, const uint8_t* data, int64_t value, uint32_t p,
+                                          uint32_t* v) {
+  const uint32_t lo = 16 * p, last = min(15u, len - 1 - lo);
+  const uint64_t desc = reinterpret_cast<const __attribute__((address_space(4))) uint64_t*>(T + kOffDesc)[p + 1];
+  const uint32_t pm = (uint32_t)desc & 0xffff, kind = (uint32_t)(desc >> 16) & 3;
+  if (kind != kDescBytes) {
+    const __attribute__((address_space(4))) uint32_t* tv =
+        reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(T + kOffTb + 16 + lo);
+    v[0] = tv[0], v[1] = tv[1], v[2] = tv[2], v[3] = tv[3];
+    if (pm) {
+      uint32_t w[4];
+      load_window(data + (int32_t)(desc >> 32), __builtin_ctz(pm), 31 - __builtin_clz(pm), w);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t mk = byte_mask32((pm >> (4 * i)) & 15);
+        v[i] = (v[i] & ~mk) | (w[i] & mk);
+      }
+    }
+    return;
+  }
+  const __attribute__((address_space(4))) uint32_t* sp =
+      reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(T + 4 * (size_t)lo);
+  uint32_t sy[16];
+#pragma unroll
+  for (int t = 0; t < 16; t++) sy[t] = sp[t];
+  uint32_t pb[16];
+#pragma unroll
+  for (uint32_t t = 0; t < 16; t++)
+    pb[t] = (t <= last && (sy[t] & kryo::kSymTypeMask) == kryo::kSymPayload)
+                ? data[(sy[t] >> 8) & (kryo::kMaxPayloadOff - 1)] : 0u;
+#pragma unroll
+  for (int i = 0; i < 4; i++) v[i] = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < 16; t++) {
+    const uint32_t x = sy[t], ty = x & kryo::kSymTypeMask;
+    uint32_t b = ty == kryo::kSymPayload ? (pb[t] | ((x & kryo::kSymOr80) ? 0x80u : 0u))
+                 : ty == kryo::kSymConst ? (x & 0xffu) : (uint32_t)kryo::sym_byte(x, nullptr, value);
+    v[t >> 2] |= (t <= last ? b : 0u) << (8 * (t & 3));
+  }
+}
+
+// kryo_hash's blocks: 256 items of ONE kind (records of `group` items: 256
+// consecutive records' component `kind`), the `group` blocks of a tile of 256
+// records on one XCD (blocks go round-robin over the 8 XCDs, so block b's tile is
+// chosen among those of XCD b % 8: the records' items and payload lines are read
+// into one L2). Ungrouped batches: 256 consecutive items per block. Returns n past
+// the last item.
+__device__ inline uint64_t hash_item_of(uint32_t b, uint32_t t, uint64_t n, uint32_t group) {
+  if (group <= 1 || group > 16 || n % group) return (uint64_t)b * 256 + t < n ? (uint64_t)b * 256 + t : n;
+  const uint32_t q = b / 8, kind = q % group;
+  const uint64_t tile = (uint64_t)(q / group) * 8 + b % 8, rec = tile * 256 + t;
+  return rec < n / group ? rec * group + kind : n;
+}
+inline uint32_t hash_blocks(uint64_t n, uint32_t group) {
+  if (!grouped(n, group)) return (uint32_t)((n + 255) / 256);
+  const uint64_t tiles = (n / group + 255) / 256;
+  return (uint32_t)((tiles + 7) / 8 * 8 * group);
+}
+
 template <int kMinWaves>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kMinWaves, 8)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves, 8)))
 kryo_hash_kernel(ItemSrc items, uint64_t n, uint32_t group,
                                                          const uint32_t* __restrict__ item_slot,
                                                          const uint32_t* __restrict__ slot_map,
@@ -880,9 +945,46 @@ kryo_hash_kernel(ItemSrc items, uint64_t n, uint32_t group,
                                                          const uint8_t* __restrict__ status,
                                                          uint32_t* __restrict__ hashes /* [n][8] BE words */) {
   kryo_priority();
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t i = item_of(j, n, group);
-  if (i >= n) return;
+  // The block's items grouped by template before any lane hashes: a wave whose
+  // lanes hold leaves of one template assembles its blocks on the scalar path, one
+  // of several templates (a cash state's quantity and nonce varints give 2-3 shapes
+  // per 64 transactions, each shifting every later byte) diverges at every piece.
+  // Up to kGroups rounds each collect the lanes of the smallest remaining key
+  // (the slot; status != 0 and past-the-end lanes last), in lane order; the rest
+  // keep theirs.
+  constexpr int kGroups = 8;
+  __shared__ uint8_t order[256];
+  __shared__ uint32_t s_min, s_cnt[4];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t i0 = hash_item_of(blockIdx.x, tid, n, group);
+  const uint32_t key = i0 >= n ? 0xffffffffu : status[i0] != 0 ? 0xfffffffeu : item_slot[i0];
+  bool placed = i0 >= n;
+  uint32_t base = 0;
+  for (int r = 0; r <= kGroups; r++) {
+    if (tid == 0) s_min = 0xffffffffu;
+    __syncthreads();
+    if (!placed && r < kGroups) atomicMin(&s_min, key);
+    __syncthreads();
+    const uint32_t cur = s_min;
+    const bool pred = !placed && (r == kGroups || key == cur);
+    const uint64_t bal = __ballot(pred);
+    if (lane == 0) s_cnt[wv] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t off = base, tot = 0;
+    for (uint32_t w = 0; w < 4; w++) {
+      off += w < wv ? s_cnt[w] : 0u;
+      tot += s_cnt[w];
+    }
+    if (pred) {
+      order[off + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = (uint8_t)tid;
+      placed = true;
+    }
+    base += tot;
+    __syncthreads();
+    if (r < kGroups && cur == 0xffffffffu) break;  // every lane with an item placed
+  }
+  if (tid >= base) return;
+  const uint64_t i = hash_item_of(blockIdx.x, order[tid], n, group);
   HashSrc h;
   h.kind = 2;
   if (status[i] == 0) {
@@ -899,7 +1001,42 @@ kryo_hash_kernel(ItemSrc items, uint64_t n, uint32_t group,
     }
   }
   uint32_t st[8];
-  if (h.kind == 2) {
+  const uint64_t tp = h.kind == 0 ? (uint64_t)(uintptr_t)h.tmpl : 0;
+  const uint64_t tp0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tp >> 32)) << 32) |
+                       __builtin_amdgcn_readfirstlane((uint32_t)tp);
+  if (__all(tp != 0 && tp == tp0)) {  // one template in the whole wave: the scalar path
+    TmplPtr T = (TmplPtr)(uintptr_t)tp0;
+    const uint32_t len = __builtin_amdgcn_readfirstlane(h.len);  // one shape: one size
+    const __attribute__((address_space(4))) uint32_t* mid =
+        reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(T + kOffMid);
+    const uint32_t b0 = mid[0];
+    sha256_init(st);
+    if (b0) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) st[k] = mid[1 + k];
+    }
+    const uint32_t nb = (len + 9 + 63) / 64;
+    for (uint32_t b = b0; b < nb; b++) {
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t p = 4 * b + q;
+        uint32_t v[4] = {0, 0, 0, 0};
+        if (16 * p < len) leaf_piece_uniform(T, len, h.data, h.value, p, v);
+        if (len >= 16 * p && len < 16 * p + 16) {  // the padding's first byte
+          const uint32_t t = len - 16 * p;
+          v[t >> 2] |= 0x80u << (8 * (t & 3));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) w[4 * q + k] = bswap32(v[k]);
+      }
+      if (b == nb - 1) {
+        w[14] = len >> 29;
+        w[15] = len << 3;
+      }
+      sha256_block(st, w);
+    }
+  } else if (h.kind == 2) {
 #pragma unroll
     for (int k = 0; k < 8; k++) st[k] = 0;
   } else {
@@ -1073,7 +1210,8 @@ hipError_t launch_kryo_hash(const cordahip_kryo_item* d_items, const uint8_t* da
     const char* v = getenv("CORDAHIP_KRYO_HASH_WAVES");
     return v ? atoi(v) : 5;
   }();
-  const dim3 grid((uint32_t)((item_threads(n, group) + sb - 1) / sb)), blk(sb);
+  const dim3 grid(hash_blocks(n, group)), blk(256);
+  (void)sb;
   if (waves >= 6)
     hipLaunchKernelGGL(kryo_hash_kernel<6>, grid, blk, 0, s, items, n, g, item_slot, k.slot_map, k.arena, sizes, status,
                        hashes);

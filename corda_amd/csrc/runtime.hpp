@@ -237,6 +237,9 @@ struct TxSet {
   // the device signed-tx calls' fork / join: the id chain runs on the id stream beside
   // the key half of the Ed25519 prep on the caller's stream
   hipEvent_t fork = nullptr, ids = nullptr;
+  // their chunked Ed25519 section (ed_verify_device_chunks): s_ed2 forks off the
+  // caller's stream and joins it again
+  hipEvent_t ed_fork = nullptr, ed_join = nullptr;
 };
 constexpr int kTxSets = 2;
 
