@@ -190,7 +190,7 @@ struct PieceInfo {
 };
 
 // One device's input shard [lo, hi) of a generic batch, streamed in chunks
-// through kPackStages BatchStages. Per chunk, on the host pool: (1) classify
+// through kPackStages BatchStages (signed-tx signature chunks: kTxStages). Per chunk, on the host pool: (1) classify
 // every lane (direct statuses written now; Ed25519 lanes grouped by message
 // length; ECDSA lanes) into per-lane class codes and per-piece counts, (2) pack
 // every lane straight into its row: Ed25519 rows group after group (each
@@ -273,8 +273,9 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_ba
   hipError_t e = hipSuccess;
   int rc = CORDAHIP_SUCCESS;
   const double t_start = tracing() ? now_ms() : 0;
+  const int nst = dev ? kTxStages : kPackStages;  // signed-tx chunks: more of them in flight
   for (size_t k = 0; k < chunks.size() && e == hipSuccess && rc == CORDAHIP_SUCCESS; k++) {
-    BatchStage& st = set.pb[k % kPackStages];
+    BatchStage& st = set.pb[k % nst];
     const double t0 = tracing() ? now_ms() : 0;
     e = finish(st);
     if (e != hipSuccess) break;
@@ -541,7 +542,7 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_ba
   // stream it used, so waiting for them (not for the shared streams, which may
   // already carry the next call's work) drains this call. After an error the
   // streams themselves are drained, so no queued work outlives the call.
-  for (int k = 0; k < kPackStages; k++) {
+  for (int k = 0; k < nst; k++) {
     if (e == hipSuccess && rc == CORDAHIP_SUCCESS) e = finish(set.pb[k]);
     set.pb[k].pending = false;
   }

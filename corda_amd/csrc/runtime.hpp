@@ -198,6 +198,14 @@ struct PackStage {
   uint64_t tag0 = 0, tag1 = 0, tag2 = 0;  // which chunk is in flight (pipeline-defined)
 };
 constexpr int kPackStages = 3;
+// Signed-tx batches keep more of their small (2^17-signature) chunks in flight:
+// a chunk's prep waits for its id slice, and with three stages the pipeline could
+// not run far enough ahead of the id chain -- c4h --components at two calls in
+// flight 79.4-82.5 M sig/s with 3 stages, 84.7-85.7 with 4, 86.3-87.1 with 5,
+// 86.4-87.6 with 6; c4h 90.3-91.5 / 90.6-91.5 / 89.3-92.6 / 92.4-92.5
+// (profiles/r06_pack_stages_ab/). Generic batches (4 M-lane chunks, ~0.55 GB of
+// pinned rows each) keep three.
+constexpr int kTxStages = 6;
 
 // one stage of the generic-batch pipeline (host_batch.cpp): a chunk of the
 // batch's lanes, classified and packed into BOTH sections' pinned buffers
@@ -229,7 +237,7 @@ struct TxWork {  // device buffers of the transaction paths (grow-only)
 struct TxSet {
   TxWork tx;
   hipEvent_t tx_ev = nullptr;
-  BatchStage pb[kPackStages];  // generic CSR batches and the signed-tx signature chunks
+  BatchStage pb[kTxStages];  // generic CSR batches (the first kPackStages) and the signed-tx signature chunks
   // component calls: the encoder's usage counters after this set's last call,
   // host-mapped: [templates in the arena, table slots in use, misses of set 0, of set 1]
   uint32_t* kryo_usage = nullptr;
