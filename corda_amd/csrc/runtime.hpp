@@ -205,7 +205,10 @@ constexpr int kPackStages = 3;
 // 86.4-87.6 with 6; c4h 90.3-91.5 / 90.6-91.5 / 89.3-92.6 / 92.4-92.5
 // (profiles/r06_pack_stages_ab/). Generic batches (4 M-lane chunks, ~0.55 GB of
 // pinned rows each) keep three.
-constexpr int kTxStages = 6;
+#ifndef CORDAHIP_TX_STAGES
+#define CORDAHIP_TX_STAGES 6  // A/B builds: -DCORDAHIP_TX_STAGES=N
+#endif
+constexpr int kTxStages = CORDAHIP_TX_STAGES;
 
 // one stage of the generic-batch pipeline (host_batch.cpp): a chunk of the
 // batch's lanes, classified and packed into BOTH sections' pinned buffers
