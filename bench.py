@@ -1211,8 +1211,10 @@ def main():
                 # VALU busy from the same PMC file: SQ_INSTS_VALU x the measured ~4 SIMD-cycles per
                 # (VOP3-dominated) wave instruction / SIMD-cycles (SQ_ACTIVE_INST_VALU
                 # counts issues on gfx950, so the issue fraction alone is the _issue figure)
-                valu_busy = {"valu_busy": dv["valu_busy_est_4cyc"], "valu_issue_frac": dv.get("valu_busy_direct"),
+                valu_busy = {"valu_busy": dv["valu_busy_est_4cyc"], "valu_busy_pmc_run": dv["valu_busy_est_4cyc"],
+                             "valu_issue_frac": dv.get("valu_busy_direct"),
                              "valu_insts_per_unit": dv.get("valu_lane_insts_per_lane"),
+                             "valu_wave_insts_per_unit": dv.get("valu_wave_insts_per_lane"),
                              "source": "profiles/%s total.derived (the verification kernels of one step)" % wl.pmc}
             per_unit = pmc.get("hbm_bytes_per_unit")
             traffic = per_unit * wl.units if per_unit else None
@@ -1289,6 +1291,17 @@ def main():
                 out["clock_ghz"] = clock["clock_ghz"]
                 # per-GPU verifications per 10^6 shader cycles: comparable across boxes
                 out["verifs_per_mclk"] = value / world / (clock["clock_ghz"] * 1e3)
+                vb = out.get("valu_busy")
+                if vb and vb.get("valu_wave_insts_per_unit"):
+                    # this run's VALU busy: the PMC file's wave instructions per unit x this step's
+                    # units x ~4 SIMD-cycles each, over 1,024 SIMDs x this step's kernel time x the
+                    # clock sampled under it. Under --pmc rocprofv3 runs dispatches one at a time, so
+                    # the file's own figure (valu_busy_pmc_run) understates lines whose kernels
+                    # overlap on several streams (the chunked and pipelined ones)
+                    vb["valu_busy"] = (vb["valu_wave_insts_per_unit"] * wl.units * 4 /
+                                       (1024 * kernel_ms * 1e-3 * clock["clock_ghz"] * 1e9))
+                    vb["valu_busy_basis"] = ("PMC wave instructions per unit x units x 4 SIMD-cycles / "
+                                             "(1024 SIMDs x kernel_ms x clock_ghz) of this run")
         if world == 1 and not args.no_cpu_baseline and not stub:
             # bounded samples sized for ~10 s of 16-thread CPU work each (C1: its whole 2^20 set)
             sample = args.cpu_sample or {"c1": 1 << 20, "c2": 1 << 22, "c3": 1 << 20, "c4": 1 << 20, "c5": 1 << 21,
