@@ -2,7 +2,11 @@
 >= 1e8 signature verdicts through cordahip_tx_submit (leaf bytes; the Ed25519
 prep's key half ahead of the ids) and cordahip_txcomp_submit (Kryo components;
 ids from the encoder's templates-only chain from the second call on), each
-batch's two tickets outstanding together on one device (the overlapped calls),
+batch's two tickets outstanding together on one device (the overlapped calls);
+with --device also through the device-resident calls on the same batch,
+cordahip_signed_txcomp_verify_ed25519_device (the device hash chain: leaf
+hashes straight from the encoder) and cordahip_signed_tx_verify_ed25519_device
+(leaf bytes in HBM), both with the Ed25519 section in alternating chunks;
 every output checked against the CPU oracle (oracle/c):
 
   * every transaction id against oracle_tx_id over the host encoder's leaves
@@ -59,7 +63,39 @@ def reduce_rule(sig_status, tso):
     return st, fb
 
 
-def one_batch(eng, orc, b, seed, ntx, threads):
+def device_calls(eng, blob, items, lb, lo, tlo, tso, K, S):
+    """the batch through the two device-resident signed-tx calls (inputs copied to HBM
+    first, outside the checks); returns {name: (ids, tx_status, first_bad, sig_status)}"""
+    import torch
+    dev = torch.device("cuda:0")
+    ntx, ns = len(tlo) - 1, len(K)
+    d_so = torch.from_numpy(tso.astype(np.int64)).to(dev)
+    d_tlo = torch.from_numpy(tlo.astype(np.int64)).to(dev)
+    k = torch.from_numpy(K).to(dev)
+    s = torch.from_numpy(S).to(dev)
+    out = {}
+    for name in ("device_txcomp", "device_leaf"):
+        txid = torch.zeros((ntx, 32), dtype=torch.uint8, device=dev)
+        st = torch.zeros(ntx, dtype=torch.uint8, device=dev)
+        fb = torch.zeros(ntx, dtype=torch.int64, device=dev)
+        sst = torch.zeros(ns, dtype=torch.uint8, device=dev)
+        if name == "device_txcomp":
+            d_items = torch.from_numpy(np.ascontiguousarray(items).view(np.uint8).copy()).to(dev)
+            d_blob = torch.from_numpy(np.ascontiguousarray(blob, dtype=np.uint8)).to(dev)
+            eng.signed_txcomp_verify_ed25519_device(d_items, len(items), d_blob, d_tlo, d_so, k, s, txid, st, fb, sst,
+                                                    group=5)
+            del d_items, d_blob
+        else:
+            d_lb = torch.from_numpy(lb).to(dev)
+            d_lo = torch.from_numpy(lo.astype(np.int64)).to(dev)
+            eng.signed_tx_verify_ed25519_device(d_lb, d_lo, d_tlo, d_so, k, s, txid, st, fb, sst)
+            del d_lb, d_lo
+        torch.cuda.synchronize()
+        out[name] = (txid.cpu().numpy(), st.cpu().numpy(), sst.cpu().numpy(), fb.cpu().numpy())
+    return out
+
+
+def one_batch(eng, orc, b, seed, ntx, threads, device=False):
     import torch
     from corda_amd import _lib
     from corda_amd._lib import check, lib
@@ -143,8 +179,12 @@ def one_batch(eng, orc, b, seed, ntx, threads):
     rec = {"batch": b, "seed": seed, "txs": ntx, "sigs": ns, "bad_txs": int(bad_tx.size), "bad_sigs": int(bad_sig.size),
            "oracle_vs_construction_mismatches": int((want_sig != construction).sum()),
            "oracle_tx_no_leaves": int((st_o != 0).sum()), "oracle_s": round(t_oracle, 2), "gpu_calls_s": round(t_gpu, 3)}
-    for name, (txid, txst, sst, fb) in zip(("tx_submit", "txcomp_submit"), outs):
-        txid, txst, sst, fb = (x.numpy() for x in (txid, txst, sst, fb))
+    results = [(name, tuple(x.numpy() for x in o)) for name, o in zip(("tx_submit", "txcomp_submit"), outs)]
+    if device:
+        t0 = time.time()
+        results += list(device_calls(eng, blob, items, lb, lo, tlo, tso, K, S).items())
+        rec["device_calls_s"] = round(time.time() - t0, 3)
+    for name, (txid, txst, sst, fb) in results:
         rec[name] = {"id_mismatches": int((txid != ids).any(axis=1).sum()),
                      "sig_status_mismatches": int((sst != want_sig).sum()),
                      "tx_status_mismatches": int((txst != want_st).sum()),
@@ -161,6 +201,7 @@ def main():
     ap.add_argument("--first", type=int, default=0)
     ap.add_argument("--log", default=None, help="append one JSON line per batch")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--device", action="store_true", help="also the two device-resident signed-tx calls")
     args = ap.parse_args()
     from conftest import load_oracle
     from corda_amd.engine import Engine
@@ -171,12 +212,12 @@ def main():
     with Engine(1) as eng:
         for k in range(args.batches):
             b = args.first + k
-            rec = one_batch(eng, orc, b, 0xA6EE0000 + b, args.txs, args.threads)
+            rec = one_batch(eng, orc, b, 0xA6EE0000 + b, args.txs, args.threads, args.device)
             tot["batches"] += 1
             tot["txs"] += rec["txs"]
             tot["sigs"] += rec["sigs"]
             tot["oracle_vs_construction_mismatches"] += rec["oracle_vs_construction_mismatches"]
-            for name in ("tx_submit", "txcomp_submit"):
+            for name in [x for x in ("tx_submit", "txcomp_submit", "device_txcomp", "device_leaf") if x in rec]:
                 r = rec[name]
                 tot["verdicts_checked"] += rec["sigs"]
                 tot["id_checks"] += rec["txs"]
@@ -187,9 +228,11 @@ def main():
                 with open(args.log, "a") as f:
                     f.write(json.dumps(rec) + "\n")
     tot["wall_s"] = round(time.time() - t_start, 1)
-    tot["what"] = ("cordahip_tx_submit + cordahip_txcomp_submit (two tickets outstanding per batch on one device), "
+    tot["what"] = ("cordahip_tx_submit + cordahip_txcomp_submit (two tickets outstanding per batch on one device)%s, "
                    "every id, signature status, tx status and first_bad_sig against oracle/c; signature statuses also "
-                   "against the construction")
+                   "against the construction" % (
+                       " + cordahip_signed_txcomp_verify_ed25519_device + cordahip_signed_tx_verify_ed25519_device"
+                       if args.device else ""))
     print(json.dumps(tot), flush=True)
     if args.out:
         with open(args.out, "w") as f:
