@@ -690,22 +690,50 @@ def _csr_rows(rows, lens):
 
 
 class _HostSigBatch:
-    """A cordahip_sig_batch over pinned host CSR arrays (scheme, key/sig/msg blobs + offsets)."""
+    """A cordahip_sig_batch over pinned host CSR arrays (scheme, key/sig/msg blobs + offsets).
+    inflight K > 1: up to K cordahip_sig_submit tickets outstanding (a JVM's verifier
+    workers or fibers submitting consecutive batches), each slot with its own status and
+    verdict arrays; run() submits one and completes the oldest once K are out."""
 
-    def __init__(self, scheme, kb, ko, sb, so, mb, mo):
+    def __init__(self, scheme, kb, ko, sb, so, mb, mo, inflight=1):
         from corda_amd import _lib
         n = len(scheme)
         self.t = [_pinned(x) for x in (scheme, kb, ko, sb, so, mb, mo)]
-        self.status = _pinned(np.zeros(n, np.uint8))
-        self.verdict = _pinned(np.zeros((n + 63) // 64, np.uint64))
         p = [x.data_ptr() for x in self.t]
-        self.b = _lib.SigBatch(n, *p, self.status.data_ptr(), self.verdict.data_ptr(), 0,
-                               self.t[1].numel(), self.t[3].numel(), self.t[5].numel())
+        self.inflight = max(1, inflight)
+        self.outs, self.bs = [], []
+        for _ in range(self.inflight):
+            st, vd = _pinned(np.zeros(n, np.uint8)), _pinned(np.zeros((n + 63) // 64, np.uint64))
+            self.outs.append((st, vd))
+            self.bs.append(_lib.SigBatch(n, *p, st.data_ptr(), vd.data_ptr(), 0,
+                                         self.t[1].numel(), self.t[3].numel(), self.t[5].numel()))
+        self.status, self.verdict = self.outs[0]
+        self.b = self.bs[0]
+        self.pending = []  # (ticket, slot), oldest first
 
     def run(self, eng):
         import ctypes
         from corda_amd._lib import check, lib
-        check(lib().cordahip_sig_verify(eng.ctx, ctypes.byref(self.b)), "cordahip_sig_verify")
+        if self.inflight == 1:
+            check(lib().cordahip_sig_verify(eng.ctx, ctypes.byref(self.b)), "cordahip_sig_verify")
+            return
+        if len(self.pending) >= self.inflight:
+            self._complete(eng)
+        busy = {k for _, k in self.pending}
+        slot = next(k for k in range(self.inflight) if k not in busy)
+        t = ctypes.c_uint64()
+        check(lib().cordahip_sig_submit(eng.ctx, ctypes.byref(self.bs[slot]), ctypes.byref(t)), "cordahip_sig_submit")
+        self.pending.append((t.value, slot))
+
+    def _complete(self, eng):
+        from corda_amd._lib import check, lib
+        t, slot = self.pending.pop(0)
+        check(lib().cordahip_wait(eng.ctx, t, -1), "cordahip_wait")
+        self.status, self.verdict = self.outs[slot]  # the last completed call's outputs
+
+    def drain(self, eng):
+        while self.pending:
+            self._complete(eng)
 
 
 class C2H(C2):
@@ -724,13 +752,20 @@ class C2H(C2):
         k, s, m = (x.cpu().numpy() for x in (self.pubs, self.sigs, self.msgs))
         ar = np.arange(n + 1, dtype=np.uint64)
         self.hb = _HostSigBatch(np.full(n, 4, np.uint8), k.reshape(-1), ar * 32, s.reshape(-1), ar * 64,
-                                m.reshape(-1), ar * 32)
+                                m.reshape(-1), ar * 32, inflight=getattr(args, "inflight", 1) or 1)
         self.workload = ("C2 via the JVM boundary: cordahip_sig_verify over a 2^%d-lane Ed25519 CSR batch in pinned "
                          "host memory (PCIe and host packing included), 1%% corrupted" % args.batch_log2)
-        self.config = dict(self.config, boundary="cordahip_sig_verify", host_memory="pinned CSR")
+        self.config = dict(self.config, boundary="cordahip_sig_verify", host_memory="pinned CSR",
+                           inflight=self.hb.inflight)
+        if self.hb.inflight > 1:
+            self.workload += ("; up to %d cordahip_sig_submit calls outstanding (the timed region ends when every "
+                              "call it submitted has completed)" % self.hb.inflight)
 
     def step(self):
         self.hb.run(self.eng)
+
+    def drain(self):
+        self.hb.drain(self.eng)
 
     def check(self):
         import torch
@@ -769,13 +804,21 @@ class C3H(C3):
         kb, ko = _csr_rows(self.keys.cpu().numpy(), self.key_len.cpu().numpy())
         sb, so = _csr_rows(self.sigs.cpu().numpy(), self.sig_len.cpu().numpy())
         ar = np.arange(n + 1, dtype=np.uint64)
-        self.hb = _HostSigBatch(self.scheme.cpu().numpy(), kb, ko, sb, so, self.msgs.cpu().numpy().reshape(-1), ar * 32)
+        self.hb = _HostSigBatch(self.scheme.cpu().numpy(), kb, ko, sb, so, self.msgs.cpu().numpy().reshape(-1), ar * 32,
+                                inflight=getattr(args, "inflight", 1) or 1)
         self.workload = ("C3 via the JVM boundary: cordahip_sig_verify over a 2^%d-lane mixed secp256k1 / P-256 CSR "
                          "batch in pinned host memory (PCIe and host packing included), 1%% corrupted" % args.batch_log2)
-        self.config = dict(self.config, boundary="cordahip_sig_verify", host_memory="pinned CSR")
+        self.config = dict(self.config, boundary="cordahip_sig_verify", host_memory="pinned CSR",
+                           inflight=self.hb.inflight)
+        if self.hb.inflight > 1:
+            self.workload += ("; up to %d cordahip_sig_submit calls outstanding (the timed region ends when every "
+                              "call it submitted has completed)" % self.hb.inflight)
 
     def step(self):
         self.hb.run(self.eng)
+
+    def drain(self):
+        self.hb.drain(self.eng)
 
     def check(self):
         self.status = self.hb.status
@@ -1057,7 +1100,7 @@ def parse_args(argv=None):
                     help="c4: native leaves encoded on the GPU every step from the components in HBM "
                          "(cordahip_kryo_encode_device; implies --native-leaves)")
     ap.add_argument("--inflight", type=int, default=1,
-                    help="c4h: calls outstanding at once (consecutive batches overlap on the device)")
+                    help="c4h, c2h, c3h: calls outstanding at once (consecutive batches overlap on the device)")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock sampling step")
