@@ -108,12 +108,17 @@ from corda_amd.engine import Engine
 from test_gpu_host_batch import make_batch, oracle_status
 orc = load_oracle()
 rows = make_batch(orc, n=3001, seed=9)
+rows2 = make_batch(orc, n=2500, seed=10)
 want = oracle_status(orc, rows, False)
+want2 = oracle_status(orc, rows2, False)
 with Engine(1) as eng:
     st, _ = eng.verify_batch(*zip(*rows))
-    t = eng.verify_batch(*zip(*rows), async_=True)   # the ticketed form, same pipeline
-    st2, _ = t.wait()
-bad = [i for i, (a, b, w) in enumerate(zip(st, st2, want)) if int(a) != w or int(b) != w]
+    # the ticketed form, three calls outstanding at once (two transaction sets per
+    # device: the third waits for a set; chunks of the first two interleave)
+    tks = [eng.verify_batch(*zip(*r), async_=True) for r in (rows, rows2, rows)]
+    st2, st3, st4 = (t.wait()[0] for t in tks)
+bad = [i for i, (a, b, c, w) in enumerate(zip(st, st2, st4, want)) if int(a) != w or int(b) != w or int(c) != w]
+bad += [("b2", i) for i, (a, w) in enumerate(zip(st3, want2)) if int(a) != w]
 print(json.dumps({"n": len(rows), "bad": bad[:10]}))
 sys.exit(1 if bad else 0)
 """
