@@ -224,6 +224,9 @@ hipError_t ensure_streams(Device& d) {
   d.s_ed = x;
   d.s_ed2 = x2;
   d.s_ec = y;
+  // generic batches' alternate ECDSA chunks run on the id-copy stream, idle in those
+  // batches (no sixth hardware queue)
+  d.s_ec2 = z;
   d.s_idcopy = z;
   d.s_copy = c;
   return hipSuccess;
@@ -304,14 +307,16 @@ hipError_t kryo_fixed_ensure(Device& d) {
 }
 
 // Enqueue ECDSA verification of n slot-layout lanes on stream s (device current,
-// d.ec_mu held): the shared work buffers are reused only after their previous
+// d.ec_mu[slot] held): the slot's work buffers are reused only after their previous
 // user's kernels (on whatever stream) have finished.
 hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
                              const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs, const uint64_t* msg_off,
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
-                             unsigned long long* verdict, uint32_t flags, hipStream_t s) {
-  EcWork& w = d.ec;
-  const uint64_t ws_slots = d.ec_ws_slots;  // the budget's ECDSA share (cordahip_init)
+                             unsigned long long* verdict, uint32_t flags, hipStream_t s, int slot) {
+  EcWork& w = d.ec[slot];
+  // the budget's ECDSA share (cordahip_init); slot 1 serves the host pipelines'
+  // alternate chunks and holds at most half of slot 0
+  const uint64_t ws_slots = slot ? std::max<uint64_t>(64, d.ec_ws_slots / 2 / 64 * 64) : d.ec_ws_slots;
   const uint64_t slots = std::min<uint64_t>(ws_slots, (std::max<uint64_t>(n, 1) + 63) / 64 * 64);
   if (w.ws.cap < slots * ecdsa_ws_slot_bytes() || w.perm.cap < std::max<uint64_t>(n, 1) * 4) {
     hipError_t e = w.ev ? hipEventSynchronize(w.ev) : hipSuccess;  // a smaller buffer may still be in use
@@ -437,19 +442,21 @@ void device_budget(Device& d) {  // device current
 
 // Free an idle device's grow-only buffers (the idle release, cordahip_trim): both
 // buffer sets and every lock that guards a buffer, in an order every path keeps
-// (sets, then kryo_mu, stream_mu, ped_mu, ed_mu, ec_mu); the events that fence
+// (sets, then kryo_mu, stream_mu, ped_mu, ed_mu, ec_mu, each slot in order); the events that fence
 // device-path users (kernels on caller streams) synchronised first. The fixed
 // tables and the encoder's shape table stay (derived data, 18 MB).
 void trim_device(Device& d) {
   SetLease l0(d, 0, true), l1(d, 1, true);
   std::lock_guard<std::mutex> gk(d.kryo_mu), gs(d.stream_mu), gp(d.ped_mu), ge0(d.ed_mu[0]), ge1(d.ed_mu[1]),
-      gc(d.ec_mu);
+      gc0(d.ec_mu[0]), gc1(d.ec_mu[1]);
   if (hipSetDevice(d.id) != hipSuccess) return;
-  for (hipEvent_t ev : {d.ed_ev[0], d.ed_ev[1], d.ec.ev, d.kryo_ev, d.set[0].tx_ev, d.set[1].tx_ev})
+  for (hipEvent_t ev : {d.ed_ev[0], d.ed_ev[1], d.ec[0].ev, d.ec[1].ev, d.kryo_ev, d.set[0].tx_ev, d.set[1].tx_ev})
     if (ev) (void)hipEventSynchronize(ev);
   for (auto& w : d.ed_ws) w.release();
-  d.ec.ws.release();
-  d.ec.perm.release();
+  for (EcWork& w : d.ec) {
+    w.ws.release();
+    w.perm.release();
+  }
   for (TxSet& S : d.set) {
     TxWork& w = S.tx;
     for (DevBuf* b : {&w.leaf_bytes, &w.leaf_off, &w.tx_leaf_off, &w.hashes, &w.txid, &w.tx_status, &w.tx_sig_off,
@@ -1381,7 +1388,7 @@ int stream_shard(Device& d, const cordahip_stream_batch* b, uint64_t e0, uint64_
     e = e ? e : hipEventRecord(st.ed_done, es);
     e = e ? e : hipStreamWaitEvent(xs, st.ec_copied, 0);
     if (mc && e == hipSuccess) {
-      std::lock_guard<std::mutex> ge(d.ec_mu);
+      std::lock_guard<std::mutex> ge(d.ec_mu[0]);
       e = ec_verify_enqueue(d, st.ec_scheme.as<uint8_t>(), st.ec_keys.as<uint8_t>(), st.ec_key_len.as<uint8_t>(),
                             st.ec_sigs.as<uint8_t>(), st.ec_sig_len.as<uint8_t>(), st.ec_msgs.as<uint8_t>(), nullptr,
                             (uint32_t)cml, mc, nullptr, st.ec_status.as<uint8_t>(), nullptr, 0u, xs);
@@ -1522,15 +1529,15 @@ void free_device(Device& d) {
     for (hipEvent_t ev : {st.ed_copied, st.ec_copied, st.ed_done, st.ec_done})
       if (ev) (void)hipEventDestroy(ev);
   }
-  for (hipStream_t ss : {d.s_copy, d.s_ed, d.s_ec, d.s_idcopy, d.s_ed2})
+  for (hipStream_t ss : {d.s_copy, d.s_ed, d.s_ec, d.s_idcopy, d.s_ed2})  // s_ec2 is s_idcopy
     if (ss) (void)hipStreamDestroy(ss);
-  for (DevBuf* b : {&d.ec.counters, &d.ec.perm, &d.ec.ws, &d.kryo_sizes, &d.kryo_temp, &d.kryo_ws, &d.kryo_fixed,
-                    &d.kryo_items})
+  for (DevBuf* b : {&d.ec[0].counters, &d.ec[0].perm, &d.ec[0].ws, &d.ec[1].counters, &d.ec[1].perm, &d.ec[1].ws,
+                    &d.kryo_sizes, &d.kryo_temp, &d.kryo_ws, &d.kryo_fixed, &d.kryo_items})
     b->release();
   for (auto& w : d.ed_ws) w.release();
   if (d.kryo_usage) (void)hipHostFree(d.kryo_usage);
   d.kryo_usage = d.kryo_usage_dev = nullptr;
-  for (hipEvent_t ev : {d.ec.ev, d.ed_ev[0], d.ed_ev[1], d.kryo_ev})
+  for (hipEvent_t ev : {d.ec[0].ev, d.ec[1].ev, d.ed_ev[0], d.ed_ev[1], d.kryo_ev})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& tc : d.ring)
     for (hipEvent_t ev : {tc.a, tc.b})
@@ -1882,7 +1889,7 @@ int cordahip_ecdsa_verify_device(cordahip_ctx* ctx, int device, const void* d_sc
   if (!d || (n && (!d_scheme || !d_keys || !d_key_len || !d_sigs || !d_sig_len || !d_status || (msg_len && !d_msgs))))
     return CORDAHIP_ERR_INVALID_ARG;
   const Activity act(*d);
-  std::lock_guard<std::mutex> g(d->ec_mu);
+  std::lock_guard<std::mutex> g(d->ec_mu[0]);
   if (hipSetDevice(d->id) != hipSuccess) return CORDAHIP_ERR_HIP;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   TimedCall* tc = timed_begin(*d, s);

@@ -274,6 +274,8 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_ba
   int rc = CORDAHIP_SUCCESS;
   const double t_start = tracing() ? now_ms() : 0;
   const int nst = dev ? kTxStages : kPackStages;  // signed-tx chunks: more of them in flight
+  static const bool ec_alt = !(getenv("CORDAHIP_EC_ALTERNATE") && getenv("CORDAHIP_EC_ALTERNATE")[0] == '0');
+  const bool ec_alone = ec_alt && d.active.load() <= 1;  // no other call on the device as this one starts
   for (size_t k = 0; k < chunks.size() && e == hipSuccess && rc == CORDAHIP_SUCCESS; k++) {
     BatchStage& st = set.pb[k % nst];
     const double t0 = tracing() ? now_ms() : 0;
@@ -510,20 +512,29 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_ba
       e = e ? e : launch_store_to_host(st.d[4].p, st.h[4].p, ne, es);
     }
     e = e ? e : hipEventRecord(st.ed_done, es);
-    e = e ? e : hipStreamWaitEvent(d.s_ec, st.copied, 0);
+    // ECDSA sections: a generic batch alone on the device alternates its chunks
+    // between s_ec with workspace slot 0 and s_ec2 (the id-copy stream, idle in
+    // generic batches) with slot 1, so chunk k + 1's partition, prep and batch
+    // inversion run beside chunk k's ladders instead of after them; a call that
+    // starts beside another keeps s_ec and slot 0. c3h +1.2-1.4% at one call in
+    // flight, +1.3% at two (CORDAHIP_EC_ALTERNATE=0 turns it off;
+    // profiles/r06_ec_slots_ab/summary.json)
+    const int ecs = nc && ec_alone && !dev ? (int)(d.ec_turn.fetch_add(1) & 1) : 0;
+    hipStream_t xs = ecs && d.s_ec2 ? d.s_ec2 : d.s_ec;
+    e = e ? e : hipStreamWaitEvent(xs, st.copied, 0);
     if (dev && nc) {
-      e = e ? e : hipStreamWaitEvent(d.s_ec, ids_ready, 0);
-      e = e ? e : launch_gather_rows32(dev->txid, st.didx[1].as<uint32_t>(), nc, st.d[10].as<uint8_t>(), d.s_ec);
+      e = e ? e : hipStreamWaitEvent(xs, ids_ready, 0);
+      e = e ? e : launch_gather_rows32(dev->txid, st.didx[1].as<uint32_t>(), nc, st.d[10].as<uint8_t>(), xs);
     }
     if (nc && e == hipSuccess) {
-      std::lock_guard<std::mutex> ge(d.ec_mu);
+      std::lock_guard<std::mutex> ge(d.ec_mu[ecs]);
       e = ec_verify_enqueue(d, st.d[5].as<uint8_t>(), st.d[6].as<uint8_t>(), st.d[7].as<uint8_t>(),
                             st.d[8].as<uint8_t>(), st.d[9].as<uint8_t>(), st.d[10].as<uint8_t>(),
                             st.d[11].as<uint64_t>(), 0, nc, st.d[12].as<uint8_t>(), st.d[13].as<uint8_t>(), nullptr,
-                            b->flags, d.s_ec);
+                            b->flags, xs, ecs);
     }
-    if (nc) e = e ? e : launch_store_to_host(st.d[13].p, st.h[13].p, nc, d.s_ec);
-    e = e ? e : hipEventRecord(st.ec_done, d.s_ec);
+    if (nc) e = e ? e : launch_store_to_host(st.d[13].p, st.h[13].p, nc, xs);
+    e = e ? e : hipEventRecord(st.ec_done, xs);
     if (e == hipSuccess) {
       st.pending = true;
       st.a = a;
@@ -547,7 +558,8 @@ int sig_pipeline(cordahip_ctx* ctx, Device& d, TxSet& set, const cordahip_sig_ba
     set.pb[k].pending = false;
   }
   if (e != hipSuccess || rc != CORDAHIP_SUCCESS) {
-    for (hipStream_t x : {d.s_copy, d.s_ed, d.s_ed2, d.s_ec}) (void)hipStreamSynchronize(x);
+    for (hipStream_t x : {d.s_copy, d.s_ed, d.s_ed2, d.s_ec, d.s_ec2})  // s_ec2: the id-copy stream
+      if (x) (void)hipStreamSynchronize(x);
     for (BatchStage& st : set.pb)
       for (hipEvent_t ev : {st.copied, st.ed_done, st.ec_done}) (void)hipEventSynchronize(ev);
   }

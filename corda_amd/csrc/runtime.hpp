@@ -291,8 +291,12 @@ struct Device {
   uint32_t* btab = nullptr;
   uint32_t* gtab_k1 = nullptr;  // [k]G tables, k = 0..128, secp256k1 / P-256
   uint32_t* gtab_r1 = nullptr;
-  std::mutex ec_mu;
-  EcWork ec;
+  // ECDSA workspaces: slot 0 for the device path and the stream drain, slot 1 for the
+  // host pipelines' alternate chunks (capped at half of slot 0), each with its lock;
+  // ec_turn alternates the host chunks between them (s_ec / s_ec2)
+  std::mutex ec_mu[2];
+  EcWork ec[2];
+  std::atomic<uint32_t> ec_turn{0};
   hipStream_t stream = nullptr;  // context stream (init-time work and host tx paths)
   std::mutex tmu;
   TimedCall ring[kTimingRing];
@@ -328,6 +332,7 @@ struct Device {
   // serialise (with 6 stage streams C5 ran 90.6 M/s at 4 queues, 93.4 at 8).
   std::mutex streams_mu;
   hipStream_t s_copy = nullptr, s_ed = nullptr, s_ec = nullptr, s_ed2 = nullptr;
+  hipStream_t s_ec2 = nullptr;  // = s_idcopy: generic batches' alternate ECDSA chunks
   // signed-tx batches: the id slices' leaf-byte H2D on a stream of its own, so
   // slice j + 1's bytes cross PCIe while slice j hashes (d.stream)
   hipStream_t s_idcopy = nullptr;
@@ -483,11 +488,11 @@ hipError_t ed_verify_enqueue(Device& d, const uint8_t* keys, const uint8_t* sigs
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
                              unsigned long long* verdict, uint32_t flags, hipStream_t s, int slot = 0,
                              const std::function<hipError_t()>* before_msgs = nullptr);
-// d.ec_mu must be held
+// d.ec_mu[slot] must be held
 hipError_t ec_verify_enqueue(Device& d, const uint8_t* scheme, const uint8_t* keys, const uint8_t* key_len,
                              const uint8_t* sigs, const uint8_t* sig_len, const uint8_t* msgs, const uint64_t* msg_off,
                              uint32_t msg_len, uint64_t n, const uint8_t* pre, uint8_t* status,
-                             unsigned long long* verdict, uint32_t flags, hipStream_t s);
+                             unsigned long long* verdict, uint32_t flags, hipStream_t s, int slot = 0);
 void shard_range(uint64_t n, uint64_t nshards, uint64_t shard, uint64_t align, uint64_t& lo, uint64_t& hi);
 uint64_t env_lanes(const char* name, uint64_t dflt);
 
