@@ -1100,7 +1100,8 @@ def parse_args(argv=None):
                     help="c4: native leaves encoded on the GPU every step from the components in HBM "
                          "(cordahip_kryo_encode_device; implies --native-leaves)")
     ap.add_argument("--inflight", type=int, default=1,
-                    help="c4h, c2h, c3h: calls outstanding at once (consecutive batches overlap on the device)")
+                    help="c4h, c2h, c3h: calls outstanding at once (consecutive batches overlap on the device); "
+                         "give --warmup >= K so every transaction set has grown its stages before timing")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock sampling step")

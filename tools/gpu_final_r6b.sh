@@ -14,4 +14,5 @@ line() {
 line c4 --workload c4 && line c4h2 --workload c4h --inflight 2 --steps 40 --warmup 6 && \
 line c4hc2 --workload c4h --components --inflight 2 --steps 40 --warmup 6 && line c4de --workload c4 --device-encode && \
 line c1 --workload c1 && line c3 --workload c3 && line c5 --workload c5 && line c2h --workload c2h && \
-line c3h --workload c3h && line c4h --workload c4h && line c4hc --workload c4h --components
+line c3h --workload c3h && line c4h --workload c4h && line c4hc --workload c4h --components && \
+line c2h2 --workload c2h --inflight 2 --steps 8 --warmup 2 && line c3h2 --workload c3h --inflight 2 --steps 8 --warmup 2
