@@ -817,12 +817,23 @@ hipError_t tx_ids_enqueue(Device& d, TxSet& S, int set_idx, const cordahip_txid_
       const uint64_t n = ls1 - ls0;
       const cordahip_kryo_item* it = w.comp_items.as<cordahip_kryo_item>() + (ls0 - l0);
       uint8_t* cst = w.comp_status.as<uint8_t>() + (ls0 - l0);
-      e = e ? e : launch_kryo_shape(it, w.payload.as<uint8_t>(), cp->c->payload_len, n, cp->group[j],
-                                    d.kryo_fixed.as<uint8_t>(), slots, slots + n, d.kryo_sizes.as<uint64_t>(), cst, s,
-                                    true, (uint32_t)set_idx);
-      e = e ? e : launch_kryo_hash(it, w.payload.as<uint8_t>(), cp->c->payload_len, n, cp->group[j],
-                                   d.kryo_fixed.as<uint8_t>(), slots, d.kryo_sizes.as<uint64_t>(), cst,
-                                   w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
+      // shapes and hashes in one launch per slice (the shape pass inside kryo_hash's
+      // template-grouped blocks): c4h --components at two calls in flight 88.7-90.1 ->
+      // 91.3-92.1 M sig/s, alternating on one box (profiles/r06_kryo_fused_ab/);
+      // CORDAHIP_KRYO_FUSED=0: the two launches
+      static const bool fused = !(getenv("CORDAHIP_KRYO_FUSED") && getenv("CORDAHIP_KRYO_FUSED")[0] == '0');
+      if (fused) {
+        e = e ? e : launch_kryo_shape_hash(it, w.payload.as<uint8_t>(), cp->c->payload_len, n, cp->group[j],
+                                           d.kryo_fixed.as<uint8_t>(), cst, w.hashes.as<uint32_t>() + (ls0 - l0) * 8,
+                                           s, (uint32_t)set_idx);
+      } else {
+        e = e ? e : launch_kryo_shape(it, w.payload.as<uint8_t>(), cp->c->payload_len, n, cp->group[j],
+                                      d.kryo_fixed.as<uint8_t>(), slots, slots + n, d.kryo_sizes.as<uint64_t>(), cst, s,
+                                      true, (uint32_t)set_idx);
+        e = e ? e : launch_kryo_hash(it, w.payload.as<uint8_t>(), cp->c->payload_len, n, cp->group[j],
+                                     d.kryo_fixed.as<uint8_t>(), slots, d.kryo_sizes.as<uint64_t>(), cst,
+                                     w.hashes.as<uint32_t>() + (ls0 - l0) * 8, s);
+      }
     } else if (cp) {
       // the slice's leaves on the GPU (the template encoder) into the leaf buffer,
       // offsets relative to it, then their SHA-256; piece by piece (whole

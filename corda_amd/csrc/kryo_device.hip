@@ -314,6 +314,92 @@ __global__ void __launch_bounds__(1024) kryo_shape_kernel(ItemSrc items, uint64_
   status[i] = st;
 }
 
+// The templates-only shape pass for one lane, as kryo_shape_kernel decides it, in
+// a form every lane of a wave calls (no early return: the fused shape + hash
+// kernel synchronises its block afterwards). live: the lane holds item i. Out: the
+// item's slot (kRawSlot / a built template's slot / kNoSlot), its leaf size and its
+// status (0, 1 rejected, kKryoMiss); misses counted per wave.
+__device__ inline void shape_templates_only(const ItemSrc& items, uint64_t i, bool live,
+                                            unsigned long long* __restrict__ table,
+                                            const int32_t* __restrict__ slot_size,
+                                            const kryo::ShapeRec* __restrict__ rec, kryo::ShapeRec* srec_wave,
+                                            uint32_t* misses, uint32_t& slot_o, uint32_t& len_o, uint8_t& st_o) {
+  cordahip_kryo_item it{};
+  if (live) it = items[i];
+  uint64_t size = 0;
+  uint8_t st = 0;
+  uint32_t slot = kNoSlot;
+  bool miss = false;
+  const bool raw = live && it.kind == CORDAHIP_KRYO_RAW;
+  if (raw) {
+    slot = kRawSlot;
+    if (it.len && !it.data) {
+      st = 1;
+    } else if (it.len >> 29) {  // kryo_hash's 32-bit bit counts: the full chain takes it
+      slot = kNoSlot;
+      st = kKryoMiss;
+      miss = true;
+    } else {
+      size = it.len;
+    }
+  }
+  const bool part = live && !raw;
+  const uint64_t act = __ballot(part);
+  if (act) {
+    const int lead = __ffsll((unsigned long long)act) - 1;
+    const bool is_lead = (int)__lane_id() == lead;
+    bool claimed = false;
+    if (is_lead) {
+      uint64_t h = 0;
+      if (kryo::shape_hash_of(it, h)) slot = probe_slot(table, h, i, true, claimed);
+    }
+    const uint32_t s0 = (uint32_t)__shfl((int)slot, lead);
+    const int32_t z0 = s0 != kNoSlot ? slot_size[s0] : kUnbuilt;
+    const bool built0 = z0 != kUnbuilt && z0 != kNoTemplate;
+    bool done = false;
+    if (built0) {
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
+      const uint32_t nact = (uint32_t)__popcll(act);
+      constexpr uint32_t kQ = sizeof(kryo::ShapeRec) / 16;
+      if (part)
+        for (uint32_t q = rank; q < kQ; q += nact)
+          reinterpret_cast<uint4*>(srec_wave)[q] = reinterpret_cast<const uint4*>(rec + s0)[q];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (part && template_item(it, *srec_wave, z0, size, st)) {
+        slot = s0;
+        done = true;
+      } else if (part && is_lead) {
+        slot = kNoSlot;  // the slot's record is another shape (a hash collision)
+        done = true;
+      }
+    }
+    if (part && !done && !is_lead) {
+      uint64_t h = 0;
+      slot = kNoSlot;
+      if (kryo::shape_hash_of(it, h)) slot = probe_slot(table, h, i, true, claimed);
+    }
+    if (part && !done && slot != kNoSlot) {
+      const int32_t z = slot_size[slot];
+      if (z == kUnbuilt || !template_item(it, rec[slot], z, size, st)) slot = kNoSlot;
+    }
+    if (part && slot == kNoSlot) {
+      size = 0;
+      if (kryo::rejected_outright(it)) {
+        st = 1;
+      } else {
+        st = kKryoMiss;
+        miss = true;
+      }
+    }
+  }
+  wave_count(misses, miss);
+  slot_o = slot;
+  len_o = (uint32_t)size;
+  st_o = st;
+}
+
 // ---- 2. records and templates ----------------------------------------------------------
 // One wave per new shape: lane 0 records the representative's shape and traces
 // it (the level buffers in LDS) into the template's symbols; then the wave
@@ -935,7 +1021,19 @@ inline uint32_t hash_blocks(uint64_t n, uint32_t group) {
   return (uint32_t)((tiles + 7) / 8 * 8 * group);
 }
 
-template <int kMinWaves>
+// kFused (the host calls' templates-only chain): the block first runs the shape
+// pass for its own items (shape_templates_only), keeps slot, size and status in
+// LDS and stores only the status (merkle_root's BAD_COMPONENT input), so one launch
+// per id slice replaces kryo_shape + kryo_hash.
+struct FusedShape {
+  unsigned long long* table;
+  const int32_t* slot_size;
+  const kryo::ShapeRec* rec;
+  uint32_t* misses;
+  uint8_t* status_out;
+};
+
+template <int kMinWaves, bool kFused = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMinWaves, 8)))
 kryo_hash_kernel(ItemSrc items, uint64_t n, uint32_t group,
                                                          const uint32_t* __restrict__ item_slot,
@@ -943,7 +1041,8 @@ kryo_hash_kernel(ItemSrc items, uint64_t n, uint32_t group,
                                                          const uint32_t* __restrict__ arena,
                                                          const uint64_t* __restrict__ sizes,
                                                          const uint8_t* __restrict__ status,
-                                                         uint32_t* __restrict__ hashes /* [n][8] BE words */) {
+                                                         uint32_t* __restrict__ hashes /* [n][8] BE words */,
+                                                         FusedShape fs = {}) {
   kryo_priority();
   // The block's items grouped by template before any lane hashes: a wave whose
   // lanes hold leaves of one template assembles its blocks on the scalar path, one
@@ -957,7 +1056,22 @@ kryo_hash_kernel(ItemSrc items, uint64_t n, uint32_t group,
   __shared__ uint32_t s_min, s_cnt[4];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t i0 = hash_item_of(blockIdx.x, tid, n, group);
-  const uint32_t key = i0 >= n ? 0xffffffffu : status[i0] != 0 ? 0xfffffffeu : item_slot[i0];
+  __shared__ uint32_t f_slot[kFused ? 256 : 1], f_len[kFused ? 256 : 1];
+  __shared__ uint8_t f_st[kFused ? 256 : 1];
+  __shared__ kryo::ShapeRec f_rec[kFused ? 4 : 1];
+  uint32_t key;
+  if constexpr (kFused) {
+    uint32_t sl, ln;
+    uint8_t st0;
+    shape_templates_only(items, i0, i0 < n, fs.table, fs.slot_size, fs.rec, &f_rec[wv], fs.misses, sl, ln, st0);
+    f_slot[tid] = sl;
+    f_len[tid] = ln;
+    f_st[tid] = st0;
+    if (i0 < n) fs.status_out[i0] = st0;
+    key = i0 >= n ? 0xffffffffu : st0 != 0 ? 0xfffffffeu : sl;
+  } else {
+    key = i0 >= n ? 0xffffffffu : status[i0] != 0 ? 0xfffffffeu : item_slot[i0];
+  }
   bool placed = i0 >= n;
   uint32_t base = 0;
   for (int r = 0; r <= kGroups; r++) {
@@ -984,15 +1098,17 @@ kryo_hash_kernel(ItemSrc items, uint64_t n, uint32_t group,
     if (r < kGroups && cur == 0xffffffffu) break;  // every lane with an item placed
   }
   if (tid >= base) return;
-  const uint64_t i = hash_item_of(blockIdx.x, order[tid], n, group);
+  const uint32_t src = order[tid];
+  const uint64_t i = hash_item_of(blockIdx.x, src, n, group);
   HashSrc h;
   h.kind = 2;
-  if (status[i] == 0) {
+  const uint8_t sti = kFused ? f_st[src] : status[i];
+  if (sti == 0) {
     const cordahip_kryo_item it = items[i];
-    const uint32_t slot = item_slot[i];
+    const uint32_t slot = kFused ? f_slot[src] : item_slot[i];
     h.data = it.data;
     h.value = it.value;
-    h.len = (uint32_t)sizes[i];
+    h.len = kFused ? f_len[src] : (uint32_t)sizes[i];
     if (slot == kRawSlot) {
       h.kind = 1;
     } else if (slot != kNoSlot && !(slot & kDefer)) {
@@ -1221,6 +1337,22 @@ hipError_t launch_kryo_hash(const cordahip_kryo_item* d_items, const uint8_t* da
   else
     hipLaunchKernelGGL(kryo_hash_kernel<1>, grid, blk, 0, s, items, n, g, item_slot, k.slot_map, k.arena, sizes, status,
                        hashes);
+  return hipGetLastError();
+}
+
+// The host calls' templates-only chain in one launch per id slice: shapes and leaf
+// hashes (kryo_hash_kernel<5, true>); statuses into `status`, misses into set's counter.
+hipError_t launch_kryo_shape_hash(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
+                                  uint64_t n, uint32_t group, uint8_t* fixed, uint8_t* status, uint32_t* hashes,
+                                  hipStream_t s, uint32_t set) {
+  if (n == 0) return hipSuccess;
+  const ItemSrc items{d_items, data_base, data_len};
+  const KryoState k(fixed);
+  const uint32_t g = grouped(n, group) ? group : 1;
+  const FusedShape fs{k.table, k.slot_size, k.rec, k.counters + kCMiss + (set < 2 ? set : 2), status};
+  hipLaunchKernelGGL((kryo_hash_kernel<5, true>), dim3(hash_blocks(n, group)), dim3(256), 0, s, items, n, g,
+                     (const uint32_t*)nullptr, k.slot_map, k.arena, (const uint64_t*)nullptr, (const uint8_t*)nullptr,
+                     hashes, fs);
   return hipGetLastError();
 }
 

@@ -72,6 +72,9 @@ hipError_t launch_kryo_shape(const cordahip_kryo_item* items, const uint8_t* dat
                              uint8_t* status, hipStream_t s, bool templates_only, uint32_t set = 0);
 // SHA-256 of every item's leaf straight from its template (after a templates-only shape
 // pass): hashes[n][8] big-endian words, zero for items with a nonzero status
+hipError_t launch_kryo_shape_hash(const cordahip_kryo_item* d_items, const uint8_t* data_base, uint64_t data_len,
+                                  uint64_t n, uint32_t group, uint8_t* fixed, uint8_t* status, uint32_t* hashes,
+                                  hipStream_t s, uint32_t set);
 hipError_t launch_kryo_hash(const cordahip_kryo_item* items, const uint8_t* data_base, uint64_t data_len, uint64_t n,
                             uint32_t group, uint8_t* fixed, const uint32_t* item_slot, const uint64_t* sizes,
                             const uint8_t* status, uint32_t* hashes, hipStream_t s);
