@@ -1107,7 +1107,12 @@ def parse_args(argv=None):
     ap.add_argument("--no-clock", action="store_true", help="skip the shader-clock sampling step")
     ap.add_argument("--global-log2", type=int, default=None,
                     help="C5 only: strong scaling over a fixed 2^G global batch (SURVEY 8d C5: G = 28)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.inflight > 1 and args.warmup < args.inflight:
+        # with fewer warmup calls than calls in flight, a transaction set would grow its
+        # pinned stages (GBs of page-locked memory) inside the timed steps
+        ap.error("--inflight %d needs --warmup >= %d" % (args.inflight, args.inflight))
+    return args
 
 
 def main():
